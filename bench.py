@@ -1,0 +1,252 @@
+#!/usr/bin/env python
+"""bench.py — whole-job env-steps/s of the fused portfolio-env step on MI355X.
+
+One step = one launch of pmenv's fused step kernel over every env of the rank:
+price relatives from the close channel, action normalisation, portfolio value
+(f64), log-return reward, weight drift, and the one-day advance of the
+[B, N, W, F] observation window in place.
+
+Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
+assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
+Philox OHLC series and softmax actions already resident in HBM. Multi-GPU runs
+are weak-scaled (65,536 envs per rank, envs sharded by global id, no collective
+in the step) and launched one process per GPU:
+
+    python bench.py                                   # N = 1
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def step_bytes(N, W, F):
+    """Algorithmic HBM bytes per env-step: read the surviving window
+    N(W-1)F*4 + the new bar N(F-1)*4 + the action N*4, write the next window NWF*4,
+    value f64 read+write 16, reward 4  =  8*N*W*F + 20."""
+    return 8 * N * W * F + 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--assets", type=int, default=30)
+    ap.add_argument("--window", type=int, default=50)
+    ap.add_argument("--features", type=int, default=5)
+    ap.add_argument("--horizon", type=int, default=256, help="resident days of synthetic bars/actions (cycled)")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample-envs", type=int, default=4096)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="target CPU-seconds of oracle work")
+    ap.add_argument("--mae-envs", type=int, default=4096)
+    ap.add_argument("--mae-steps", type=int, default=64)
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
+    """Bounded sample on rank 0: (1) the CPU restatement (oracle, test infrastructure)
+    timed on the host cores; (2) reward MAE of the HIP path vs that CPU reference on
+    identical inputs (a fresh sample env, outside the timed region)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle import OracleEnv
+    from pmenv.config import EnvConfig
+
+    N, W, F = args.assets, args.window, args.features
+    S = min(args.mae_envs, args.envs_per_gpu)
+    T = args.mae_steps
+    ser = synth.series(W + T, S, N, env_offset=0, seed=args.seed, device=dev)
+    act = synth.actions(T, S, N, env_offset=0, seed=args.seed + 1, device=dev)
+    obs = synth.window_from_series(ser, W, F)
+    obs_h = obs.cpu().numpy().copy()
+    ser_h, act_h = ser.cpu().numpy(), act.cpu().numpy()
+    # HIP path on the sample
+    genv = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=dev)
+    genv.reset(obs)
+    g_r = []
+    for t in range(T):
+        r, _ = genv.step(act[t], obs, bar=ser[W + t])
+        g_r.append(r)
+    g_r = torch.stack(g_r).cpu().numpy().astype(np.float64)
+    g_v = genv.value.cpu().numpy()
+    # CPU restatement on the same inputs
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F))
+    cenv.reset(obs_h)
+    c_r = np.stack([cenv.step(act_h[t], obs_h, bar=ser_h[W + t], threads=threads)[0] for t in range(T)])
+    mae = float(np.mean(np.abs(g_r - c_r)))
+    max_rel_value = float(np.max(np.abs(g_v / cenv.value - 1.0)))
+    obs_equal = bool(np.array_equal(obs.cpu().numpy(), obs_h))
+
+    # timing: bounded sample of the same workload shape
+    Sc = min(args.cpu_sample_envs, S)
+    tenv = OracleEnv(EnvConfig(num_envs=Sc, num_assets=N, window=W, features=F))
+    tobs = np.ascontiguousarray(obs_h[:Sc])
+    tenv.reset(tobs)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        t = steps % T
+        tenv.step(np.ascontiguousarray(act_h[t, :Sc]), tobs, bar=np.ascontiguousarray(ser_h[W + t, :Sc]),
+                  threads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el * threads >= args.cpu_budget_s or el >= args.cpu_budget_s or steps >= 100000:
+            break
+    rate = Sc * steps / el
+    return {
+        "value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+        "sample": f"{Sc} envs x {steps} steps of the same N={N} W={W} F={F} fused step "
+                  f"(oracle/pmenv_oracle.c, OpenMP over envs) in {el:.2f} s on {cpu_model()}",
+    }, {"reward_mae": mae, "value_max_rel": max_rel_value, "obs_bit_exact": obs_equal,
+        "sample": f"{S} envs x {T} steps, HIP vs CPU restatement"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pmenv import TradingEnv, synth, _abi
+    lib = _abi.load()
+
+    B, N, W, F = args.envs_per_gpu, args.assets, args.window, args.features
+    lo = rank * B                                    # weak scaling: global env ids of this rank
+    H = max(1, min(args.horizon, args.steps + args.warmup))
+    series = synth.series(H + W, B, N, env_offset=lo, seed=args.seed, device=dev)      # [H+W, B, N, 4]
+    actions = synth.actions(H, B, N, env_offset=lo, seed=args.seed + 1, device=dev)     # [H, B, N]
+    obs = synth.window_from_series(series, W, F)                                         # [B, N, W, F]
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev)
+    env.reset(obs)
+    reward = torch.empty(B, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    h, op, rp = env._h, ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(reward.data_ptr())
+    bar_ptrs = [ctypes.c_void_p(series[W + t].data_ptr()) for t in range(H)]
+    act_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(H)]
+    step_fn = lib.pmenv_step
+
+    def one_step(i):
+        t = i % H
+        rc = step_fn(h, act_ptrs[t], None, bar_ptrs[t], op, rp, sp)
+        if rc != 0:
+            _abi.check(rc, h, "pmenv_step")
+
+    for i in range(args.warmup):
+        one_step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        one_step(args.warmup + i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_avg_s = float(t[0]), float(t[1])
+    nonfinite = env.nonfinite_count()
+
+    total_env_steps = world * B * args.steps
+    value = total_env_steps / elapsed
+    bstep = step_bytes(N, W, F)
+    achieved = bstep * B / kern_avg_s / 1e9
+    traffic = None
+    try:
+        pmc = json.load(open(args.pmc_file))
+        if pmc.get("workload") == [B, N, W, F]:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    cpu = mae = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu, mae = cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv)
+
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node) at 65k envs x 30 assets; reward MAE vs CPU ref",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Philox OHLC random walk + softmax actions, resident in HBM)",
+            "config": {
+                "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels",
+                "envs_per_gpu": B, "global_envs": world * B, "assets": N, "window": W, "features": F,
+                "reward": "log_returns", "commission": 0.0, "obs_dtype": "f32", "accumulate": "f64",
+                "parallelism": f"env-sharded x{world} (no collective in the step)",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "step_advance_kernel<true>", "kernel_avg_us": kern_avg_s * 1e6,
+                "bytes_per_env_step": bstep,
+            },
+            "cpu_baseline": cpu,
+            "reward_mae": None if mae is None else mae["reward_mae"],
+            "parity_sample": mae,
+            "nonfinite_envs": nonfinite,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

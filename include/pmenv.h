@@ -1,0 +1,202 @@
+/*
+ * pmenv.h — C ABI of the MI355X-native vectorised portfolio environment.
+ *
+ * This is the drop-in boundary for the hot path of zachramsey/pm-rl:
+ *   env/sim/trading_env.py   (TradingEnv.__init__ :8-18, reset :21-41, step :44-105)
+ *   env/sim/weight_buffer.py (ActionBuffer :5-51 — the W x N weight ring)
+ *   env/reward.py            (Reward :6-31 — returns / log_returns / sharpe_ratio)
+ *   data/instrument.py:79    (price relatives y_t = close_t / close_{t-1})
+ *   data/instrument.py:339-356 (sliding window; fused here as an in-place window advance)
+ *
+ * The reference is a single-env Python class driven from train/on_policy.py:59-67;
+ * here B lockstep envs share one handle and one HIP kernel launch per step.
+ *
+ * Conventions
+ *   - every entry point returns 0 (PMENV_OK) or a negative pmenv_status;
+ *     pmenv_last_error(h) then holds a message.
+ *   - every data pointer passed to reset/step is a DEVICE pointer owned by the
+ *     caller (e.g. a torch tensor's data_ptr()); env state is owned by the handle.
+ *   - layouts are dense row-major: obs [B, N, W, F] fp32, action [B, N] fp32,
+ *     prices [B, N] fp32, bar [B, N, F-1] fp32, reward [B] fp32.
+ *   - one handle belongs to one device; calls on a handle are not thread-safe;
+ *     reset/step enqueue on `stream` and never synchronise the host, allocate,
+ *     or free (they are hipGraph-capturable).
+ */
+#ifndef PMENV_H
+#define PMENV_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMENV_ABI_VERSION 1
+
+/* Opaque HIP stream (identical to HIP's own typedef); NULL = default stream. */
+typedef struct ihipStream_t* hipStream_t;
+
+typedef struct pmenv pmenv; /* opaque handle */
+
+typedef enum pmenv_status {
+    PMENV_OK = 0,
+    PMENV_ERR_ARG = -1,    /* bad config value or NULL where a pointer is required */
+    PMENV_ERR_SHAPE = -2,  /* shape mismatch; weight_buffer.py:18-19 raises ValueError */
+    PMENV_ERR_HIP = -3,    /* a HIP runtime call failed */
+    PMENV_ERR_ALIGN = -4   /* pointer not 4-byte aligned */
+} pmenv_status;
+
+/* Reward kinds. The reference step() hard-codes log_returns (trading_env.py:99);
+ * REWARD switch at trading_env.py:93-98 is commented out; env/reward.py:15-31
+ * restates returns/log_returns/sharpe_ratio; differential Sharpe is absent from
+ * the reference (north star addition, parity unpinned by the reference). */
+typedef enum pmenv_reward_kind {
+    PMENV_REWARD_LOG_RETURN = 0,  /* r = log(ret) * scale           trading_env.py:99 */
+    PMENV_REWARD_RETURN = 1,      /* r = ret * scale                reward.py:20-21   */
+    PMENV_REWARD_SHARPE = 2,      /* (mean(ret_1..t) - rf) / std(ret_1..t, ddof=1) * scale, reward.py:26-31 (NaN while t < 2, as numpy) */
+    PMENV_REWARD_DIFF_SHARPE = 3  /* Moody-Saffell differential Sharpe on R = ret - 1, EMA rate eta */
+} pmenv_reward_kind;
+
+/* Action normalisation predicate (trading_env.py:58 vs agent/pg/pg.py:52). */
+typedef enum pmenv_norm_mode {
+    PMENV_NORM_AND = 0, /* reference env: normalise iff !isclose(sum,1) AND min<0; exp(w)/sum(exp(w)) */
+    PMENV_NORM_OR = 1   /* batched trainer: normalise iff !isclose(sum,1) OR min<0; softmax */
+} pmenv_norm_mode;
+
+/* Weight-history channel order once the ring has wrapped (weight_buffer.py:38-44). */
+typedef enum pmenv_ring_mode {
+    PMENV_RING_STORAGE = 0, /* reference: ring returned in storage order after wrap */
+    PMENV_RING_CHRONO = 1   /* intended: oldest..newest always */
+} pmenv_ring_mode;
+
+/* Which value the return uses (trading_env.py:75,88). */
+typedef enum pmenv_ret_mode {
+    PMENV_RET_GROSS = 0, /* reference: ret = value / (mu * V_prev), i.e. excludes commission */
+    PMENV_RET_NET = 1    /* ret = value / V_prev, includes commission */
+} pmenv_ret_mode;
+
+typedef struct pmenv_cfg {
+    int32_t num_envs;       /* B */
+    int32_t num_assets;     /* N  (config/base.py:29 NUM_ASSETS) — asset 0 is cash */
+    int32_t window;         /* W  (config/base.py:28 WINDOW_SIZE) */
+    int32_t features;       /* F  (last channel F-1 carries the weight history, trading_env.py:103) */
+    int32_t close_channel;  /* channel of the close price in obs / bar (price relatives) */
+    int32_t reward_kind;    /* pmenv_reward_kind */
+    int32_t norm_mode;      /* pmenv_norm_mode */
+    int32_t ring_mode;      /* pmenv_ring_mode */
+    int32_t ret_mode;       /* pmenv_ret_mode */
+    int32_t mu_max_iter;    /* cap on the commission fixed point (trading_env.py:70 has none) */
+    double init_cash;       /* config/base.py:47 INITIAL_CASH = 25000 */
+    double commission;      /* config/base.py:48 COMISSION = 0.0 */
+    double reward_scale;    /* config/base.py:52 REWARD_SCALE = 1 */
+    double risk_free_rate;  /* config/base.py:53 RISK_FREE_RATE = 0.04 (sharpe_ratio only) */
+    double sharpe_eta;      /* EMA rate of the differential Sharpe reward */
+    double mu_tol;          /* fixed-point tolerance, trading_env.py:70 uses 1e-10 */
+} pmenv_cfg;
+
+/* Fills cfg with the reference defaults for the given shapes
+ * (close_channel = 3 for [open, high, low, close, weight] when F >= 5, else 0). */
+void pmenv_cfg_default(pmenv_cfg* cfg, int32_t num_envs, int32_t num_assets,
+                       int32_t window, int32_t features);
+
+int32_t pmenv_abi_version(void);
+
+/* Allocates per-env state on `device` (value f64, update counter, W x N weight
+ * ring, reward-statistic pair) and puts every env in the reset state.
+ * Replaces TradingEnv.__init__ (trading_env.py:8-18) + ActionBuffer.__init__ (weight_buffer.py:6-11). */
+int pmenv_create(const pmenv_cfg* cfg, int device, pmenv** out);
+/* Same, with the state living in caller-provided device memory of at least
+ * pmenv_state_bytes_for(cfg) bytes, 16-B aligned (e.g. a torch uint8 tensor, so
+ * the host wrapper gets zero-copy views); the handle never frees it. */
+size_t pmenv_state_bytes_for(const pmenv_cfg* cfg);
+int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_bytes, pmenv** out);
+/* Byte offsets of the state fields inside the state blob:
+ * [0] value f64[B], [1] stat_a f64[B], [2] stat_b f64[B], [3] counter i32[B],
+ * [4] ring f32[B,W,N], [5] nonfinite u64. */
+int pmenv_state_layout(const pmenv_cfg* cfg, size_t offsets[6]);
+int pmenv_destroy(pmenv* h);
+const char* pmenv_last_error(const pmenv* h);
+int pmenv_get_cfg(const pmenv* h, pmenv_cfg* out);
+
+/* TradingEnv.reset (trading_env.py:21-41): value <- init_cash, ring <- e0, and
+ * obs[:, :, :, F-1] <- get_all() (weight_buffer.py:32-44) in place.
+ * mask [B] (uint8, device) selects which envs reset; NULL resets all.
+ * obs may be NULL (state-only reset). */
+int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream);
+
+/* Optional per-step outputs (the reference's info dict, trading_env.py:80,85,90,100). */
+typedef struct pmenv_step_args {
+    const float* action;   /* [B, N]  target weights (raw policy output)            */
+    const float* prices;   /* [B, N]  price relatives y_t, or NULL (needs bar)       */
+    const float* bar;      /* [B, N, F-1] new day's market channels, or NULL          */
+    float* obs;            /* [B, N, W, F] in/out                                     */
+    float* reward;         /* [B] out, may be NULL                                    */
+    double* ret;           /* [B] out (info["returns"]), may be NULL                  */
+    float* weights;        /* [B, N] out post-drift weights (info["actions"]), may be NULL */
+} pmenv_step_args;
+
+/* TradingEnv.step (trading_env.py:44-105) for all B envs in one kernel.
+ *  - bar == NULL  ("surface" mode, the reference's own contract): obs is the
+ *    caller's next-day window; only channel F-1 is rewritten from the ring.
+ *    prices must be given.
+ *  - bar != NULL  ("advance" mode, the north-star fused path): obs is the
+ *    env-owned window returned by the previous reset/step; it is advanced one
+ *    day in place (instrument.py:339-356 sliding window), the bar is appended
+ *    at t = W-1, and if prices == NULL the relatives are
+ *    bar[close] / obs[W-1, close] (instrument.py:79).
+ * Portfolio value (f64, env-owned) is readable through pmenv_value(). */
+int pmenv_step_ex(pmenv* h, const pmenv_step_args* args, hipStream_t stream);
+int pmenv_step(pmenv* h, const float* action, const float* prices, const float* bar,
+               float* obs, float* reward, hipStream_t stream);
+
+/* Device pointer to the env-owned portfolio values [B] f64 (TradingEnv.value). */
+double* pmenv_value(pmenv* h);
+/* Device pointer to the weight ring [B, W, N] f32 (ActionBuffer.buffer) and
+ * update counters [B] i32 (ActionBuffer.idx = (1 + k) % W, is_full = k >= W-1). */
+float* pmenv_ring(pmenv* h);
+int32_t* pmenv_counter(pmenv* h);
+
+/* Checkpoint: the whole env state as one opaque device blob. */
+size_t pmenv_state_bytes(const pmenv* h);
+int pmenv_get_state(pmenv* h, void* dst_device, hipStream_t stream);
+int pmenv_set_state(pmenv* h, const void* src_device, hipStream_t stream);
+
+/* Count of envs whose reward or value came out non-finite since create
+ * (synchronises `stream`). */
+int pmenv_nonfinite_count(pmenv* h, uint64_t* out, hipStream_t stream);
+
+/* ---- synthetic data path (Philox4x32-10, key = seed) ---- */
+
+/* OHLC random walk: series [T, B, Fm=4 ... ] written as [T][B][N][4] =
+ * [open, high, low, close]; env ids are env_offset .. env_offset+B-1 so a
+ * sharded run generates exactly the slice of the unsharded series. */
+int pmenv_synth_series(float* series, int32_t T, int32_t B, int32_t N,
+                       int64_t env_offset, uint64_t seed, float sigma, hipStream_t stream);
+/* Softmax-of-N(0,1) simplex actions [T][B][N]. */
+int pmenv_synth_actions(float* actions, int32_t T, int32_t B, int32_t N,
+                        int64_t env_offset, uint64_t seed, hipStream_t stream);
+/* obs[b, n, t, f] = series[t, b, n, f] for t < W, f < 4; channel F-1 left for reset. F must be 5. */
+int pmenv_window_init(float* obs, const float* series, int32_t B, int32_t N,
+                      int32_t W, int32_t F, hipStream_t stream);
+
+/* ---- rollout returns (north star: replay/rollout_buffer.py's GAE / discounted
+ * return pass as a device scan; the reference stores (s,a,v,r) but computes no
+ * returns, rollout_buffer.py:43-57) ---- */
+
+/* adv[t,b] = delta_t + gamma*lambda*(1-done[t,b])*adv[t+1,b],
+ * delta_t = r[t,b] + gamma*(1-done[t,b])*v[t+1,b] - v[t,b];  ret = adv + v.
+ * rewards/dones [T,B], values [T+1,B]; dones may be NULL. */
+int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones,
+              float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam,
+              hipStream_t stream);
+
+/* Per-rank advantage moments {count, sum, sum of squares} in f64 into out[3]
+ * (the only cross-GPU exchange: a 24-byte all-reduce over xGMI). */
+int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PMENV_H */

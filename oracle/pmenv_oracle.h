@@ -1,0 +1,60 @@
+/*
+ * pmenv_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C CPU restatement of the reference env step (zachramsey/pm-rl
+ * env/sim/trading_env.py, env/sim/weight_buffer.py, env/reward.py) used as
+ * the parity checker for the HIP path and as bench.py's cpu_baseline leg.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may load it;
+ * the product path (pm-rl_amd/) never links or calls it.
+ *
+ * Pinned against golden vectors produced by the reference Python itself
+ * (tests/golden/gen_golden.py -> tests/golden/<case>.npz, checked by
+ * tests/test_oracle_golden.py). Commission > 0 and the differential Sharpe
+ * reward have no runnable reference (trading_env.py:72 raises TypeError;
+ * differential Sharpe is absent): those branches are "parity unpinned by the
+ * reference" and rest on this restatement alone.
+ */
+#ifndef PMENV_ORACLE_H
+#define PMENV_ORACLE_H
+
+#include <stdint.h>
+#include "../include/pmenv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_env {
+    pmenv_cfg cfg;
+    double* value;   /* [B] */
+    int32_t* k;      /* [B] updates since reset */
+    float* ring;     /* [B, W, N] */
+    double* sa;      /* [B] Sharpe running mean | diff-Sharpe A */
+    double* sb;      /* [B] Sharpe running M2   | diff-Sharpe B */
+} or_env;
+
+or_env* or_create(const pmenv_cfg* cfg);
+void or_destroy(or_env* e);
+void or_reset(or_env* e, float* obs, const uint8_t* mask);
+void or_step(or_env* e, const float* action, const float* prices, const float* bar,
+             float* obs, float* reward, double* ret, float* weights);
+/* same as or_step but runs envs with `threads` OpenMP threads (<=0: runtime default) */
+void or_step_mt(or_env* e, const float* action, const float* prices, const float* bar,
+                float* obs, float* reward, double* ret, float* weights, int threads);
+
+void or_gae(const float* rewards, const float* values, const uint8_t* dones,
+            float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam);
+void or_moments(const float* x, int64_t n, double* out);
+
+/* Philox4x32-10 and the synthetic generators (restating pmenv.hip's device code). */
+void or_philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                   uint32_t k0, uint32_t k1, uint32_t out[4]);
+void or_synth_series(float* series, int32_t T, int32_t B, int32_t N,
+                     int64_t env_offset, uint64_t seed, float sigma);
+void or_synth_actions(float* actions, int32_t T, int32_t B, int32_t N,
+                      int64_t env_offset, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,60 @@
+"""Build the in-tree native libraries.
+
+    python pm-rl_amd/build.py            # libpmenv.so (HIP, gfx950) + oracle/liboracle.so
+
+libpmenv.so is the product (the C ABI of include/pmenv.h). oracle/liboracle.so is
+the CPU parity checker (test infrastructure). Both are built in place so they
+travel with the repository snapshot to the GPU box.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "pmenv", "libpmenv.so")
+SRC = os.path.join(HERE, "csrc", "pmenv.hip")
+ORACLE_SRC = os.path.join(ROOT, "oracle", "pmenv_oracle.c")
+ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PMENV_ARCH", "gfx950")
+
+
+def _stale(out, *srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _run(cmd):
+    print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_pmenv(force=False):
+    hdr = os.path.join(ROOT, "include", "pmenv.h")
+    if not force and not _stale(LIB, SRC, hdr, __file__):
+        return LIB
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+          "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+          "-o", LIB, SRC])
+    return LIB
+
+
+def build_oracle(force=False):
+    hdrs = [os.path.join(ROOT, "oracle", "pmenv_oracle.h"), os.path.join(ROOT, "include", "pmenv.h")]
+    if not force and not _stale(ORACLE_LIB, ORACLE_SRC, *hdrs):
+        return ORACLE_LIB
+    _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-fopenmp", "-Wall", "-Wextra",
+          "-Wno-unused-parameter", "-o", ORACLE_LIB, ORACLE_SRC, "-lm"])
+    return ORACLE_LIB
+
+
+def build_all(force=False):
+    build_pmenv(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

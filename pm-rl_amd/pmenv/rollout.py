@@ -1,0 +1,43 @@
+"""Rollout returns on device.
+
+The reference's replay/rollout_buffer.py stores (s, a, v, r) per day (:43-57) and
+computes no returns; the north star asks for its GAE / discounted-return pass as
+a device kernel. pmenv_gae walks each env's column of a time-major [T, B] rollout
+backwards (one thread per env, coalesced across envs).
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def gae(rewards, values, dones=None, gamma=0.99, lam=0.95):
+    """rewards [T, B], values [T+1, B] (bootstrap row last), dones [T, B] bool.
+    Returns (advantages, returns), each [T, B] float32."""
+    lib = _abi.load()
+    T, B = rewards.shape
+    if tuple(values.shape) != (T + 1, B):
+        raise ValueError(f"values must be [T+1, B] = {(T + 1, B)}, got {tuple(values.shape)}")
+    r = rewards.to(torch.float32).contiguous()
+    v = values.to(torch.float32).contiguous()
+    d = dones.to(torch.uint8).contiguous() if dones is not None else None
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+    _abi.check(lib.pmenv_gae(_p(r), _p(v), _p(d), _p(adv), _p(ret), T, B, gamma, lam, s), None, "pmenv_gae")
+    return adv, ret
+
+
+def moments(x):
+    """{count, sum, sum of squares} of x in f64 (device tensor [3])."""
+    lib = _abi.load()
+    x = x.to(torch.float32).contiguous().reshape(-1)
+    out = torch.empty(3, dtype=torch.float64, device=x.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    _abi.check(lib.pmenv_moments(_p(x), x.numel(), _p(out), s), None, "pmenv_moments")
+    return out

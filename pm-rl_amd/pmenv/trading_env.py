@@ -1,0 +1,258 @@
+"""TradingEnv — batched, device-resident drop-in for the reference env.
+
+Mirrors zachramsey/pm-rl env/sim/trading_env.py (`TradingEnv`, :7-115) call for
+call, with a leading batch dimension B of lockstep envs:
+
+    reference                                  here
+    TradingEnv()                      :8-18    TradingEnv(num_envs=B, num_assets=N, window=W)
+    reset(features) -> features       :21-41   reset(features[, mask]) -> features  (in place)
+    step(action, features, prices)    :44-105  step(action, features, prices) -> (r, features)
+      -> (r, features)                         step(action, features, bar=bar)  (fused window advance)
+    .value                            :9,89    .value  (f64 [B], device view)
+    .weights (ActionBuffer)           :10      .weights (RingView: get_last / get_all)
+    .info values/actions/rewards/returns       .info (opt-in, track_info=True)
+
+Every compute call goes through libpmenv.so (include/pmenv.h); there is no CPU
+path. `features` must be a float32, contiguous tensor on the env's device: it is
+written in place and returned, exactly as trading_env.py:32,103 mutate the
+caller's tensor.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+from .config import EnvConfig
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class RingView:
+    """Read-only view of the device weight ring with ActionBuffer's accessors
+    (env/sim/weight_buffer.py:28-44); for inspection and tests, not the hot path."""
+
+    def __init__(self, env):
+        self._env = env
+
+    @property
+    def buffer(self):                      # [B, W, N] (weight_buffer.py:8)
+        return self._env._ring
+
+    @property
+    def idx(self):                         # [B] (weight_buffer.py:10,22)
+        return (1 + self._env._counter.long()) % self._env.cfg.window
+
+    @property
+    def is_full(self):                     # [B] (weight_buffer.py:11,25-26)
+        return self._env._counter.long() >= self._env.cfg.window - 1
+
+    def get_last(self):                    # [B, N] (weight_buffer.py:28-30)
+        W = self._env.cfg.window
+        k = self._env._counter.long() % W
+        return self._env._ring[torch.arange(k.numel(), device=k.device), k]
+
+    def get_all(self):                     # [B, N, W] (weight_buffer.py:32-44)
+        cfg = self._env.cfg
+        W = cfg.window
+        ring = self._env._ring                                     # [B, W, N]
+        B = ring.shape[0]
+        idx = self.idx.view(B, 1)
+        t = torch.arange(W, device=ring.device).view(1, W)
+        pad = W - idx
+        pre = t - pad                                               # not full: zero pad then ring[:idx]
+        if cfg.ring == "storage":
+            full_slot = t.expand(B, W)
+        else:
+            full_slot = (idx + t) % W
+        slot = torch.where(self.is_full.view(B, 1), full_slot, pre.clamp(min=0))
+        vals = torch.gather(ring, 1, slot.unsqueeze(-1).expand(B, W, ring.shape[2]))
+        vals = torch.where((~self.is_full.view(B, 1, 1)) & (pre.unsqueeze(-1) < 0), torch.zeros_like(vals), vals)
+        return vals.transpose(1, 2)
+
+
+class TradingEnv:
+    def __init__(self, num_envs=1, num_assets=None, window=None, features=5, device=None,
+                 config=None, track_info=False, **overrides):
+        if config is None:
+            kw = dict(num_envs=num_envs, features=features)
+            if num_assets is not None:
+                kw["num_assets"] = num_assets
+            if window is not None:
+                kw["window"] = window
+            kw.update(overrides)
+            config = EnvConfig(**kw)
+        self.cfg = config.validate()
+        self._lib = _abi.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("pmenv runs on a GPU device only (no CPU fallback)")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self._c = self.cfg.to_c()
+        nbytes = self._lib.pmenv_state_bytes_for(ctypes.byref(self._c))
+        if nbytes == 0:
+            raise ValueError("invalid env shape")
+        off = (ctypes.c_size_t * 6)()
+        _abi.check(self._lib.pmenv_state_layout(ctypes.byref(self._c), off), None, "pmenv_state_layout")
+        self._state = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        h = ctypes.c_void_p()
+        torch.cuda.synchronize(self.device)
+        _abi.check(self._lib.pmenv_create_in(ctypes.byref(self._c), self.device.index, _ptr(self._state),
+                                             nbytes, ctypes.byref(h)), None, "pmenv_create_in")
+        self._h = h
+        B, N, W = self.cfg.num_envs, self.cfg.num_assets, self.cfg.window
+        s = self._state
+        self._value = s[off[0]:off[0] + 8 * B].view(torch.float64)
+        self._stat_a = s[off[1]:off[1] + 8 * B].view(torch.float64)
+        self._stat_b = s[off[2]:off[2] + 8 * B].view(torch.float64)
+        self._counter = s[off[3]:off[3] + 4 * B].view(torch.int32)
+        self._ring = s[off[4]:off[4] + 4 * B * W * N].view(torch.float32).view(B, W, N)
+        self._nonfinite = s[off[5]:off[5] + 8].view(torch.int64)
+        self.weights = RingView(self)
+        self.track_info = track_info
+        self._unbatched = False
+        self.info = None
+        self._reset_info()
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _reset_info(self):
+        if not self.track_info:
+            self.info = None
+            return
+        B, N = self.cfg.num_envs, self.cfg.num_assets
+        e0 = torch.zeros(B, N, device=self.device)
+        e0[:, 0] = 1
+        # trading_env.py:13-18 / :34-39 (dict order is relied on by util/plot.py:61)
+        self.info = {"values": [self._value.clone()], "actions": [e0], "rewards": [torch.zeros(B, device=self.device)],
+                     "returns": [torch.zeros(B, device=self.device, dtype=torch.float64)]}
+
+    def _obs_check(self, features, name="features"):
+        cfg = self.cfg
+        shape = (cfg.num_envs, cfg.num_assets, cfg.window, cfg.features)
+        if features.dtype != torch.float32 or not features.is_contiguous() or features.device != self.device:
+            raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device} (written in place)")
+        if tuple(features.shape) == shape:
+            return False
+        if cfg.num_envs == 1 and tuple(features.shape) == shape[1:]:
+            return True
+        raise ValueError(f"{name} must have shape {shape} (or {shape[1:]} when num_envs == 1), "
+                         f"got {tuple(features.shape)}")
+
+    def _vec(self, x, per_env, name):
+        """Coerce an action / prices tensor to a contiguous float32 [B, per_env]."""
+        B = self.cfg.num_envs
+        if not torch.is_tensor(x):
+            x = torch.as_tensor(x)
+        if x.numel() != B * per_env:
+            # weight_buffer.py:18-19 raises ValueError on a mis-shaped action
+            raise ValueError(f"{name} must have {B} x {per_env} elements, got shape {tuple(x.shape)}")
+        return x.to(device=self.device, dtype=torch.float32).reshape(B, per_env).contiguous()
+
+    # ------------------------------------------------------------------ API
+    @property
+    def value(self):
+        """Portfolio value (trading_env.py:9,89) — f64 [B] view of the device state."""
+        return self._value[0] if self._unbatched else self._value
+
+    @property
+    def num_envs(self):
+        return self.cfg.num_envs
+
+    def reset(self, features=None, mask=None):
+        """trading_env.py:21-41 for all envs (or the envs where mask is True)."""
+        unb = False
+        if features is not None:
+            unb = self._obs_check(features)
+            self._unbatched = unb
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).reshape(-1).to(torch.uint8).contiguous()
+            if m.numel() != self.cfg.num_envs:
+                raise ValueError("mask must have num_envs elements")
+        _abi.check(self._lib.pmenv_reset(self._h, _ptr(features), _ptr(m), self._stream()), self._h, "pmenv_reset")
+        if mask is None:
+            self._reset_info()
+        return features
+
+    def step(self, action, features, prices=None, bar=None):
+        """trading_env.py:44-105 for all B envs in one kernel launch.
+
+        prices given, bar None : the reference contract — `features` is the next
+                                 day's window; channel F-1 is rewritten in place.
+        bar given              : fused path — `features` (the window returned by
+                                 the previous reset/step) is advanced one day in
+                                 place and `bar` [B, N, F-1] appended; prices
+                                 default to bar.close / window[W-1].close.
+        Returns (r, features); r is f32 [B] (0-dim for unbatched single-env input).
+        """
+        cfg = self.cfg
+        B, N = cfg.num_envs, cfg.num_assets
+        unb = self._obs_check(features)
+        a = self._vec(action, N, "action")
+        p = self._vec(prices, N, "prices") if prices is not None else None
+        br = None
+        if bar is not None:
+            br = self._vec(bar, N * (cfg.features - 1), "bar")
+        elif p is None:
+            raise ValueError("step needs prices (reference contract) or bar (fused window advance)")
+        r = torch.empty(B, dtype=torch.float32, device=self.device)
+        args = _abi.PmenvStepArgs()
+        args.action = a.data_ptr()
+        args.prices = p.data_ptr() if p is not None else None
+        args.bar = br.data_ptr() if br is not None else None
+        args.obs = features.data_ptr()
+        args.reward = r.data_ptr()
+        ret = w = None
+        if self.track_info:
+            ret = torch.empty(B, dtype=torch.float64, device=self.device)
+            w = torch.empty(B, N, dtype=torch.float32, device=self.device)
+            args.ret = ret.data_ptr()
+            args.weights = w.data_ptr()
+        _abi.check(self._lib.pmenv_step_ex(self._h, ctypes.byref(args), self._stream()), self._h, "pmenv_step")
+        if self.track_info:
+            # trading_env.py:80,85,90,100
+            self.info["values"].append(self._value.clone())
+            self.info["actions"].append(w)
+            self.info["returns"].append(ret)
+            self.info["rewards"].append(r)
+        self._unbatched = unb
+        return (r[0] if unb else r), features
+
+    def advance(self, action, features, bar, prices=None):
+        """Fused step: window advance + bar append (see step)."""
+        return self.step(action, features, prices=prices, bar=bar)
+
+    # ------------------------------------------------------------------ state
+    def state_dict(self):
+        """Checkpoint (value, reward statistics, counters, ring) as one tensor."""
+        return {"state": self._state.clone(), "cfg": self.cfg.as_dict()}
+
+    def load_state_dict(self, sd):
+        st = sd["state"]
+        if st.numel() != self._state.numel():
+            raise ValueError("state blob size mismatch (different env shape)")
+        self._state.copy_(st.to(self.device))
+
+    def nonfinite_count(self):
+        return int(self._nonfinite.item())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self._lib.pmenv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                self._lib.pmenv_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass

@@ -1,0 +1,204 @@
+"""Generate golden vectors by running the REFERENCE env (zachramsey/pm-rl) itself.
+
+Run in the build container only (it reads /root/reference at run time; nothing it
+reads is copied into this repository — the outputs are data):
+
+    python tests/golden/gen_golden.py            # writes tests/golden/*.npz
+
+Loader notes:
+  * config constants bind at import (weight_buffer.py:1, trading_env.py:1), so
+    config.base.WINDOW_SIZE / NUM_ASSETS are patched before each (re)import;
+  * env/sim/trading_env.py:115 is a PEP 701 f-string inside the dead
+    `log_info` method that Python 3.10 cannot compile; the source text is read,
+    that one line is replaced by `pass`, and the module is compiled under its
+    original filename. reset()/step() are untouched;
+  * fp64 goldens use torch.set_default_dtype(torch.float64) before the env is
+    built, so the ring and every step op run in f64.
+
+Data alignment follows the reference's intended loop (train/on_policy.py:59-67 with
+data/instrument.py:79 and :339-356): at loop index i the env gets
+window_i = series[:, i:i+W] and prices_i = fl32(close[i+W-1] / close[i+W-2]).
+"""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the read-only reference
+REF = os.environ.get("PMRL_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_reference(W, N, commission=0.0):
+    import torch  # noqa: F401
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import config.base as cb
+    cb.WINDOW_SIZE, cb.NUM_ASSETS, cb.COMISSION = W, N, commission
+    for m in ["env.sim.weight_buffer", "env.reward", "env.sim.trading_env"]:
+        sys.modules.pop(m, None)
+    import env.sim.weight_buffer  # noqa: F401  (binds W, N)
+    import env.reward  # noqa: F401
+    path = os.path.join(REF, "env/sim/trading_env.py")
+    lines = open(path).read().split("\n")
+    assert "self.info[" in lines[114] and lines[114].lstrip().startswith("f.write(f"), lines[114]
+    indent = lines[114][: len(lines[114]) - len(lines[114].lstrip())]
+    lines[114] = indent + "pass"
+    mod = types.ModuleType("env.sim.trading_env")
+    mod.__file__ = path
+    exec(compile("\n".join(lines), path, "exec"), mod.__dict__)
+    sys.modules["env.sim.trading_env"] = mod
+    return mod.TradingEnv
+
+
+def make_series(rng, N, D, F=5, sigma=0.01):
+    """OHLC random walk [N, D, F] fp32; channel F-1 is a zero placeholder that
+    trading_env.py:103 overwrites with the weight history."""
+    z = rng.standard_normal((N, D + 1, 4))
+    close = np.empty((N, D + 1))
+    close[:, 0] = 100.0 * np.exp(0.2 * rng.standard_normal(N))
+    for d in range(1, D + 1):
+        close[:, d] = close[:, d - 1] * np.exp(sigma * z[:, d, 0])
+    prev = close[:, :-1]
+    c = close[:, 1:]
+    o = prev * np.exp(0.3 * sigma * z[:, 1:, 1])
+    h = np.maximum(o, c) * np.exp(np.abs(0.5 * sigma * z[:, 1:, 2]))
+    lo = np.minimum(o, c) * np.exp(-np.abs(0.5 * sigma * z[:, 1:, 3]))
+    s = np.zeros((N, D, F), np.float32)
+    s[:, :, 0], s[:, :, 1], s[:, :, 2], s[:, :, 3] = o, h, lo, c
+    return s
+
+
+def make_actions(rng, kind, T, N):
+    a = np.zeros((T + 1, N), np.float32)
+    for i in range(1, T + 1):
+        if kind == "simplex":
+            z = rng.standard_normal(N).astype(np.float32)
+            e = np.exp(z - z.max())
+            a[i] = (e / e.sum()).astype(np.float32)
+        elif kind == "mixed":
+            a[i] = rng.standard_normal(N).astype(np.float32)
+        elif kind == "rawpos":
+            a[i] = rng.uniform(0.0, 1.0, N).astype(np.float32)
+        elif kind == "negsum1":
+            m = rng.integers(-4, 9, N)
+            m[1] = -abs(m[1]) - 1                     # at least one negative
+            m[0] = 8 - m[1:].sum()                    # sum exactly 8
+            a[i] = (m / 8.0).astype(np.float32)       # sum exactly 1, exactly representable
+        else:
+            raise ValueError(kind)
+    return a
+
+
+def run_case(name, N, W, T, dtype, kind, resets=(), chan_steps=None, seed=0):
+    import torch
+    torch.set_default_dtype(torch.float64 if dtype == "f64" else torch.float32)
+    tdt = torch.get_default_dtype()
+    TradingEnv = load_reference(W, N)
+    rng = np.random.default_rng(seed)
+    F = 5
+    series = make_series(rng, N, T + W, F)
+    actions = make_actions(rng, kind, T, N)
+    # instrument.py:79 divides float32 close tensors, so the relatives the env sees
+    # are fp32-rounded even when the env itself runs in f64
+    close = series[:, :, 3]
+    prices = np.zeros((T + 1, N), np.float64 if dtype == "f64" else np.float32)
+    for i in range(1, T + 1):
+        prices[i] = (close[:, i + W - 1] / close[:, i + W - 2]).astype(np.float32)
+    ops = np.zeros(T + 1, np.int8)
+    ops[0] = 1
+    for r in resets:
+        ops[r] = 1
+    if chan_steps is None:
+        chan_steps = list(range(T + 1))
+    chan_steps = sorted(set(chan_steps))
+
+    env = TradingEnv()
+    rewards = np.full(T + 1, np.nan)
+    values = np.zeros(T + 1)
+    rets = np.full(T + 1, np.nan)
+    wpost = np.full((T + 1, N), np.nan)
+    chans = []
+    for i in range(T + 1):
+        window = torch.tensor(series[:, i:i + W, :], dtype=tdt)
+        if ops[i]:
+            obs = env.reset(window)
+        else:
+            a = torch.tensor(actions[i], dtype=tdt).reshape(N, 1)      # agent emits [N, 1]
+            p = torch.tensor(prices[i], dtype=tdt)
+            r, obs = env.step(a, window, p)
+            rewards[i] = float(r)
+            rets[i] = float(env.info["returns"][-1])
+            wpost[i] = np.asarray(env.info["actions"][-1], np.float64)
+        values[i] = float(env.value)
+        if i in chan_steps:
+            chans.append(obs[:, :, -1].numpy().astype(np.float64))
+        # market channels are returned untouched (in-place write of channel F-1 only)
+        assert np.array_equal(obs[:, :, :-1].numpy().astype(np.float32), series[:, i:i + W, :-1])
+    meta = dict(name=name, N=N, W=W, F=F, T=T, dtype=dtype, kind=kind, resets=list(resets),
+                seed=seed, reference="zachramsey/pm-rl @ 2025-03-04 env/sim/trading_env.py",
+                torch=torch.__version__)
+    np.savez_compressed(
+        os.path.join(OUT, name + ".npz"), meta=np.array(json.dumps(meta)), series=series,
+        actions=actions, prices=prices, ops=ops, rewards=rewards, values=values, rets=rets,
+        wpost=wpost, chan_steps=np.array(chan_steps, np.int32), chans=np.array(chans))
+    return meta
+
+
+def reward_module_vectors():
+    """env/reward.py:15-31 on fixed value histories (the class is dead code in
+    step(), but it defines the returns / log_returns / sharpe_ratio semantics)."""
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import config.base as cb
+    sys.modules.pop("env.reward", None)
+    import env.reward as rw
+    rng = np.random.default_rng(7)
+    out = {}
+    for L in (2, 3, 10, 64):
+        vals = [25000.0]
+        for _ in range(L - 1):
+            vals.append(vals[-1] * float(1.0 + 0.01 * rng.standard_normal()))
+        fake = types.SimpleNamespace(info={"values": vals})
+        R = rw.Reward(fake)
+        out[f"values_{L}"] = np.array(vals)
+        out[f"returns_{L}"] = np.array(R.returns())
+        out[f"log_returns_{L}"] = np.array(R.log_returns())
+        with np.errstate(all="ignore"):
+            out[f"sharpe_{L}"] = np.array(R.sharpe_ratio())
+    out["risk_free_rate"] = np.array(cb.RISK_FREE_RATE)
+    np.savez_compressed(os.path.join(OUT, "reward_module.npz"), **out)
+
+
+CASES = [
+    # name, N, W, T, dtype, kind, resets, chan_steps
+    ("simplex_n5_w50_t64_f64", 5, 50, 64, "f64", "simplex", (), None),
+    ("simplex_n5_w50_t64_f32", 5, 50, 64, "f32", "simplex", (), None),
+    ("simplex_n30_w50_t256_f64", 30, 50, 256, "f64", "simplex", (), [0, 1, 2, 47, 48, 49, 50, 51, 100, 255, 256]),
+    ("simplex_n30_w50_t256_f32", 30, 50, 256, "f32", "simplex", (), [0, 1, 2, 48, 49, 50, 51, 256]),
+    ("mixed_n30_w50_t64_f64", 30, 50, 64, "f64", "mixed", (), [0, 1, 49, 50, 64]),
+    ("mixed_n30_w50_t64_f32", 30, 50, 64, "f32", "mixed", (), [0, 1, 49, 50, 64]),
+    ("rawpos_n30_w50_t48_f64", 30, 50, 48, "f64", "rawpos", (), [0, 1, 48]),
+    ("rawpos_n30_w50_t48_f32", 30, 50, 48, "f32", "rawpos", (), [0, 1, 48]),
+    ("negsum1_n5_w8_t24_f64", 5, 8, 24, "f64", "negsum1", (), None),
+    ("negsum1_n5_w8_t24_f32", 5, 8, 24, "f32", "negsum1", (), None),
+    ("wrap_n5_w8_t40_f64", 5, 8, 40, "f64", "simplex", (), None),
+    ("wrap_n5_w4_t12_f32", 5, 4, 12, "f32", "simplex", (), None),
+    ("reset_n5_w8_t40_f64", 5, 8, 40, "f64", "simplex", (13, 29), None),
+    ("reset_n7_w6_t30_f32", 7, 6, 30, "f32", "mixed", (5, 6, 20), None),
+    ("simplex_n129_w50_t16_f64", 129, 50, 16, "f64", "simplex", (), [0, 1, 16]),
+]
+
+
+def main():
+    for i, (name, N, W, T, dt, kind, resets, cs) in enumerate(CASES):
+        m = run_case(name, N, W, T, dt, kind, resets, cs, seed=1000 + i)
+        print("wrote", m["name"])
+    reward_module_vectors()
+    print("wrote reward_module")
+
+
+if __name__ == "__main__":
+    main()

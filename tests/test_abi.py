@@ -1,0 +1,98 @@
+"""The C-ABI library loads and exports exactly what include/pmenv.h declares
+(no compute calls: this runs on CPU-only hosts)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pmenv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pmenv_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pmenv import _abi
+    lib = _abi.load()
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"libpmenv.so lacks {n}"
+    bound = {s[0] for s in _abi.SIGNATURES}
+    assert set(names) == bound, f"ctypes binding drift: {set(names) ^ bound}"
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\b(pmenv_[a-z_]+)\b", out))
+    assert exported == set(names), f"exported but undeclared / declared but missing: {exported ^ set(names)}"
+
+
+def test_library_is_gfx950_code_object():
+    from pmenv import _abi
+    blob = open(_abi.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_and_cfg_defaults_match_reference_config():
+    from pmenv import _abi
+    lib = _abi.load()
+    assert lib.pmenv_abi_version() == _abi.PMENV_ABI_VERSION
+    c = _abi.PmenvCfg()
+    lib.pmenv_cfg_default(ctypes.byref(c), 7, 30, 50, 5)
+    assert (c.num_envs, c.num_assets, c.window, c.features, c.close_channel) == (7, 30, 50, 5, 3)
+    # config/base.py:47-53
+    assert c.init_cash == 25000 and c.commission == 0.0 and c.reward_scale == 1.0
+    assert c.risk_free_rate == 0.04 and c.reward_kind == 0
+    assert c.norm_mode == 0 and c.ring_mode == 0 and c.ret_mode == 0 and c.mu_tol == 1e-10
+    assert ctypes.sizeof(_abi.PmenvCfg) == 88
+
+
+def test_state_layout_is_consistent():
+    from pmenv import _abi
+    from pmenv.config import EnvConfig
+    lib = _abi.load()
+    for B, N, W in [(1, 5, 50), (4096, 30, 50), (3, 7, 6)]:
+        c = EnvConfig(num_envs=B, num_assets=N, window=W).to_c()
+        off = (ctypes.c_size_t * 6)()
+        assert lib.pmenv_state_layout(ctypes.byref(c), off) == 0
+        up = lambda x: (x + 15) // 16 * 16  # noqa: E731
+        assert list(off)[:4] == [0, up(8 * B), 2 * up(8 * B), 3 * up(8 * B)]
+        assert all(o % 16 == 0 for o in off)
+        assert off[5] - off[4] >= 4 * B * W * N
+        assert lib.pmenv_state_bytes_for(ctypes.byref(c)) == off[5] + 16
+
+
+def test_create_rejects_bad_config_without_touching_the_gpu():
+    from pmenv import _abi
+    lib = _abi.load()
+    c = _abi.PmenvCfg()
+    lib.pmenv_cfg_default(ctypes.byref(c), 4, 30, 50, 5)
+    c.close_channel = 4                     # the weight channel is not a price
+    h = ctypes.c_void_p()
+    assert lib.pmenv_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
+    assert b"close_channel" in lib.pmenv_last_error(None)
+    c.close_channel = 3
+    c.window = 4000                         # W*F beyond the LDS tile
+    assert lib.pmenv_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
+    assert not h.value
+
+
+def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
+    from pmenv import _abi
+    monkeypatch.setattr(_abi, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_abi, "_lib", None)
+    with pytest.raises(ImportError):
+        _abi.load()
+
+
+def test_product_does_not_reference_the_oracle():
+    pkg = os.path.join(ROOT, "pm-rl_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")) and f != "build.py":
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in txt.lower(), f"{f} references the oracle"

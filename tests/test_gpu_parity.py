@@ -1,0 +1,318 @@
+"""HIP path (libpmenv.so through the C ABI) vs the reference's golden vectors and
+vs the CPU oracle; full-size properties at BASELINE sizes. Needs an MI355X."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+from test_oracle_golden import compare
+from oracle import OracleEnv, gae as or_gae, moments as or_moments, synth_series, synth_actions
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(DEV)
+
+
+def _t(x, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
+
+
+def replay_gpu(g, mode):
+    from pmenv import TradingEnv
+    m = g["meta"]
+    N, W, F, T = m["N"], m["W"], m["F"], m["T"]
+    env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True)
+    out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
+           "wpost": np.full((T + 1, N), np.nan), "chans": {}, "market_ok": True}
+    obs = None
+    for i in range(T + 1):
+        if g["ops"][i]:
+            obs = _t(gu.window(g, i)[0])             # unbatched [N, W, F] like the reference
+            env.reset(obs)
+        else:
+            if mode == "surface":
+                obs = _t(gu.window(g, i)[0])
+                r, obs2 = env.step(_t(g["actions"][i]).reshape(N, 1), obs, _t(g["prices"][i]))
+            else:
+                r, obs2 = env.step(_t(g["actions"][i]).reshape(N, 1), obs, bar=_t(gu.bar(g, i)))
+                out["market_ok"] &= np.array_equal(obs[..., :-1].cpu().numpy(), gu.window(g, i)[0, ..., :-1])
+            assert obs2 is obs and r.dim() == 0
+            out["rewards"][i] = float(r)
+            out["rets"][i] = float(env.info["returns"][-1][0])
+            out["wpost"][i] = env.info["actions"][-1][0].cpu().numpy()
+        out["values"][i] = float(env.value)
+        out["chans"][i] = obs[:, :, -1].cpu().numpy()
+    return out
+
+
+@pytest.mark.parametrize("name", gu.cases())
+@pytest.mark.parametrize("mode", ["surface", "advance"])
+def test_gpu_matches_reference_goldens(name, mode):
+    g = gu.load(name)
+    out = replay_gpu(g, mode)
+    assert out["market_ok"]
+    compare(g, out)
+
+
+def _run_both(cfg_kw, B, N, W, T, kind="simplex", seed=0, F=5, resets=None, mode="advance"):
+    """Drive pmenv and the oracle side by side on identical inputs."""
+    from pmenv import TradingEnv
+    from pmenv.config import EnvConfig
+    rng = np.random.default_rng(seed)
+    Fm = F - 1
+    closes = 100 * np.exp(np.cumsum(0.01 * rng.standard_normal((W + T, B, N)), axis=0))
+    ser = np.empty((W + T, B, N, Fm), np.float32)
+    for f in range(Fm):
+        ser[..., f] = closes * np.exp(0.002 * rng.standard_normal(closes.shape))
+    ser[..., cfg_kw.get("close_channel", min(3, Fm - 1))] = closes
+    obs0 = np.zeros((B, N, W, F), np.float32)
+    obs0[..., :Fm] = ser[:W].transpose(1, 2, 0, 3)
+    if kind == "simplex":
+        z = rng.standard_normal((T, B, N))
+        act = np.exp(z) / np.exp(z).sum(-1, keepdims=True)
+    elif kind == "mixed":
+        act = rng.standard_normal((T, B, N))
+    else:
+        act = rng.uniform(0, 1, (T, B, N)) / N * 2
+    act = act.astype(np.float32)
+    cfg = EnvConfig(num_envs=B, num_assets=N, window=W, features=F, **cfg_kw)
+    genv = TradingEnv(config=cfg, device=DEV, track_info=True)
+    cenv = OracleEnv(cfg)
+    gobs = _t(obs0)
+    cobs = obs0.copy()
+    genv.reset(gobs)
+    cenv.reset(cobs)
+    for t in range(T):
+        if resets is not None and t in resets:
+            mask = resets[t]
+            genv.reset(gobs, mask=_t(mask, torch.bool))
+            cenv.reset(cobs, mask=mask)
+        y = None
+        if mode == "surface":
+            y = (ser[W + t, ..., cfg.close_channel] / ser[W + t - 1, ..., cfg.close_channel]).astype(np.float32)
+            win = np.zeros_like(cobs)
+            win[..., :Fm] = ser[t + 1:t + 1 + W].transpose(1, 2, 0, 3)
+            cobs[...] = win
+            gobs.copy_(_t(win))
+            gr, _ = genv.step(_t(act[t]), gobs, prices=_t(y))
+            cr, cret, cw = cenv.step(act[t], cobs, prices=y)
+        else:
+            gr, _ = genv.step(_t(act[t]), gobs, bar=_t(ser[W + t]))
+            cr, cret, cw = cenv.step(act[t], cobs, bar=ser[W + t])
+        g_r = gr.cpu().numpy()
+        both_nan = np.isnan(g_r) & np.isnan(cr)
+        err = np.where(both_nan, 0, np.abs(g_r.astype(np.float64) - cr))
+        tol = 1e-6 * np.abs(cr) + 1e-9
+        assert np.all(err <= tol), f"step {t}: reward err {np.nanmax(err):.3e}"
+        np.testing.assert_allclose(genv.info["returns"][-1].cpu().numpy(), cret, rtol=1e-12)
+        gv = genv.value.cpu().numpy()
+        np.testing.assert_allclose(gv, cenv.value, rtol=1e-12)
+        np.testing.assert_allclose(genv.info["actions"][-1].cpu().numpy(), cw, rtol=2e-7, atol=1e-12)
+        go = gobs.cpu().numpy()
+        assert np.array_equal(go[..., :Fm], cobs[..., :Fm]), f"market channels differ at step {t}"
+        np.testing.assert_allclose(go[..., Fm], cobs[..., Fm], rtol=2e-7, atol=1e-12)
+    assert np.array_equal(genv._counter.cpu().numpy(), cenv.k)
+    np.testing.assert_allclose(genv._ring.cpu().numpy(), cenv.ring, rtol=2e-7, atol=1e-12)
+    np.testing.assert_allclose(genv._stat_a.cpu().numpy(), cenv.stat_a, rtol=1e-9, atol=1e-14)
+    return genv, cenv
+
+
+MODES = [
+    dict(),
+    dict(ring="chrono"),
+    dict(reward="returns"),
+    dict(reward="sharpe_ratio"),
+    dict(reward="diff_sharpe", sharpe_eta=0.05),
+    dict(commission=0.0025),
+    dict(commission=0.01, ret="net", reward="diff_sharpe"),
+    dict(norm="or"),
+    dict(reward_scale=100.0, init_cash=1e6),
+]
+
+
+@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+@pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])
+def test_gpu_vs_oracle_modes(kw, kind):
+    _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"{kw}{kind}".encode()))
+
+
+@pytest.mark.parametrize("mode", ["surface", "advance"])
+def test_gpu_vs_oracle_surface_and_advance(mode):
+    _run_both({}, B=33, N=30, W=12, T=30, kind="mixed", mode=mode, seed=3)
+
+
+@pytest.mark.parametrize("N,W,F,B", [
+    (129, 50, 5, 9),      # multi-tile: 129 rows > one 32 KiB LDS tile
+    (500, 50, 5, 4),      # config 5 asset count (S&P 500)
+    (5, 50, 5, 7),        # env block 1250 floats: not 16-B granular -> scalar path
+    (64, 16, 5, 5), (65, 16, 5, 5),   # wave-width edges of the per-asset loop
+    (7, 6, 3, 11),        # F = 3 (two market channels)
+    (3, 1, 5, 4),         # W = 1: the ring is "full" from the first update
+    (1, 4, 2, 3),         # single asset, single market channel
+])
+def test_gpu_vs_oracle_shapes(N, W, F, B):
+    kw = {} if F == 5 else {"close_channel": F - 2}
+    _run_both(kw, B=B, N=N, W=W, T=2 * W + 3, kind="mixed", F=F, seed=N * 1000 + W)
+
+
+def test_gpu_masked_reset_mid_run():
+    B = 20
+    rng = np.random.default_rng(5)
+    resets = {7: rng.random(B) < 0.3, 15: rng.random(B) < 0.5, 16: np.ones(B, bool)}
+    _run_both({}, B=B, N=9, W=8, T=30, kind="simplex", resets=resets)
+
+
+def test_gpu_state_roundtrip():
+    from pmenv import TradingEnv
+    B, N, W = 16, 10, 8
+    ser = torch.rand(W + 40, B, N, 4, device=DEV) + 1.0
+    act = torch.softmax(torch.randn(40, B, N, device=DEV), -1)
+    obs = torch.zeros(B, N, W, 5, device=DEV)
+    obs[..., :4] = ser[:W].permute(1, 2, 0, 3)
+    e1 = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, reward="diff_sharpe")
+    e1.reset(obs)
+    for t in range(13):
+        e1.step(act[t], obs, bar=ser[W + t])
+    sd = e1.state_dict()
+    obs_ck = obs.clone()
+    r1 = [e1.step(act[t], obs, bar=ser[W + t])[0].clone() for t in range(13, 40)]
+    e2 = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, reward="diff_sharpe")
+    e2.load_state_dict(sd)
+    r2 = [e2.step(act[t], obs_ck, bar=ser[W + t])[0].clone() for t in range(13, 40)]
+    assert all(torch.equal(a, b) for a, b in zip(r1, r2))
+    assert torch.equal(obs, obs_ck) and torch.equal(e1.value, e2.value)
+
+
+def test_gpu_full_size_properties():
+    """BASELINE config (65,536 envs x 30 assets x 50 x 5) through past the ring wrap:
+    market channels are exactly the sliding window of the series, the reward is
+    log(sum w*y) with y the fp32 close relative, the value compounds the returns,
+    and the weight channel is the ring in the reference's storage order."""
+    from pmenv import TradingEnv, synth
+    B, N, W, F, T = 65536, 30, 50, 5, 60
+    ser = synth.series(W + T, B, N, seed=11, device=DEV)
+    act = synth.actions(T, B, N, seed=12, device=DEV)
+    obs = synth.window_from_series(ser, W, F)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV)
+    env.reset(obs)
+    logv = torch.full((B,), float(np.log(25000.0)), dtype=torch.float64, device=DEV)
+    for t in range(T):
+        r, _ = env.step(act[t], obs, bar=ser[W + t])
+        y = (ser[W + t, ..., 3] / ser[W + t - 1, ..., 3]).double()
+        ref = torch.log((act[t].double() * y).sum(-1))
+        err = (r.double() - ref).abs()
+        assert bool((err <= 1e-6 * ref.abs() + 1e-8).all()), f"step {t}: {float(err.max()):.3e}"
+        logv += ref
+    assert torch.equal(obs[..., :4], ser[T:T + W].permute(1, 2, 0, 3))
+    assert torch.allclose(env.value.log(), logv, rtol=0, atol=1e-9)
+    chan = obs[..., 4]                                          # [B, N, W]
+    assert torch.equal(chan, env.weights.get_all())
+    assert bool(env.weights.is_full.all())
+    assert torch.allclose(chan.sum(1), torch.ones_like(chan.sum(1)), atol=1e-5)   # simplex per day
+    assert env.nonfinite_count() == 0
+    # a sample of envs against the oracle on the same inputs, from a fresh reset
+    S = 64
+    sub = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=DEV)
+    sobs = synth.window_from_series(ser[:, :S].contiguous(), W, F)
+    from pmenv.config import EnvConfig
+    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F))
+    cobs = sobs.cpu().numpy().copy()
+    sub.reset(sobs)
+    cenv.reset(cobs)
+    ser_h, act_h = ser[:, :S].cpu().numpy(), act[:, :S].cpu().numpy()
+    for t in range(T):
+        gr, _ = sub.step(act[t, :S].contiguous(), sobs, bar=ser[W + t, :S].contiguous())
+        cr, _, _ = cenv.step(act_h[t], cobs, bar=ser_h[W + t])
+        assert np.all(np.abs(gr.cpu().numpy() - cr) <= 1e-6 * np.abs(cr) + 1e-9)
+    assert np.array_equal(sobs.cpu().numpy(), cobs)
+
+
+def test_gpu_synth_matches_oracle():
+    from pmenv import synth
+    s = synth.series(20, 9, 7, env_offset=5, seed=3, device=DEV).cpu().numpy()
+    np.testing.assert_allclose(s, synth_series(20, 9, 7, env_offset=5, seed=3), rtol=1e-6)
+    a = synth.actions(6, 9, 7, env_offset=5, seed=4, device=DEV).cpu().numpy()
+    np.testing.assert_allclose(a, synth_actions(6, 9, 7, env_offset=5, seed=4), rtol=1e-6)
+
+
+def test_gpu_gae_and_moments_match_oracle():
+    from pmenv import rollout
+    rng = np.random.default_rng(1)
+    T, B = 64, 1000
+    r = rng.standard_normal((T, B)).astype(np.float32)
+    v = rng.standard_normal((T + 1, B)).astype(np.float32)
+    d = rng.random((T, B)) < 0.05
+    adv, ret = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
+    oadv, oret = or_gae(r, v, d, 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-6, atol=1e-6)
+    x = rng.standard_normal(1_000_003).astype(np.float32)
+    m = rollout.moments(_t(x)).cpu().numpy()
+    om = or_moments(x)
+    assert m[0] == om[0]
+    np.testing.assert_allclose(m[1:], om[1:], rtol=1e-9)
+
+
+def test_gpu_errors_mirror_reference():
+    from pmenv import TradingEnv
+    env = TradingEnv(num_envs=2, num_assets=5, window=8, device=DEV)
+    obs = torch.zeros(2, 5, 8, 5, device=DEV)
+    env.reset(obs)
+    with pytest.raises(ValueError):               # weight_buffer.py:18-19
+        env.step(torch.ones(2, 4, device=DEV), obs, torch.ones(2, 5, device=DEV))
+    with pytest.raises(ValueError):
+        env.step(torch.ones(2, 5, device=DEV), obs)
+    with pytest.raises(ValueError):
+        env.step(torch.ones(2, 5, device=DEV), obs.double(), torch.ones(2, 5, device=DEV))
+
+
+def test_gpu_nonfinite_counter():
+    from pmenv import TradingEnv
+    env = TradingEnv(num_envs=3, num_assets=4, window=4, device=DEV)
+    obs = torch.ones(3, 4, 4, 5, device=DEV)
+    env.reset(obs)
+    a = torch.full((3, 4), 0.25, device=DEV)
+    a[1, 2] = float("nan")
+    env.step(a, obs, torch.ones(3, 4, device=DEV))
+    assert env.nonfinite_count() == 1
+
+
+def test_gpu_step_is_graph_capturable():
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 256, 30, 50, 8
+    ser = synth.series(W + T, B, N, device=DEV)
+    act = synth.actions(T, B, N, device=DEV)
+    obs_a = synth.window_from_series(ser, W)
+    obs_b = obs_a.clone()
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    torch.cuda.synchronize()
+    from pmenv import _abi
+    import ctypes
+    lib = _abi.load()
+    rew = torch.empty(T, B, device=DEV)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for t in range(T):
+            _abi.check(lib.pmenv_step(eb._h, ctypes.c_void_p(act[t].data_ptr()), None,
+                                      ctypes.c_void_p(ser[W + t].data_ptr()), ctypes.c_void_p(obs_b.data_ptr()),
+                                      ctypes.c_void_p(rew[t].data_ptr()), s), eb._h)
+    eb.reset(obs_b)            # capture does not execute; start both from reset
+    obs_b.copy_(synth.window_from_series(ser, W))
+    eb.reset(obs_b)
+    g.replay()
+    ref = torch.stack([ea.step(act[t], obs_a, bar=ser[W + t])[0] for t in range(T)])
+    torch.cuda.synchronize()
+    assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)

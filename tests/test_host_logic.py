@@ -1,0 +1,43 @@
+"""Host-side logic that needs no GPU: config validation, sharding, the wrapper's
+shape checks, and the bench's algorithmic byte model."""
+import pytest
+
+from pmenv.config import EnvConfig
+from pmenv.parallel import shard_range
+
+
+def test_config_validation():
+    EnvConfig(num_envs=4, num_assets=30, window=50).validate()
+    with pytest.raises(ValueError):
+        EnvConfig(reward="sharpe").validate()
+    with pytest.raises(ValueError):
+        EnvConfig(close_channel=4, features=5).validate()
+    with pytest.raises(ValueError):
+        EnvConfig(commission=1.5).validate()
+    with pytest.raises(ValueError):
+        EnvConfig(num_envs=0).validate()
+    c = EnvConfig(reward="diff_sharpe", ring="chrono", norm="or", ret="net").to_c()
+    assert (c.reward_kind, c.ring_mode, c.norm_mode, c.ret_mode) == (3, 1, 1, 1)
+
+
+@pytest.mark.parametrize("G,world", [(65536, 8), (10, 3), (7, 8), (1, 1)])
+def test_shard_range_partitions(G, world):
+    spans = [shard_range(G, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == G
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c and a <= b
+    assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_bench_byte_model():
+    import bench
+    # B_step = 8*N*W*F + 20
+    assert bench.step_bytes(30, 50, 5) == 60020
+    assert bench.step_bytes(500, 50, 5) == 1000020
+    assert bench.step_bytes(5, 50, 5) == 10020
+
+
+def test_wrapper_refuses_cpu_device():
+    from pmenv import TradingEnv
+    with pytest.raises(ValueError):
+        TradingEnv(num_envs=2, num_assets=5, window=8, device="cpu")
