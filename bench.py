@@ -1,16 +1,20 @@
 #!/usr/bin/env python
 """bench.py — whole-job env-steps/s of the fused portfolio-env step on MI355X.
 
-One step = one launch of pmenv's fused step kernel over every env of the rank:
+One step = one pass of pmenv's fused env step over every env of the rank:
 price relatives from the close channel, action normalisation, portfolio value
 (f64), log-return reward, weight drift, and the one-day advance of the
-[B, N, W, F] observation window in place.
+[B, N, W, F] observation window.
 
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
 assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
-Philox OHLC series and softmax actions already resident in HBM. Multi-GPU runs
-are weak-scaled (65,536 envs per rank, envs sharded by global id, no collective
-in the step) and launched one process per GPU:
+Philox OHLC series and softmax actions already resident in HBM. The step runs as
+two launches (scalar_step_kernel, then the streaming advance_rows_kernel); the
+window is double-buffered by default (each day's window is a fresh buffer, as the
+reference's data path hands the env a new window every day — instrument.py:339-356),
+and the in-place advance is timed as well and reported under "inplace".
+Multi-GPU runs are weak-scaled (65,536 envs per rank, envs sharded by global id,
+no collective in the step) and launched one process per GPU:
 
     python bench.py                                   # N = 1
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -56,6 +60,8 @@ def parse():
     ap.add_argument("--mae-envs", type=int, default=4096)
     ap.add_argument("--mae-steps", type=int, default=64)
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--windows", choices=["double", "inplace"], default="double")
+    ap.add_argument("--inplace-steps", type=int, default=50, help="extra timed in-place steps (0: skip)")
     return ap.parse_args()
 
 
@@ -155,40 +161,70 @@ def main():
     obs = synth.window_from_series(series, W, F)                                         # [B, N, W, F]
     env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev)
     env.reset(obs)
+    obs_b = torch.empty_like(obs) if args.windows == "double" else None
     reward = torch.empty(B, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
-    h, op, rp = env._h, ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(reward.data_ptr())
-    bar_ptrs = [ctypes.c_void_p(series[W + t].data_ptr()) for t in range(H)]
-    act_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(H)]
-    step_fn = lib.pmenv_step
+    h = env._h
+    bar_ptrs = [series[W + t].data_ptr() for t in range(H)]
+    act_ptrs = [actions[t].data_ptr() for t in range(H)]
+    step_fn = lib.pmenv_step_ex
+    args_s = _abi.PmenvStepArgs()
+    args_s.reward = reward.data_ptr()
+    args_a = _abi.PmenvStepArgs()
+    args_a.reward = reward.data_ptr()
+    ping = [obs, obs_b]
 
-    def one_step(i):
+    def one_step(i, double, phase_events=None):
         t = i % H
-        rc = step_fn(h, act_ptrs[t], None, bar_ptrs[t], op, rp, sp)
+        src, dst = (ping[i % 2], ping[(i + 1) % 2]) if double else (obs, None)
+        for a in (args_s, args_a):
+            a.action, a.bar = act_ptrs[t], bar_ptrs[t]
+            a.obs = src.data_ptr()
+            a.obs_out = dst.data_ptr() if dst is not None else None
+        if phase_events is None:
+            args_s.phases = 0
+            rc = step_fn(h, ctypes.byref(args_s), sp)
+        else:
+            # same two launches as phases=0, with an event between them so the
+            # streaming kernel is timed on its own stream
+            args_s.phases, args_a.phases = _abi.PHASE_SCALAR, _abi.PHASE_ADVANCE
+            rc = step_fn(h, ctypes.byref(args_s), sp)
+            phase_events[0].record(stream)
+            rc = rc or step_fn(h, ctypes.byref(args_a), sp)
+            phase_events[1].record(stream)
         if rc != 0:
-            _abi.check(rc, h, "pmenv_step")
+            _abi.check(rc, h, "pmenv_step_ex")
 
-    for i in range(args.warmup):
-        one_step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    def timed(steps, warmup, double):
+        for i in range(warmup):
+            one_step(i, double)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            one_step(warmup + i, double, ev[i])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        k_ms = [a.elapsed_time(b) for a, b in ev]
+        return el, sum(k_ms) / len(k_ms) / 1e3
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        one_step(args.warmup + i)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    double = args.windows == "double"
+    elapsed, kern_avg_s = timed(args.steps, args.warmup, double)
+    inplace = None
+    if double and args.inplace_steps > 0:
+        # continue from the latest window, advancing it in place
+        if (args.warmup + args.steps) % 2:
+            obs.copy_(obs_b)
+        ip_el, ip_k = timed(args.inplace_steps, 2, False)
+        inplace = {"env_steps_per_s_per_gpu": B * args.inplace_steps / ip_el,
+                   "ms_per_step": ip_el / args.inplace_steps * 1e3, "advance_kernel_avg_us": ip_k * 1e6}
 
     if world > 1:
         t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64, device=dev)
@@ -230,18 +266,21 @@ def main():
                 "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels",
                 "envs_per_gpu": B, "global_envs": world * B, "assets": N, "window": W, "features": F,
                 "reward": "log_returns", "commission": 0.0, "obs_dtype": "f32", "accumulate": "f64",
+                "windows": args.windows,
                 "parallelism": f"env-sharded x{world} (no collective in the step)",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "step_advance_kernel<true>", "kernel_avg_us": kern_avg_s * 1e6,
+                "kernel": "advance_rows_kernel", "kernel_avg_us": kern_avg_s * 1e6,
                 "bytes_per_env_step": bstep,
             },
             "cpu_baseline": cpu,
             "reward_mae": None if mae is None else mae["reward_mae"],
             "parity_sample": mae,
             "nonfinite_envs": nonfinite,
+            "step_path": env.step_path,
+            "inplace": inplace,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

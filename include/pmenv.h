@@ -113,8 +113,13 @@ size_t pmenv_state_bytes_for(const pmenv_cfg* cfg);
 int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_bytes, pmenv** out);
 /* Byte offsets of the state fields inside the state blob:
  * [0] value f64[B], [1] stat_a f64[B], [2] stat_b f64[B], [3] counter i32[B],
- * [4] ring f32[B,W,N], [5] nonfinite u64. */
-int pmenv_state_layout(const pmenv_cfg* cfg, size_t offsets[6]);
+ * [4] ring f32[B,W,N], [5] nonfinite u64, [6] last_close f32[B,N] (the close of
+ * the window's last day, i.e. obs[b, n, W-1, close_channel], kept by reset/step
+ * so the advance path never re-reads the window to form price relatives),
+ * [7] w_new f32[B,N] (post-drift weights of the latest step = the ring slot just
+ * written, stored densely for the streaming kernel). */
+#define PMENV_STATE_FIELDS 8
+int pmenv_state_layout(const pmenv_cfg* cfg, size_t offsets[PMENV_STATE_FIELDS]);
 int pmenv_destroy(pmenv* h);
 const char* pmenv_last_error(const pmenv* h);
 int pmenv_get_cfg(const pmenv* h, pmenv_cfg* out);
@@ -131,10 +136,20 @@ typedef struct pmenv_step_args {
     const float* prices;   /* [B, N]  price relatives y_t, or NULL (needs bar)       */
     const float* bar;      /* [B, N, F-1] new day's market channels, or NULL          */
     float* obs;            /* [B, N, W, F] in/out                                     */
+    float* obs_out;        /* advance mode only: NULL = advance obs in place; else the
+                              advanced window is written here and obs is left untouched
+                              (double-buffered windows; must not overlap obs)           */
     float* reward;         /* [B] out, may be NULL                                    */
     double* ret;           /* [B] out (info["returns"]), may be NULL                  */
     float* weights;        /* [B, N] out post-drift weights (info["actions"]), may be NULL */
+    uint32_t phases;       /* 0 = whole step; PMENV_PHASE_SCALAR / PMENV_PHASE_ADVANCE run
+                              one launch of the two-launch advance path (the advance
+                              phase must follow the scalar phase of the same step;
+                              used to time the streaming kernel on its own)          */
 } pmenv_step_args;
+
+#define PMENV_PHASE_SCALAR 1u
+#define PMENV_PHASE_ADVANCE 2u
 
 /* TradingEnv.step (trading_env.py:44-105) for all B envs in one kernel.
  *  - bar == NULL  ("surface" mode, the reference's own contract): obs is the
@@ -144,11 +159,16 @@ typedef struct pmenv_step_args {
  *    env-owned window returned by the previous reset/step; it is advanced one
  *    day in place (instrument.py:339-356 sliding window), the bar is appended
  *    at t = W-1, and if prices == NULL the relatives are
- *    bar[close] / obs[W-1, close] (instrument.py:79).
+ *    bar[close] / obs[W-1, close] (instrument.py:79), with obs[W-1, close]
+ *    taken from the env's last_close state (equal to it by construction).
  * Portfolio value (f64, env-owned) is readable through pmenv_value(). */
 int pmenv_step_ex(pmenv* h, const pmenv_step_args* args, hipStream_t stream);
 int pmenv_step(pmenv* h, const float* action, const float* prices, const float* bar,
                float* obs, float* reward, hipStream_t stream);
+
+/* Which kernels the advance path launches for this handle's shape (diagnostics):
+ * "scalar_step_kernel+advance_rows_kernel" or "step_advance_lds_kernel". */
+const char* pmenv_step_path(const pmenv* h);
 
 /* Device pointer to the env-owned portfolio values [B] f64 (TradingEnv.value). */
 double* pmenv_value(pmenv* h);

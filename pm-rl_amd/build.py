@@ -33,8 +33,9 @@ def _run(cmd):
 
 
 def build_pmenv(force=False):
-    hdr = os.path.join(ROOT, "include", "pmenv.h")
-    if not force and not _stale(LIB, SRC, hdr, __file__):
+    deps = [os.path.join(ROOT, "include", "pmenv.h")] + [
+        os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
+    if not force and not _stale(LIB, SRC, *deps, __file__):
         return LIB
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),

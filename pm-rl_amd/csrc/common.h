@@ -1,0 +1,131 @@
+// common.h — shared device helpers and the kernel parameter block.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/pmenv.h"
+
+namespace pmenv_dev {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-B access
+
+// ---------------------------------------------------------------- fast division
+// q = floor(n / d) for 0 <= n < 2^31 by multiply-high (Granlund & Montgomery).
+struct FastDiv {
+    uint32_t mul, shift, d;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    f.shift = s;
+    f.mul = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    uint32_t hi = __umulhi(n, f.mul);
+    return (uint32_t)(((uint64_t)hi + n) >> f.shift);
+}
+
+// ---------------------------------------------------------------- parameter block
+struct StepParams {
+    int B, N, W, F, close_ch;
+    int reward_kind, norm_mode, ring_mode, ret_mode, mu_max_iter;
+    int rows_per_tile;     // LDS kernel: asset rows per staged tile
+    int tile_floats;       // LDS kernel: floats reserved for the tile region (multiple of 4)
+    int unit_rows;         // streaming kernel: asset rows per workgroup
+    int units_per_env;
+    double init_cash, commission, scale, rf, eta, mu_tol;
+    const float* action;
+    const float* prices;
+    const float* bar;
+    float* obs;
+    float* obs_out;        // advance mode: destination window (== obs when in place)
+    float* reward;
+    double* ret;
+    float* weights;
+    // env state (handle-owned)
+    double* value;
+    int32_t* k;
+    float* ring;
+    float* last_close;
+    float* w_new;          // [B, N] post-drift weights of the latest step (dense copy of the ring slot)
+    double* sa;
+    double* sb;
+    unsigned long long* nonfinite;
+    FastDiv div_wf, div_f, div_w, div_units;
+};
+
+// ---------------------------------------------------------------- buffer access
+// Range-checked buffer loads/stores (CDNA SRSRC descriptors): a lane whose byte
+// offset falls outside [0, bytes) reads 0 / stores nothing, so prologues need no
+// per-lane branches (and no control-flow joins that force early vmcnt waits).
+// Build descriptors from wave-uniform values only (kernel args, blockIdx).
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+}
+__device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, uint32_t off, f4 v) {
+    const u4v u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
+}
+
+// ---------------------------------------------------------------- wave reductions
+// f64 reductions over one wave with DPP row shifts (no LDS crossbar): four
+// row_shr steps leave each 16-lane row's total in its lane 15, and the four row
+// totals are combined in a fixed order from v_readlane — so every lane gets
+// bitwise the same value and every branch taken on it is wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift(double v, double fill) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const int flo = __double2loint(fill), fhi = __double2hiint(fill);
+    const int rlo = __builtin_amdgcn_update_dpp(flo, lo, CTRL, 0xF, 0xF, false);
+    const int rhi = __builtin_amdgcn_update_dpp(fhi, hi, CTRL, 0xF, 0xF, false);
+    return __hiloint2double(rhi, rlo);
+}
+
+__device__ __forceinline__ double lane_value(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+
+__device__ __forceinline__ double wave_sum(double v) {
+    v += dpp_shift<kRowShr1>(v, 0.0);
+    v += dpp_shift<kRowShr2>(v, 0.0);
+    v += dpp_shift<kRowShr4>(v, 0.0);
+    v += dpp_shift<kRowShr8>(v, 0.0);
+    return (lane_value(v, 15) + lane_value(v, 31)) + (lane_value(v, 47) + lane_value(v, 63));
+}
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, dpp_shift<kRowShr1>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr2>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr4>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr8>(v, -INFINITY));
+    return fmax(fmax(lane_value(v, 15), lane_value(v, 31)), fmax(lane_value(v, 47), lane_value(v, 63)));
+}
+__device__ __forceinline__ double wave_min(double v) {
+    v = fmin(v, dpp_shift<kRowShr1>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr2>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr4>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr8>(v, INFINITY));
+    return fmin(fmin(lane_value(v, 15), lane_value(v, 31)), fmin(lane_value(v, 47), lane_value(v, 63)));
+}
+
+}  // namespace pmenv_dev

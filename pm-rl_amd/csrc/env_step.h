@@ -1,0 +1,626 @@
+// env_step.h — the env step and reset kernels.
+//
+// Reference semantics restated (zachramsey/pm-rl):
+//   env/sim/trading_env.py:21-41 reset, :44-105 step
+//   env/sim/weight_buffer.py:13-51 ring update / get_last / get_all
+//   env/reward.py:20-31 returns / log_returns / sharpe_ratio
+//   data/instrument.py:79 price relatives, :339-356 sliding window
+//
+// Advance mode (north-star fused path) runs as two launches on the caller's stream:
+//   scalar_step_kernel  — one wave per env: normalisation, commission fixed point,
+//                         value (f64), return, reward, weight drift; writes w' into
+//                         the ring slot. Latency-bound, so it is kept out of the
+//                         streaming kernel where it would stall every workgroup.
+//   advance_rows_kernel — pure HBM streaming: each workgroup advances a unit of
+//                         whole asset rows of one env's [N, W, F] window by one day
+//                         in place and appends the bar and w'.
+// step_advance_lds_kernel is the single-launch fallback for shapes the streaming
+// kernel does not cover (F < 5, env blocks that are not 16-B granular, rows too long).
+#pragma once
+#include "common.h"
+
+namespace pmenv_dev {
+
+constexpr int kBlock = 256;         // threads per env workgroup (LDS / surface / reset kernels)
+constexpr int kMaxVec = 8;          // float4 per thread for one LDS tile
+constexpr int kTileFloats = kBlock * kMaxVec * 4;  // 8192 floats = 32 KiB LDS tile
+constexpr int kScalarWaves = 4;     // envs (waves) per scalar_step_kernel workgroup
+constexpr int kStreamBlock = 512;   // threads per advance_rows_kernel workgroup
+
+// LDS carve of the per-env scalar scratch, behind an optional 16-B aligned tile region.
+struct Scratch {
+    double* wv;   // [N] target weights, then portfolio values
+    double* yv;   // [N] price relatives
+    float* wl;    // [N] w_last (ring.get_last())
+    float* wp;    // [N] post-drift weights w'
+    float* bar;   // [N * (F-1)] new bar (LDS kernel)
+    int* ints;    // [3] shift_weights, slot, counter after the step
+    int wp_off, bar_off;  // float offsets of wp / bar inside the LDS float array
+};
+
+__device__ __forceinline__ Scratch carve(float* lds, int tile_floats, int N, int F) {
+    Scratch s;
+    s.wv = reinterpret_cast<double*>(lds + tile_floats);
+    s.yv = s.wv + N;
+    s.wl = reinterpret_cast<float*>(s.yv + N);
+    s.wp = s.wl + N;
+    s.bar = s.wp + N;
+    s.ints = reinterpret_cast<int*>(s.bar + N * (F - 1));
+    s.wp_off = tile_floats + 4 * N + N;
+    s.bar_off = s.wp_off + N;
+    return s;
+}
+
+inline size_t scratch_bytes(int tile_floats, int N, int F) {
+    return (size_t)tile_floats * 4 + (size_t)N * 16 + (size_t)N * 8 + (size_t)N * (F - 1) * 4 + 16;
+}
+
+// ---------------------------------------------------------------- the scalar step
+// The per-env scalar part of TradingEnv.step (trading_env.py:54-100), on one wave,
+// split in two so the loads can be issued early:
+//   gather_inputs  — action, price relatives, w_last -> LDS scratch
+//   scalar_compute — everything else, from LDS, in f64.
+__device__ __forceinline__ void gather_inputs(const StepParams& p, int b, Scratch& s, int32_t k) {
+    const int lane = threadIdx.x & 63;
+    const int N = p.N, W = p.W, Fm = p.F - 1;
+    // w_last = ActionBuffer.get_last() = ring slot k % W (weight_buffer.py:28-30), kept
+    // densely in w_new so no load depends on the step counter
+    const float* wlast = p.w_new + (size_t)b * N;
+    (void)W; (void)k;
+    for (int n = lane; n < N; n += 64) {
+        const size_t i = (size_t)b * N + n;
+        const float a = p.action[i];
+        double y = 0.0;
+        if (p.bar) {
+            // instrument.py:79 divides float32 tensors: the relative is the correctly
+            // rounded fp32 quotient of today's close over the window's last close
+            const float cn = p.bar[i * Fm + p.close_ch];
+            y = p.prices ? (double)p.prices[i] : (double)(cn / p.last_close[i]);
+            p.last_close[i] = cn;
+        } else {
+            y = (double)p.prices[i];
+        }
+        s.wv[n] = (double)a;
+        s.yv[n] = y;
+        s.wl[n] = wlast[n];
+    }
+}
+
+__device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scratch& s, int32_t k,
+                                               double v_prev) {
+    const int lane = threadIdx.x & 63;
+    const int N = p.N, W = p.W;
+
+    // :54-55 flatten; :58 isclose(sum) / min(action)
+    double sum = 0.0, mn = INFINITY;
+    int nan_seen = 0;
+    for (int n = lane; n < N; n += 64) {
+        const double a = s.wv[n];
+        sum += a;
+        mn = fmin(mn, a);
+        nan_seen |= isnan(a);
+    }
+    sum = wave_sum(sum);
+    mn = wave_min(mn);
+    if (__any(nan_seen)) mn = NAN;               // torch.min propagates NaN
+
+    // :58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR for the trainer) min < 0
+    const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
+    const bool negative = mn < 0.0;
+    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    if (norm) {
+        double shift = 0.0;
+        if (p.norm_mode == PMENV_NORM_OR) {      // torch.softmax is max-shifted
+            double m = -INFINITY;
+            for (int n = lane; n < N; n += 64) m = fmax(m, s.wv[n]);
+            shift = wave_max(m);
+        }
+        double z = 0.0;
+        for (int n = lane; n < N; n += 64) {
+            double e = exp(s.wv[n] - shift);      // :59 exp(w) (no max-shift in AND mode)
+            s.wv[n] = e;
+            z += e;
+        }
+        z = wave_sum(z);
+        for (int n = lane; n < N; n += 64) s.wv[n] = s.wv[n] / z;   // :60
+    }
+
+    // :67-75 transaction remainder factor mu (PGPortfolio fixed point), f64, capped
+    double V = v_prev;
+    if (p.commission > 0.0) {
+        const double c = p.commission;
+        double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
+        const double w0 = s.wv[0];
+        const double wl0 = (double)s.wl[0];
+        int it = 0;
+        while (fabs(mu - mu_last) > p.mu_tol && it < p.mu_max_iter) {
+            mu_last = mu;
+            double part = 0.0;
+            for (int n = lane; n < N; n += 64) {
+                if (n == 0) continue;
+                double d = (double)s.wl[n] - mu * s.wv[n];
+                part += d > 0.0 ? d : 0.0;        // torch.maximum(x, 0) as intended
+            }
+            double tot = wave_sum(part);
+            mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
+            ++it;
+        }
+        V = mu * V;
+    }
+
+    // :78-79 portfolio = V * (w * y); value = sum(portfolio)
+    double part = 0.0;
+    for (int n = lane; n < N; n += 64) {
+        double pv = V * (s.wv[n] * s.yv[n]);
+        s.wv[n] = pv;
+        part += pv;
+    }
+    const double value = wave_sum(part);
+
+    // :83-84 w' = portfolio / value ; ring.update(w') at slot idx = (1 + k) % W
+    const int slot = (int)((1 + (int64_t)k) % W);
+    float* ring_slot = p.ring + (size_t)b * W * N + (size_t)slot * N;
+    for (int n = lane; n < N; n += 64) {
+        float w = (float)(s.wv[n] / value);
+        s.wp[n] = w;
+        ring_slot[n] = w;
+        p.w_new[(size_t)b * N + n] = w;
+        if (p.weights) p.weights[(size_t)b * N + n] = w;
+    }
+
+    if (lane == 0) {
+        // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
+        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
+        double r;
+        switch (p.reward_kind) {
+        case PMENV_REWARD_RETURN:
+            r = ret * p.scale;
+            break;
+        case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
+            double m = (double)(k + 1);
+            double mean = p.sa[b], m2 = p.sb[b];
+            double d = ret - mean;
+            mean += d / m;
+            m2 += d * (ret - mean);
+            p.sa[b] = mean;
+            p.sb[b] = m2;
+            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
+            break;
+        }
+        case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
+            double R = ret - 1.0, A = p.sa[b], Bm = p.sb[b];
+            double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
+            r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
+            p.sa[b] = A + p.eta * dA;
+            p.sb[b] = Bm + p.eta * dB;
+            break;
+        }
+        default:
+            r = log(ret) * p.scale;              // :99
+        }
+        p.value[b] = value;
+        p.k[b] = k + 1;
+        if (p.reward) p.reward[b] = (float)r;
+        if (p.ret) p.ret[b] = ret;
+        if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
+        // weight channel: shift with the window until the ring is full, then
+        // (reference storage order) overwrite slot `slot` in place
+        s.ints[0] = (p.ring_mode == PMENV_RING_CHRONO) || (k < W - 1);
+        s.ints[1] = slot;
+        s.ints[2] = k + 1;
+    }
+}
+
+// ---------------------------------------------------------------- K1: scalar step
+// One wave per env, kScalarWaves envs per workgroup, no barriers.
+__global__ __launch_bounds__(64 * kScalarWaves) void scalar_step_kernel(StepParams p, int scratch_floats) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int wave = threadIdx.x >> 6;
+    const int b = blockIdx.x * kScalarWaves + wave;
+    if (b >= p.B) return;
+    Scratch s = carve(lds + wave * scratch_floats, 0, p.N, p.F);
+    const int32_t k = p.k[b];
+    const double v_prev = p.value[b];
+    gather_inputs(p, b, s, k);
+    scalar_compute(p, b, s, k, v_prev);
+}
+
+// ---------------------------------------------------------------- K1, register form (N <= 64)
+// L lanes per env (L = 32: two envs per wave for N <= 32; L = 64: one), one asset
+// per lane, every per-asset value in VGPRs. Reductions are DPP row shifts plus a
+// fixed-order combine of the row totals of the lane's group, so each group's lanes
+// hold bitwise the same value. No LDS, no barrier, one memory round trip.
+template <int L>
+__device__ __forceinline__ double group_combine(double r0, double r1, double r2, double r3, int lane) {
+    if (L == 64) return (r0 + r1) + (r2 + r3);
+    return lane < 32 ? r0 + r1 : r2 + r3;
+}
+template <int L>
+__device__ __forceinline__ double group_sum(double v, int lane) {
+    v += dpp_shift<kRowShr1>(v, 0.0);
+    v += dpp_shift<kRowShr2>(v, 0.0);
+    v += dpp_shift<kRowShr4>(v, 0.0);
+    v += dpp_shift<kRowShr8>(v, 0.0);
+    return group_combine<L>(lane_value(v, 15), lane_value(v, 31), lane_value(v, 47), lane_value(v, 63), lane);
+}
+template <int L>
+__device__ __forceinline__ double group_max(double v, int lane) {
+    v = fmax(v, dpp_shift<kRowShr1>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr2>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr4>(v, -INFINITY));
+    v = fmax(v, dpp_shift<kRowShr8>(v, -INFINITY));
+    const double r0 = lane_value(v, 15), r1 = lane_value(v, 31), r2 = lane_value(v, 47), r3 = lane_value(v, 63);
+    if (L == 64) return fmax(fmax(r0, r1), fmax(r2, r3));
+    return lane < 32 ? fmax(r0, r1) : fmax(r2, r3);
+}
+template <int L>
+__device__ __forceinline__ double group_min(double v, int lane) {
+    v = fmin(v, dpp_shift<kRowShr1>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr2>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr4>(v, INFINITY));
+    v = fmin(v, dpp_shift<kRowShr8>(v, INFINITY));
+    const double r0 = lane_value(v, 15), r1 = lane_value(v, 31), r2 = lane_value(v, 47), r3 = lane_value(v, 63);
+    if (L == 64) return fmin(fmin(r0, r1), fmin(r2, r3));
+    return lane < 32 ? fmin(r0, r1) : fmin(r2, r3);
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
+    constexpr int EPW = 64 / L;                   // envs per wave
+    const int lane = threadIdx.x & 63;
+    const int n = lane % L;
+    const int b = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * EPW + lane / L;
+    const int N = p.N, W = p.W, Fm = p.F - 1;
+    const bool env_ok = b < p.B;
+    const bool act = env_ok && n < N;
+    const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
+
+    // every load up front, none dependent on another
+    const int32_t k = env_ok ? p.k[env_ok ? b : 0] : 0;
+    const double v_prev = env_ok ? p.value[env_ok ? b : 0] : 1.0;
+    const double a = act ? (double)p.action[i] : 0.0;
+    const float wlf = act ? p.w_new[i] : 0.0f;                       // get_last() (weight_buffer.py:28-30)
+    double y = 1.0;
+    float cn = 0.0f;
+    if (act) {
+        if (p.bar) {
+            cn = p.bar[i * Fm + p.close_ch];
+            y = p.prices ? (double)p.prices[i] : (double)(cn / p.last_close[i]);   // instrument.py:79
+        } else {
+            y = (double)p.prices[i];
+        }
+    }
+
+    // :58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min(action) < 0
+    const double sum = group_sum<L>(act ? a : 0.0, lane);
+    double mn = group_min<L>(act ? a : INFINITY, lane);
+    const bool nan_here = act && isnan(a);
+    const uint64_t nan_mask = __ballot(nan_here);
+    const uint64_t gmask = L == 64 ? ~0ull : (lane < 32 ? 0xFFFFFFFFull : 0xFFFFFFFF00000000ull);
+    if (nan_mask & gmask) mn = NAN;               // torch.min propagates NaN
+    const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
+    const bool negative = mn < 0.0;
+    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    double w = a;
+    if (__any(norm)) {
+        double shift = 0.0;
+        if (p.norm_mode == PMENV_NORM_OR) shift = group_max<L>(act ? a : -INFINITY, lane);
+        const double e = act ? exp(a - shift) : 0.0;             // :59 (no max-shift in AND mode)
+        const double z = group_sum<L>(e, lane);
+        if (norm) w = e / z;                                      // :60
+    }
+
+    // :67-75 commission fixed point (f64, capped), per env group
+    double V = v_prev;
+    if (p.commission > 0.0) {
+        const double c = p.commission;
+        const double w0 = __shfl(w, lane & ~(L - 1), 64);
+        const double wl0 = (double)__shfl(wlf, lane & ~(L - 1), 64);
+        double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
+        int it = 0;
+        bool done = !(fabs(mu - mu_last) > p.mu_tol) || p.mu_max_iter <= 0;
+        while (__any(!done)) {
+            const double d = (act && n > 0) ? (double)wlf - mu * w : 0.0;
+            const double tot = group_sum<L>(d > 0.0 ? d : 0.0, lane);   // torch.maximum(x, 0) as intended
+            if (!done) {
+                mu_last = mu;
+                mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
+                ++it;
+                done = !(fabs(mu - mu_last) > p.mu_tol) || it >= p.mu_max_iter;
+            }
+        }
+        V = mu * V;
+    }
+
+    // :78-79 portfolio value; :83-84 w' = portfolio / value -> ring slot (1 + k) % W
+    const double pv = act ? V * (w * y) : 0.0;
+    const double value = group_sum<L>(pv, lane);
+    const int slot = (int)((1 + (int64_t)k) % W);
+    if (act) {
+        const float wp = (float)(pv / value);
+        p.ring[(size_t)b * W * N + (size_t)slot * N + n] = wp;
+        p.w_new[i] = wp;
+        if (p.weights) p.weights[i] = wp;
+        if (p.bar) p.last_close[i] = cn;
+    }
+    if (env_ok && n == 0) {
+        // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
+        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
+        double r;
+        switch (p.reward_kind) {
+        case PMENV_REWARD_RETURN:
+            r = ret * p.scale;
+            break;
+        case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
+            double m = (double)(k + 1);
+            double mean = p.sa[b], m2 = p.sb[b];
+            double d = ret - mean;
+            mean += d / m;
+            m2 += d * (ret - mean);
+            p.sa[b] = mean;
+            p.sb[b] = m2;
+            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
+            break;
+        }
+        case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
+            double R = ret - 1.0, A = p.sa[b], Bm = p.sb[b];
+            double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
+            r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
+            p.sa[b] = A + p.eta * dA;
+            p.sb[b] = Bm + p.eta * dB;
+            break;
+        }
+        default:
+            r = log(ret) * p.scale;              // :99
+        }
+        p.value[b] = value;
+        p.k[b] = k + 1;
+        if (p.reward) p.reward[b] = (float)r;
+        if (p.ret) p.ret[b] = ret;
+        if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
+    }
+}
+
+// ---------------------------------------------------------------- K2: window advance
+// A workgroup owns `unit_rows` whole asset rows of one env (a unit never straddles
+// an env; rows only ever read themselves, so units are independent). F = 5
+// ([open, high, low, close, weight], the BASELINE layout; other F take the LDS
+// fallback). Thread q owns output chunk q = floats 4q..4q+3 of the unit:
+//   out[n, t, f]   = t < W-1 ? in[n, t+1, f] : bar[n, f]               (market)
+//   out[n, t, F-1] = shifted with w'[n] appended at t = W-1, or — ring full,
+//                    storage order (weight_buffer.py:38-39) — in[n, t, F-1] with
+//                    w'[n] at t == slot.
+// Everything a chunk can need is loaded straight into VGPRs before the one
+// barrier, with no dependency on the step counter: the shifted source
+// in[4q+5 .. 4q+8] (one dword-aligned 16-B load), the bar row of the chunk's
+// asset (16 B, only if the chunk touches the last day), w'[n] and the chunk's
+// unshifted weight float. After the barrier — which closes the in-place
+// read-before-write window of the unit — the chunk is pure selects and one 16-B
+// store: a workgroup lives one memory round trip plus its store issue, which is
+// what bounds this kernel (bytes in flight per CU = residency x unit size).
+// ABL (timing-only ablation builds, tools/ab_advance.py; 0 in the product):
+//   1 = skip the bar / w' loads, 2 = skip the unshifted-weight load, 4 = store xs as is.
+template <int BLOCK, int V, bool INPLACE, int ABL = 0>
+__global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
+    constexpr int F = 5;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W;
+    const int WF = W * F;
+    const int R = p.unit_rows;
+    const int b = (int)fdiv(blockIdx.x, p.div_units);
+    const int r0 = (int)(blockIdx.x - (uint32_t)b * (uint32_t)p.units_per_env) * R;
+    const int rows = min(R, N - r0);
+    const uint32_t nf = (uint32_t)(rows * WF);
+    const uint32_t nq = nf >> 2;
+    // descriptors: the env's window (loads may run past the unit into the env,
+    // never past the env), this unit's rows (stores), the env's bar and w' rows
+    float* env_obs = p.obs + (size_t)b * N * WF;
+    const uint32_t unit_off = (uint32_t)(r0 * WF) * 4u;
+    const auto rs_env = make_rsrc(env_obs, (uint32_t)(N * WF) * 4u);
+    float* env_out = p.obs_out + (size_t)b * N * WF;
+    const auto rs_unit = make_rsrc(env_out + (size_t)r0 * WF, nf * 4u);
+    const auto rs_bar = make_rsrc(p.bar + (size_t)b * N * 4, (uint32_t)(rows + r0) * 16u);
+    const auto rs_wp = make_rsrc(p.w_new + (size_t)b * N, (uint32_t)(rows + r0) * 4u);
+
+    f4 xs[V], xb[V];
+    float xwp[V], xun[V];
+    int kk0[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint32_t q = (uint32_t)(tid + i * BLOCK);
+        const uint32_t j0 = 4u * q;
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const int kk = (int)(j0 - row * (uint32_t)WF);   // position of the chunk's first float in its row
+        const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+        const int ew = min(F - 1 - f0, 3);                // element holding the weight channel
+        kk0[i] = kk;
+        xs[i] = buf_load4(rs_env, unit_off + (j0 + F) * 4u);                 // shifted source
+        xb[i] = f4{0.f, 0.f, 0.f, 0.f};
+        xwp[i] = 0.f;
+        xun[i] = 0.f;
+        if (!(ABL & 1)) {
+            xb[i] = buf_load4(rs_bar, (uint32_t)(r0 + (int)row) * 16u);     // the asset's new bar
+            xwp[i] = buf_load1(rs_wp, (uint32_t)(r0 + (int)row) * 4u);      // its new weight w'
+        }
+        if (!(ABL & 2)) xun[i] = buf_load1(rs_env, unit_off + (j0 + (uint32_t)ew) * 4u);   // unshifted weight
+    }
+    const int32_t k = p.k[b] - 1;                    // scalar_step_kernel already counted this step
+    if (INPLACE) {
+        // in place: every load of the unit lands before the unit's first store
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
+    const int slotF = (int)((1 + (int64_t)k) % W) * F;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint32_t q = (uint32_t)(tid + i * BLOCK);
+        float v[4] = {xs[i].x, xs[i].y, xs[i].z, xs[i].w};
+        const float bv[4] = {xb[i].x, xb[i].y, xb[i].z, xb[i].w};
+        int kk = kk0[i];
+        int f = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+#pragma unroll
+        for (int e = 0; e < ((ABL & 4) ? 0 : 4); ++e) {
+            const bool lastday = kk >= WF - F;        // false after wrapping into the next row
+            if (f == F - 1) {
+                const bool w_here = shift_w ? lastday : (kk - f == slotF);
+                v[e] = w_here ? xwp[i] : (shift_w ? v[e] : xun[i]);
+            } else {
+                const float bf = f == 0 ? bv[0] : f == 1 ? bv[1] : f == 2 ? bv[2] : bv[3];
+                v[e] = lastday ? bf : v[e];
+            }
+            ++kk;
+            if (++f == F) f = 0;
+            if (kk == WF) kk = 0;
+        }
+        if (ABL & 4) v[0] += bv[0] + xwp[i] + xun[i];
+        buf_store4(rs_unit, q * 16u, f4{v[0], v[1], v[2], v[3]});        // lanes past the unit: dropped
+    }
+    (void)nq;
+}
+
+// ---------------------------------------------------------------- single-launch fallback
+// The whole step in one workgroup per env with the obs staged through an LDS tile
+// (rows of any length up to kTileFloats, any F >= 2, any alignment).
+template <int BLOCK, int MAXV, bool VEC>
+__device__ __forceinline__ void stage_tile(const float* __restrict__ src, float* lds, int nf, int tid) {
+    if (VEC) {
+        f4 reg[MAXV];
+        const int nq = nf >> 2;
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            int q = tid + i * BLOCK;
+            reg[i] = q < nq ? reinterpret_cast<const f4*>(src)[q] : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < MAXV; ++i) {
+            int q = tid + i * BLOCK;
+            if (q < nq) reinterpret_cast<f4*>(lds)[q] = reg[i];
+        }
+    } else {
+        float reg[MAXV * 4];
+#pragma unroll
+        for (int i = 0; i < MAXV * 4; ++i) {
+            int j = tid + i * BLOCK;
+            reg[i] = j < nf ? src[j] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < MAXV * 4; ++i) {
+            int j = tid + i * BLOCK;
+            if (j < nf) lds[j] = reg[i];
+        }
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
+    const int WF = W * F;
+    const int R = p.rows_per_tile;
+    Scratch s = carve(lds, p.tile_floats, N, F);
+    float* obs = p.obs + (size_t)b * N * WF;
+
+    const float* barg = p.bar + (size_t)b * N * Fm;
+    for (int i = tid; i < N * Fm; i += kBlock) s.bar[i] = barg[i];
+    if (tid < 64) {
+        const int32_t k = p.k[b];
+        const double v_prev = p.value[b];
+        gather_inputs(p, b, s, k);
+        scalar_compute(p, b, s, k, v_prev);
+    }
+    __syncthreads();
+    const int shift_w = s.ints[0];
+    const int slot = s.ints[1];
+
+    for (int r0 = 0; r0 < N; r0 += R) {
+        const int rows = min(R, N - r0);
+        const int nf = rows * WF;
+        if (r0 > 0) __syncthreads();
+        stage_tile<kBlock, kMaxVec, VEC>(obs + (size_t)r0 * WF, lds, nf, tid);
+        __syncthreads();
+        float* dst = p.obs_out + (size_t)b * N * WF + (size_t)r0 * WF;
+        for (int j = tid; j < nf; j += kBlock) {
+            uint32_t row = fdiv((uint32_t)j, p.div_wf);
+            uint32_t kk = (uint32_t)j - row * (uint32_t)WF;
+            uint32_t t = fdiv(kk, p.div_f);
+            uint32_t f = kk - t * (uint32_t)F;
+            const int n = r0 + (int)row;
+            const bool lastday = (int)t == W - 1;
+            int idx;
+            if ((int)f == F - 1)
+                idx = shift_w ? (lastday ? s.wp_off + n : j + F) : ((int)t == slot ? s.wp_off + n : j);
+            else
+                idx = lastday ? s.bar_off + n * Fm + (int)f : j + F;
+            dst[j] = lds[idx];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- surface kernel
+// The reference contract: obs is the caller's next-day window; only channel F-1
+// is rewritten with ActionBuffer.get_all() (trading_env.py:103).
+__global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W, F = p.F;
+    Scratch s = carve(lds, 0, N, F);
+    if (tid < 64) {
+        const int32_t k = p.k[b];
+        const double v_prev = p.value[b];
+        gather_inputs(p, b, s, k);
+        scalar_compute(p, b, s, k, v_prev);
+    }
+    __syncthreads();
+    if (!p.obs) return;
+    const int slot = s.ints[1];
+    const int32_t k1 = s.ints[2];                 // updates since reset, after this step
+    const int idx = (int)((1 + (int64_t)k1) % W);
+    const bool full = (int64_t)k1 >= W - 1;
+    const float* ringb = p.ring + (size_t)b * W * N;
+    float* obs = p.obs + (size_t)b * N * W * F;
+    for (int i = tid; i < N * W; i += kBlock) {
+        const int n = (int)fdiv((uint32_t)i, p.div_w);
+        const int t = i - n * W;
+        int rs;  // ring slot feeding position t, or -1 for zero padding (weight_buffer.py:38-44)
+        if (!full) rs = t < W - idx ? -1 : t - (W - idx);
+        else rs = p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
+        float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
+        obs[((size_t)n * W + t) * F + (F - 1)] = v;
+    }
+    // keep the advance-mode close in step with the caller's window
+    for (int n = tid; n < N; n += kBlock)
+        p.last_close[(size_t)b * N + n] = obs[((size_t)n * W + (W - 1)) * F + p.close_ch];
+}
+
+// ---------------------------------------------------------------- reset kernel
+__global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask) {
+    const int b = blockIdx.x;
+    if (mask && !mask[b]) return;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W, F = p.F;
+    if (tid == 0) {
+        p.value[b] = p.init_cash;                 // trading_env.py:28
+        p.k[b] = 0;                               // weight_buffer.py:49 idx = 1
+        p.sa[b] = 0.0;
+        p.sb[b] = 0.0;
+    }
+    float* ringb = p.ring + (size_t)b * W * N;     // weight_buffer.py:47-48 e0 in slot 0
+    for (int i = tid; i < W * N; i += kBlock) ringb[i] = i == 0 ? 1.0f : 0.0f;
+    for (int n = tid; n < N; n += kBlock) p.w_new[(size_t)b * N + n] = n == 0 ? 1.0f : 0.0f;   // get_last()
+    if (!obs) return;
+    float* ob = obs + (size_t)b * N * W * F;       // trading_env.py:31-32 get_all() at idx = 1
+    for (int i = tid; i < N * W; i += kBlock) {
+        const int n = (int)fdiv((uint32_t)i, p.div_w);
+        const int t = i - n * W;
+        ob[((size_t)n * W + t) * F + (F - 1)] = (n == 0 && t == W - 1) ? 1.0f : 0.0f;
+    }
+    for (int n = tid; n < N; n += kBlock)
+        p.last_close[(size_t)b * N + n] = ob[((size_t)n * W + (W - 1)) * F + p.close_ch];
+}
+
+}  // namespace pmenv_dev

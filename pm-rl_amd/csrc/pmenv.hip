@@ -1,592 +1,50 @@
-// pmenv.hip — MI355X (gfx950) vectorised portfolio environment: HIP kernels + C ABI.
+// pmenv.hip — host side and C ABI (include/pmenv.h) of the MI355X-native
+// vectorised portfolio environment. Device code lives in env_step.h (step / reset),
+// data.h (synthetic market data) and rollout.h (GAE, moments).
 //
-// One workgroup owns one env per launch. The env's [N, W, F] observation block is
-// staged through LDS, so the one-day window advance (a shift by F floats inside
-// every asset row: 20 B for F = 5, not 16-B aligned) is done with aligned 16-B
-// global loads and stores and arbitrary-offset LDS reads. The per-env scalar work
-// (normalisation, commission fixed point, value, return, reward, weight drift)
-// runs on wave 0 with 64-lane shuffle reductions in f64.
-//
-// Reference semantics restated (zachramsey/pm-rl):
-//   env/sim/trading_env.py:21-41 reset, :44-105 step
-//   env/sim/weight_buffer.py:13-51 ring update / get_last / get_all
-//   env/reward.py:20-31 returns / log_returns / sharpe_ratio
-//   data/instrument.py:79 price relatives, :339-356 sliding window
+// Every entry point enqueues on the caller's stream and never synchronises,
+// allocates or frees (graph-capturable), except create / destroy / the explicit
+// synchronous queries documented in the header.
 #include <hip/hip_runtime.h>
 
-#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pmenv.h"
+#include "common.h"
+#include "data.h"
+#include "env_step.h"
+#include "rollout.h"
 
-namespace {
+using namespace pmenv_dev;
 
-constexpr int kBlock = 256;         // threads per env workgroup (4 waves)
-constexpr int kMaxVec = 8;          // float4 registers per thread for one tile
-constexpr int kTileFloats = kBlock * kMaxVec * 4;  // 8192 floats = 32 KiB LDS tile
-
-// ---------------------------------------------------------------- fast division
-// q = floor(n / d) for 0 <= n < 2^31 by multiply-high (Granlund & Montgomery).
-struct FastDiv {
-    uint32_t mul, shift, d;
-};
-
-FastDiv make_fastdiv(uint32_t d) {
-    FastDiv f;
-    f.d = d;
-    uint32_t s = 0;
-    while ((1ull << s) < d) ++s;
-    f.shift = s;
-    f.mul = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-    return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-    uint32_t hi = __umulhi(n, f.mul);
-    return (uint32_t)(((uint64_t)hi + n) >> f.shift);
-}
-
-// ---------------------------------------------------------------- params
-struct StepParams {
-    int B, N, W, F, close_ch;
-    int reward_kind, norm_mode, ring_mode, ret_mode, mu_max_iter;
-    int rows_per_tile;     // asset rows per LDS tile
-    int tile_floats;       // floats reserved for the tile region (multiple of 4)
-    double init_cash, commission, scale, rf, eta, mu_tol;
-    const float* action;
-    const float* prices;
-    const float* bar;
-    float* obs;
-    float* reward;
-    double* ret;
-    float* weights;
-    double* value;
-    int32_t* k;
-    float* ring;
-    double* sa;
-    double* sb;
-    unsigned long long* nonfinite;
-    FastDiv div_wf, div_f, div_w;
-};
-
-// ---------------------------------------------------------------- wave reductions
-// Butterfly over 64 lanes then broadcast lane 0, so every lane holds bitwise the
-// same value and every branch taken on it is wave-uniform.
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return __shfl(v, 0, 64);
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return __shfl(v, 0, 64);
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return __shfl(v, 0, 64);
-}
-
-// LDS carve of the per-env scratch, behind the (16-B aligned) tile region.
-struct Scratch {
-    double* wv;   // [N] target weights, then portfolio values
-    double* yv;   // [N] price relatives
-    float* wl;    // [N] w_last (ring.get_last())
-    float* wp;    // [N] post-drift weights w'
-    float* bar;   // [N * (F-1)] new bar (advance mode)
-    int* ints;    // [3] shift_weights, slot, counter after the step
-    int wp_off, bar_off;  // float offsets of wp / bar inside the LDS float array
-};
-
-__device__ __forceinline__ Scratch carve(float* lds, int tile_floats, int N, int F) {
-    Scratch s;
-    s.wv = reinterpret_cast<double*>(lds + tile_floats);
-    s.yv = s.wv + N;
-    s.wl = reinterpret_cast<float*>(s.yv + N);
-    s.wp = s.wl + N;
-    s.bar = s.wp + N;
-    s.ints = reinterpret_cast<int*>(s.bar + N * (F - 1));
-    s.wp_off = tile_floats + 4 * N + N;
-    s.bar_off = s.wp_off + N;
-    return s;
-}
-
-size_t scratch_bytes(int tile_floats, int N, int F) {
-    return (size_t)tile_floats * 4 + (size_t)N * 16 + (size_t)N * 8 + (size_t)N * (F - 1) * 4 + 16;
-}
-
-// ---------------------------------------------------------------- phase A
-// The per-env scalar part of TradingEnv.step (trading_env.py:54-100), on wave 0.
-// `tile` is the env's staged obs block in LDS (advance mode, single tile) or null.
-__device__ __forceinline__ void env_scalar_step(const StepParams& p, int b, Scratch& s, const float* tile) {
-    const int lane = threadIdx.x;
-    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
-    const size_t env_off = (size_t)b * N * W * F;
-    const int32_t k = p.k[b];
-    const double v_prev = p.value[b];
-    const float* ringb = p.ring + (size_t)b * W * N;
-    const int last = k % W;                        // weight_buffer.py:30 (idx-1) % W
-
-    // :54-55 flatten; price relatives (given, or instrument.py:79 from the close channel)
-    double sum = 0.0, mn = INFINITY;
-    int nan_seen = 0;
-    for (int n = lane; n < N; n += 64) {
-        double a = (double)p.action[(size_t)b * N + n];
-        double y;
-        if (p.prices) {
-            y = (double)p.prices[(size_t)b * N + n];
-        } else {
-            // instrument.py:79 divides float32 tensors: correctly rounded fp32 quotient
-            float cn = s.bar[n * Fm + p.close_ch];
-            size_t o = (size_t)n * W * F + (size_t)(W - 1) * F + p.close_ch;
-            float co = tile ? tile[o] : p.obs[env_off + o];
-            y = (double)(cn / co);  // IEEE division (hipcc default: correctly rounded)
-        }
-        s.wv[n] = a;
-        s.yv[n] = y;
-        s.wl[n] = ringb[(size_t)last * N + n];
-        sum += a;
-        mn = fmin(mn, a);
-        nan_seen |= isnan(a);
-    }
-    sum = wave_sum(sum);
-    mn = wave_min(mn);
-    if (__any(nan_seen)) mn = NAN;               // torch.min propagates NaN
-
-    // :58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR for the trainer) min < 0
-    const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
-    const bool negative = mn < 0.0;
-    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
-    if (norm) {
-        double shift = 0.0;
-        if (p.norm_mode == PMENV_NORM_OR) {      // torch.softmax is max-shifted
-            double m = -INFINITY;
-            for (int n = lane; n < N; n += 64) m = fmax(m, s.wv[n]);
-            shift = wave_max(m);
-        }
-        double z = 0.0;
-        for (int n = lane; n < N; n += 64) {
-            double e = exp(s.wv[n] - shift);      // :59 exp(w) (no max-shift in AND mode)
-            s.wv[n] = e;
-            z += e;
-        }
-        z = wave_sum(z);
-        for (int n = lane; n < N; n += 64) s.wv[n] = s.wv[n] / z;   // :60
-    }
-
-    // :67-75 transaction remainder factor mu (PGPortfolio fixed point), f64, capped
-    double V = v_prev;
-    if (p.commission > 0.0) {
-        const double c = p.commission;
-        double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
-        double w0 = __shfl(lane == 0 ? s.wv[0] : 0.0, 0, 64);
-        double wl0 = (double)s.wl[0];
-        int it = 0;
-        while (fabs(mu - mu_last) > p.mu_tol && it < p.mu_max_iter) {
-            mu_last = mu;
-            double part = 0.0;
-            for (int n = lane; n < N; n += 64) {
-                if (n == 0) continue;
-                double d = (double)s.wl[n] - mu * s.wv[n];
-                part += d > 0.0 ? d : 0.0;        // torch.maximum(x, 0) as intended
-            }
-            double tot = wave_sum(part);
-            mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
-            ++it;
-        }
-        V = mu * V;
-    }
-
-    // :78-79 portfolio = V * (w * y); value = sum(portfolio)
-    double part = 0.0;
-    for (int n = lane; n < N; n += 64) {
-        double pv = V * (s.wv[n] * s.yv[n]);
-        s.wv[n] = pv;
-        part += pv;
-    }
-    const double value = wave_sum(part);
-
-    // :83-84 w' = portfolio / value ; ring.update(w') at slot idx = (1 + k) % W
-    const int slot = (int)((1 + (int64_t)k) % W);
-    float* ring_slot = p.ring + (size_t)b * W * N + (size_t)slot * N;
-    for (int n = lane; n < N; n += 64) {
-        float w = (float)(s.wv[n] / value);
-        s.wp[n] = w;
-        ring_slot[n] = w;
-        if (p.weights) p.weights[(size_t)b * N + n] = w;
-    }
-
-    if (lane == 0) {
-        // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
-        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
-        double r;
-        switch (p.reward_kind) {
-        case PMENV_REWARD_RETURN:
-            r = ret * p.scale;
-            break;
-        case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
-            double m = (double)(k + 1);
-            double mean = p.sa[b], m2 = p.sb[b];
-            double d = ret - mean;
-            mean += d / m;
-            m2 += d * (ret - mean);
-            p.sa[b] = mean;
-            p.sb[b] = m2;
-            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
-            break;
-        }
-        case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
-            double R = ret - 1.0, A = p.sa[b], Bm = p.sb[b];
-            double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
-            r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
-            p.sa[b] = A + p.eta * dA;
-            p.sb[b] = Bm + p.eta * dB;
-            break;
-        }
-        default:
-            r = log(ret) * p.scale;              // :99
-        }
-        p.value[b] = value;
-        p.k[b] = k + 1;
-        if (p.reward) p.reward[b] = (float)r;
-        if (p.ret) p.ret[b] = ret;
-        if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
-        // weight channel: shift with the window until the ring is full, then
-        // (reference storage order) overwrite slot `slot` in place
-        s.ints[0] = (p.ring_mode == PMENV_RING_CHRONO) || (k < W - 1);
-        s.ints[1] = slot;
-        s.ints[2] = k + 1;
-    }
-}
-
-// Copy nf floats of one tile HBM -> registers -> LDS. All loads are issued before
-// the first LDS store so up to kMaxVec 16-B loads per lane are in flight.
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-template <bool VEC>
-__device__ __forceinline__ void stage_tile(const float* __restrict__ src, float* lds, int nf, int tid) {
-    if (VEC) {
-        f4 reg[kMaxVec];
-        const int nq = nf >> 2;
-#pragma unroll
-        for (int i = 0; i < kMaxVec; ++i) {
-            int q = tid + i * kBlock;
-            reg[i] = q < nq ? reinterpret_cast<const f4*>(src)[q] : f4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int i = 0; i < kMaxVec; ++i) {
-            int q = tid + i * kBlock;
-            if (q < nq) reinterpret_cast<f4*>(lds)[q] = reg[i];
-        }
-    } else {
-        float reg[kMaxVec * 4];
-#pragma unroll
-        for (int i = 0; i < kMaxVec * 4; ++i) {
-            int j = tid + i * kBlock;
-            reg[i] = j < nf ? src[j] : 0.0f;
-        }
-#pragma unroll
-        for (int i = 0; i < kMaxVec * 4; ++i) {
-            int j = tid + i * kBlock;
-            if (j < nf) lds[j] = reg[i];
-        }
-    }
-}
-
-// ---------------------------------------------------------------- advance kernel
-// out[n, t, f] = t < W-1 ? in[n, t+1, f] : bar[n, f]           (market channels)
-// out[n, t, F-1] = shifted like the market channels with w' appended, or, once the
-// ring is full in storage mode, in[n, t, F-1] with w' at t == slot.
-template <bool VEC>
-__global__ __launch_bounds__(kBlock) void step_advance_kernel(StepParams p) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
-    const int WF = W * F;
-    const int R = p.rows_per_tile;
-    const bool single = R >= N;
-    Scratch s = carve(lds, p.tile_floats, N, F);
-    float* obs = p.obs + (size_t)b * N * WF;
-
-    // the new bar -> LDS (N * Fm floats, coalesced)
-    const float* barg = p.bar + (size_t)b * N * Fm;
-    for (int i = tid; i < N * Fm; i += kBlock) s.bar[i] = barg[i];
-
-    if (single) stage_tile<VEC>(obs, lds, N * WF, tid);
-    __syncthreads();
-    if (tid < 64) env_scalar_step(p, b, s, single ? lds : nullptr);
-    __syncthreads();
-    const int shift_w = s.ints[0];
-    const int slot = s.ints[1];
-
-    for (int r0 = 0; r0 < N; r0 += R) {
-        const int rows = min(R, N - r0);
-        const int nf = rows * WF;
-        if (!single) {
-            if (r0 > 0) __syncthreads();
-            stage_tile<VEC>(obs + (size_t)r0 * WF, lds, nf, tid);
-            __syncthreads();
-        }
-        float* dst = obs + (size_t)r0 * WF;
-        if (VEC) {
-            const int nq = nf >> 2;
-            for (int q = tid; q < nq; q += kBlock) {
-                uint32_t j = (uint32_t)q * 4u;
-                uint32_t row = fdiv(j, p.div_wf);
-                uint32_t kk = j - row * (uint32_t)WF;
-                uint32_t t = fdiv(kk, p.div_f);
-                uint32_t f = kk - t * (uint32_t)F;
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int n = r0 + (int)row;
-                    const bool lastday = (int)t == W - 1;
-                    int idx;
-                    if ((int)f == F - 1)
-                        idx = shift_w ? (lastday ? s.wp_off + n : (int)j + F)
-                                      : ((int)t == slot ? s.wp_off + n : (int)j);
-                    else
-                        idx = lastday ? s.bar_off + n * Fm + (int)f : (int)j + F;
-                    v[e] = lds[idx];
-                    ++j;
-                    if (++f == (uint32_t)F) {
-                        f = 0;
-                        if (++t == (uint32_t)W) { t = 0; ++row; }
-                    }
-                }
-                reinterpret_cast<f4*>(dst)[q] = f4{v[0], v[1], v[2], v[3]};
-            }
-        } else {
-            for (int j = tid; j < nf; j += kBlock) {
-                uint32_t row = fdiv((uint32_t)j, p.div_wf);
-                uint32_t kk = (uint32_t)j - row * (uint32_t)WF;
-                uint32_t t = fdiv(kk, p.div_f);
-                uint32_t f = kk - t * (uint32_t)F;
-                const int n = r0 + (int)row;
-                const bool lastday = (int)t == W - 1;
-                int idx;
-                if ((int)f == F - 1)
-                    idx = shift_w ? (lastday ? s.wp_off + n : j + F) : ((int)t == slot ? s.wp_off + n : j);
-                else
-                    idx = lastday ? s.bar_off + n * Fm + (int)f : j + F;
-                dst[j] = lds[idx];
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------- surface kernel
-// The reference contract: obs is the caller's next-day window; only channel F-1
-// is rewritten with ActionBuffer.get_all() (trading_env.py:103).
-__global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int N = p.N, W = p.W, F = p.F;
-    Scratch s = carve(lds, 0, N, F);
-    if (tid < 64) env_scalar_step(p, b, s, nullptr);
-    __syncthreads();
-    if (!p.obs) return;
-    const int slot = s.ints[1];
-    const int32_t k1 = s.ints[2];                 // updates since reset, after this step
-    const int idx = (int)((1 + (int64_t)k1) % W);
-    const bool full = (int64_t)k1 >= W - 1;
-    const float* ringb = p.ring + (size_t)b * W * N;
-    float* obs = p.obs + (size_t)b * N * W * F;
-    for (int i = tid; i < N * W; i += kBlock) {
-        const int n = (int)fdiv((uint32_t)i, p.div_w);
-        const int t = i - n * W;
-        int rs;  // ring slot feeding position t, or -1 for zero padding (weight_buffer.py:38-44)
-        if (!full) rs = t < W - idx ? -1 : t - (W - idx);
-        else rs = p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
-        float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
-        obs[((size_t)n * W + t) * F + (F - 1)] = v;
-    }
-}
-
-// ---------------------------------------------------------------- reset kernel
-__global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask) {
-    const int b = blockIdx.x;
-    if (mask && !mask[b]) return;
-    const int tid = threadIdx.x;
-    const int N = p.N, W = p.W, F = p.F;
-    if (tid == 0) {
-        p.value[b] = p.init_cash;                 // trading_env.py:28
-        p.k[b] = 0;                               // weight_buffer.py:49 idx = 1
-        p.sa[b] = 0.0;
-        p.sb[b] = 0.0;
-    }
-    float* ringb = p.ring + (size_t)b * W * N;     // weight_buffer.py:47-48 e0 in slot 0
-    for (int i = tid; i < W * N; i += kBlock) ringb[i] = i == 0 ? 1.0f : 0.0f;
-    if (!obs) return;
-    float* ob = obs + (size_t)b * N * W * F;       // trading_env.py:31-32 get_all() at idx = 1
-    for (int i = tid; i < N * W; i += kBlock) {
-        const int n = (int)fdiv((uint32_t)i, p.div_w);
-        const int t = i - n * W;
-        ob[((size_t)n * W + t) * F + (F - 1)] = (n == 0 && t == W - 1) ? 1.0f : 0.0f;
-    }
-}
-
-// ---------------------------------------------------------------- Philox + synthetic data
-__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
-        uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
-        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-}
-
-__device__ __forceinline__ double u01(uint32_t x) { return ((double)(x >> 8) + 0.5) * (1.0 / 16777216.0); }
-
-__device__ __forceinline__ void normals4(uint32_t c0, uint32_t c1, uint64_t g, uint64_t seed, double z[4]) {
-    uint32_t c[4] = {c0, c1, (uint32_t)g, (uint32_t)(g >> 32)};
-    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const double two_pi = 6.283185307179586476925286766559;
-    double r0 = sqrt(-2.0 * log(u01(c[0]))), r1 = sqrt(-2.0 * log(u01(c[2])));
-    z[0] = r0 * cos(two_pi * u01(c[1]));
-    z[1] = r0 * sin(two_pi * u01(c[1]));
-    z[2] = r1 * cos(two_pi * u01(c[3]));
-    z[3] = r1 * sin(two_pi * u01(c[3]));
-}
-
-// One thread per (env, asset): close_t = close_{t-1} exp(sigma z - sigma^2/2), OHLC
-// around it (SURVEY.md §8d synthetic inputs). series [T][B][N][4].
-__global__ void synth_series_kernel(float4* series, int T, int B, int N, int64_t env_offset,
-                                    uint64_t seed, double sigma) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)B * N) return;
-    const int b = (int)(i / N), n = (int)(i % N);
-    const uint64_t g = (uint64_t)(env_offset + b);
-    double z[4];
-    normals4(0u, (uint32_t)n, g, seed, z);
-    double close = 100.0 * exp(0.2 * z[0]);
-    for (int t = 0; t < T; ++t) {
-        normals4((uint32_t)(t + 1), (uint32_t)n, g, seed, z);
-        double cl = close * exp(sigma * z[0] - 0.5 * sigma * sigma);
-        double op = close * exp(0.3 * sigma * z[1]);
-        double hi = fmax(op, cl) * exp(fabs(0.5 * sigma * z[2]));
-        double lo = fmin(op, cl) * exp(-fabs(0.5 * sigma * z[3]));
-        series[((size_t)t * B + b) * N + n] = make_float4((float)op, (float)hi, (float)lo, (float)cl);
-        close = cl;
-    }
-}
-
-// One thread per (t, env): softmax of N(0,1) logits over the N assets.
-__global__ void synth_actions_kernel(float* actions, int T, int B, int N, int64_t env_offset, uint64_t seed) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)T * B) return;
-    const int t = (int)(i / B), b = (int)(i % B);
-    const uint64_t g = (uint64_t)(env_offset + b);
-    float* out = actions + (size_t)i * N;
-    double mx = -INFINITY;
-    for (int n = 0; n < N; ++n) {
-        double z[4];
-        normals4((uint32_t)t, 0x80000000u | (uint32_t)n, g, seed, z);
-        out[n] = (float)z[0];
-        mx = fmax(mx, z[0]);
-    }
-    double sum = 0.0;
-    for (int n = 0; n < N; ++n) {
-        double z[4];
-        normals4((uint32_t)t, 0x80000000u | (uint32_t)n, g, seed, z);
-        sum += exp(z[0] - mx);
-    }
-    for (int n = 0; n < N; ++n) {
-        double z[4];
-        normals4((uint32_t)t, 0x80000000u | (uint32_t)n, g, seed, z);
-        out[n] = (float)(exp(z[0] - mx) / sum);
-    }
-}
-
-__global__ void window_init_kernel(float* obs, const float4* series, int B, int N, int W, int F) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over B*N*W
-    if (i >= (int64_t)B * N * W) return;
-    const int t = (int)(i % W);
-    const int64_t bn = i / W;
-    const int n = (int)(bn % N), b = (int)(bn / N);
-    float4 v = series[((size_t)t * B + b) * N + n];
-    float* o = obs + (size_t)i * F;
-    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    for (int f = 4; f < F; ++f) o[f] = 0.0f;
-}
-
-// ---------------------------------------------------------------- GAE / moments
-// One thread per env walks its column of the [T, B] rollout backwards; for a fixed
-// t the B threads touch B consecutive floats, so every access is coalesced.
-__global__ void gae_kernel(const float* r, const float* v, const uint8_t* dones, float* adv, float* ret,
-                           int T, int B, float gamma, float lam) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    double a = 0.0;
-    for (int t = T - 1; t >= 0; --t) {
-        size_t i = (size_t)t * B + b;
-        double nd = dones ? (dones[i] ? 0.0 : 1.0) : 1.0;
-        double vt = (double)v[i];
-        double delta = (double)r[i] + (double)gamma * nd * (double)v[i + B] - vt;
-        a = delta + (double)gamma * (double)lam * nd * a;
-        adv[i] = (float)a;
-        ret[i] = (float)(a + vt);
-    }
-}
-
-constexpr int kMomBlocks = 1024;
-__device__ double g_mom_partial[kMomBlocks * 3];
-
-__global__ __launch_bounds__(kBlock) void moments_partial_kernel(const float* x, int64_t n) {
-    __shared__ double sh[2][kBlock / 64];
-    double s = 0.0, q = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        double v = (double)x[i];
-        s += v;
-        q += v * v;
-    }
-    for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sh[0][w] = s; sh[1][w] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double ts = 0.0, tq = 0.0;
-        for (int i = 0; i < kBlock / 64; ++i) { ts += sh[0][i]; tq += sh[1][i]; }
-        g_mom_partial[blockIdx.x * 3 + 0] = ts;
-        g_mom_partial[blockIdx.x * 3 + 1] = tq;
-    }
-}
-
-__global__ void moments_final_kernel(int nblocks, int64_t n, double* out) {
-    if (threadIdx.x != 0) return;
-    double s = 0.0, q = 0.0;
-    for (int i = 0; i < nblocks; ++i) { s += g_mom_partial[i * 3 + 0]; q += g_mom_partial[i * 3 + 1]; }
-    out[0] = (double)n;
-    out[1] = s;
-    out[2] = q;
-}
-
-}  // namespace
-
-// ================================================================ host side / C ABI
 struct pmenv {
     pmenv_cfg cfg;
     int device;
-    void* state;          // one allocation: value | sa | sb | k | ring | nonfinite
+    void* state;          // value | stat_a | stat_b | counter | ring | nonfinite | last_close | w_new
     size_t state_bytes;
+    bool owns_state;
     double* value;
     double* sa;
     double* sb;
     int32_t* k;
     float* ring;
+    float* last_close;
+    float* w_new;
     unsigned long long* nonfinite;
+    // LDS single-launch fallback geometry
     int rows_per_tile, tile_floats;
     bool vec;
-    bool owns_state;
-    size_t lds_advance, lds_surface;
+    size_t lds_tile, lds_surface;
+    // two-launch streaming path geometry
+    bool streaming;       // scalar_step_kernel + advance_rows_kernel
+    int unit_rows, units_per_env, stream_vec;          // in-place advance
+    int unit_rows_db, units_per_env_db, stream_vec_db; // double-buffered advance (obs_out)
+    int scalar_scratch_floats;
+    int ablate;           // PMENV_ABLATE timing-only variants of advance_rows_kernel (0 = product)
+    size_t lds_scalar, lds_stream;
     char err[512];
 };
 
@@ -606,9 +64,7 @@ struct DeviceGuard {
     int prev = -1;
     bool changed = false;
     explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
-            changed = hipSetDevice(dev) == hipSuccess;
-        }
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) changed = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
         if (changed) (void)hipSetDevice(prev);
@@ -625,13 +81,18 @@ StepParams base_params(const pmenv* h) {
     p.ret_mode = c.ret_mode; p.mu_max_iter = c.mu_max_iter;
     p.rows_per_tile = h->rows_per_tile;
     p.tile_floats = h->tile_floats;
+    p.unit_rows = h->unit_rows;
+    p.units_per_env = h->units_per_env;
     p.init_cash = c.init_cash; p.commission = c.commission; p.scale = c.reward_scale;
     p.rf = c.risk_free_rate; p.eta = c.sharpe_eta; p.mu_tol = c.mu_tol;
-    p.value = h->value; p.k = h->k; p.ring = h->ring; p.sa = h->sa; p.sb = h->sb;
+    p.value = h->value; p.k = h->k; p.ring = h->ring; p.last_close = h->last_close;
+    p.w_new = h->w_new;
+    p.sa = h->sa; p.sb = h->sb;
     p.nonfinite = h->nonfinite;
     p.div_wf = make_fastdiv((uint32_t)(c.window * c.features));
     p.div_f = make_fastdiv((uint32_t)c.features);
     p.div_w = make_fastdiv((uint32_t)c.window);
+    p.div_units = make_fastdiv((uint32_t)(h->units_per_env > 0 ? h->units_per_env : 1));
     return p;
 }
 
@@ -644,6 +105,71 @@ int check_launch(pmenv* h, const char* what) {
         return PMENV_ERR_HIP;
     }
     return PMENV_OK;
+}
+
+// Geometry of the streaming path: units of R whole asset rows per 512-thread
+// workgroup, R*W*F floats <= 2048*V (V float4 per thread) and R*W*F % 4 == 0 so
+// every unit starts 16-B aligned. Measured on MI355X at the BASELINE shape
+// (tools/ab_advance.py, interleaved rounds in one process): in place, 16 KiB units
+// (V = 2) beat 32 KiB (V = 4) by ~3 % and 8 KiB (V = 1) by ~20 %; double-buffered,
+// 32 KiB units win by ~3 %. `v_order` lists V in preference order. Returns false
+// when the shape needs the LDS fallback.
+bool plan_streaming(const pmenv_cfg& c, const int* v_order, int* unit_rows, int* vec_per_thread) {
+    const int64_t WF = (int64_t)c.window * c.features;
+    if (c.features != 5 || ((int64_t)c.num_assets * WF) % 4 != 0) return false;
+    int align = 1;                       // rows per unit must be a multiple of this
+    while ((align * WF) % 4 != 0) ++align;
+    int want = 0;
+    if (const char* knob = getenv("PMENV_UNIT_ROWS")) want = atoi(knob);   // tuning knob
+    for (int vi = 0; vi < 3; ++vi) {
+        const int V = v_order[vi];
+        const int64_t cap = (int64_t)kStreamBlock * 4 * V;
+        int R = (int)(cap / WF);
+        if (R >= c.num_assets) R = c.num_assets;
+        else R -= R % align;
+        if (R < 1 || (int64_t)R * WF > cap) continue;
+        if (want > 0) {
+            if (want > R) continue;
+            if (want != c.num_assets && want % align) return false;
+            R = want;
+        }
+        *unit_rows = R;
+        *vec_per_thread = V;
+        return true;
+    }
+    return false;
+}
+
+template <int V, int ABL>
+void launch_advance_v(const StepParams& p, unsigned grid, hipStream_t stream) {
+    if (p.obs_out == p.obs)
+        advance_rows_kernel<kStreamBlock, V, true, ABL><<<grid, kStreamBlock, 0, stream>>>(p);
+    else
+        advance_rows_kernel<kStreamBlock, V, false, ABL><<<grid, kStreamBlock, 0, stream>>>(p);
+}
+
+template <int ABL>
+void launch_advance_a(int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
+    if (vec == 1) launch_advance_v<1, ABL>(p, grid, stream);
+    else if (vec == 2) launch_advance_v<2, ABL>(p, grid, stream);
+    else launch_advance_v<4, ABL>(p, grid, stream);
+}
+
+// ablation builds are selected only by the PMENV_ABLATE knob (timing studies)
+void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
+    const bool db = p.obs_out != p.obs;
+    p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
+    p.units_per_env = db ? h->units_per_env_db : h->units_per_env;
+    p.div_units = make_fastdiv((uint32_t)p.units_per_env);
+    const int vec = db ? h->stream_vec_db : h->stream_vec;
+    const unsigned grid = (unsigned)(h->cfg.num_envs * p.units_per_env);
+    switch (h->ablate) {
+    case 1: launch_advance_a<1>(vec, p, grid, stream); break;
+    case 2: launch_advance_a<2>(vec, p, grid, stream); break;
+    case 3: launch_advance_a<3>(vec, p, grid, stream); break;
+    case 7: launch_advance_a<7>(vec, p, grid, stream); break;
+    default: launch_advance_a<0>(vec, p, grid, stream);
+    }
 }
 
 }  // namespace
@@ -681,25 +207,27 @@ int pmenv_get_cfg(const pmenv* h, pmenv_cfg* out) {
     return PMENV_OK;
 }
 
-int pmenv_state_layout(const pmenv_cfg* cfg, size_t off[6]) {
+int pmenv_state_layout(const pmenv_cfg* cfg, size_t off[PMENV_STATE_FIELDS]) {
     if (!cfg || !off || cfg->num_envs < 1 || cfg->num_assets < 1 || cfg->window < 1) return PMENV_ERR_ARG;
-    const size_t B = (size_t)cfg->num_envs;
-    const size_t ring_elems = B * (size_t)cfg->window * (size_t)cfg->num_assets;
+    const size_t B = (size_t)cfg->num_envs, N = (size_t)cfg->num_assets;
+    const size_t ring_elems = B * (size_t)cfg->window * N;
     auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
     size_t o = 0;
-    off[0] = o; o = up16(o + B * 8);
-    off[1] = o; o = up16(o + B * 8);
-    off[2] = o; o = up16(o + B * 8);
-    off[3] = o; o = up16(o + B * 4);
-    off[4] = o; o = up16(o + ring_elems * 4);
-    off[5] = o;
+    off[0] = o; o = up16(o + B * 8);           // value
+    off[1] = o; o = up16(o + B * 8);           // stat_a
+    off[2] = o; o = up16(o + B * 8);           // stat_b
+    off[3] = o; o = up16(o + B * 4);           // counter
+    off[4] = o; o = up16(o + ring_elems * 4);  // ring
+    off[5] = o; o = up16(o + 8);               // nonfinite
+    off[6] = o; o = up16(o + B * N * 4);       // last_close
+    off[7] = o;                                // w_new
     return PMENV_OK;
 }
 
 size_t pmenv_state_bytes_for(const pmenv_cfg* cfg) {
-    size_t off[6];
+    size_t off[PMENV_STATE_FIELDS];
     if (pmenv_state_layout(cfg, off) != PMENV_OK) return 0;
-    return off[5] + 16;
+    return (off[7] + (size_t)cfg->num_envs * cfg->num_assets * 4 + 15) / 16 * 16;
 }
 
 int pmenv_create(const pmenv_cfg* cfg, int device, pmenv** out) {
@@ -731,8 +259,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         return fail(PMENV_ERR_ARG);
     }
     if (c.reward_kind < 0 || c.reward_kind > 3 || c.norm_mode < 0 || c.norm_mode > 1 || c.ring_mode < 0 ||
-        c.ring_mode > 1 || c.ret_mode < 0 || c.ret_mode > 1 || c.mu_max_iter < 0 || c.commission < 0.0 ||
-        c.commission >= 1.0) {
+        c.ring_mode > 1 || c.ret_mode < 0 || c.ret_mode > 1 || c.mu_max_iter < 0 || !(c.commission >= 0.0) ||
+        !(c.commission < 1.0)) {
         set_err(h, "invalid mode/commission value in cfg");
         return fail(PMENV_ERR_ARG);
     }
@@ -745,7 +273,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         set_err(h, "per-env obs block too large");
         return fail(PMENV_ERR_ARG);
     }
-    // tile geometry: whole asset rows, 16-B granular when every env block is
+    // LDS fallback tile geometry: whole asset rows, 16-B granular when every env block is
     int R = (int)(kTileFloats / WF);
     if (R > c.num_assets) R = c.num_assets;
     bool vec = ((int64_t)c.num_assets * WF) % 4 == 0;
@@ -756,17 +284,37 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->rows_per_tile = R;
     h->vec = vec;
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
-    h->lds_advance = scratch_bytes(h->tile_floats, c.num_assets, c.features);
+    h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
-    if (h->lds_advance > 160 * 1024) {
-        set_err(h, "num_assets %d needs %zu B of LDS (> 160 KiB)", c.num_assets, h->lds_advance);
+    // streaming geometry
+    static const int kInplaceOrder[3] = {2, 4, 1}, kDoubleOrder[3] = {4, 2, 1};
+    h->streaming = plan_streaming(c, kInplaceOrder, &h->unit_rows, &h->stream_vec) &&
+                   plan_streaming(c, kDoubleOrder, &h->unit_rows_db, &h->stream_vec_db);
+    if (const char* knob = getenv("PMENV_ADVANCE"))   // A/B knob: force the single-launch LDS kernel
+        if (!strcmp(knob, "lds")) h->streaming = false;
+    if (const char* knob = getenv("PMENV_ABLATE")) h->ablate = atoi(knob);
+    if (h->streaming) {
+        h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
+        h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
+        h->lds_stream = 0;
+    }
+    h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
+    h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
+    if (h->lds_tile > 160 * 1024 || h->lds_scalar > 160 * 1024) {
+        set_err(h, "num_assets %d needs more than 160 KiB of LDS", c.num_assets);
+        return fail(PMENV_ERR_ARG);
+    }
+    if ((int64_t)c.num_envs * (h->streaming ? (h->units_per_env > h->units_per_env_db ? h->units_per_env
+                                                                                    : h->units_per_env_db)
+                                               : 1) >= (1ll << 31)) {
+        set_err(h, "too many envs for one launch");
         return fail(PMENV_ERR_ARG);
     }
 
     DeviceGuard g(device);
-    size_t off[6];
+    size_t off[PMENV_STATE_FIELDS];
     pmenv_state_layout(&c, off);
-    h->state_bytes = off[5] + 16;
+    h->state_bytes = pmenv_state_bytes_for(&c);
     if (state) {
         if (state_bytes < h->state_bytes || ((uintptr_t)state & 15u)) {
             set_err(h, "caller state buffer too small (%zu < %zu) or not 16-B aligned", state_bytes, h->state_bytes);
@@ -790,16 +338,18 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->k = (int32_t*)(base + off[3]);
     h->ring = (float*)(base + off[4]);
     h->nonfinite = (unsigned long long*)(base + off[5]);
-    hipError_t e;
-    if (hipFuncSetAttribute((const void*)step_advance_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)h->lds_advance) != hipSuccess ||
-        hipFuncSetAttribute((const void*)step_advance_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)h->lds_advance) != hipSuccess ||
-        hipFuncSetAttribute((const void*)step_surface_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)h->lds_surface) != hipSuccess) {
-        (void)hipGetLastError();  // attribute is advisory below 64 KiB
-    }
-    e = hipMemset(h->nonfinite, 0, 16);
+    h->last_close = (float*)(base + off[6]);
+    h->w_new = (float*)(base + off[7]);
+    const struct { const void* fn; size_t lds; } attrs[] = {
+        {(const void*)step_advance_lds_kernel<true>, h->lds_tile},
+        {(const void*)step_advance_lds_kernel<false>, h->lds_tile},
+        {(const void*)step_surface_kernel, h->lds_surface},
+        {(const void*)scalar_step_kernel, h->lds_scalar},
+    };
+    for (const auto& a : attrs)   // only needed above 64 KiB; failures surface at launch
+        if (hipFuncSetAttribute(a.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds) != hipSuccess)
+            (void)hipGetLastError();
+    hipError_t e = hipMemset(h->state, 0, h->state_bytes);
     if (e != hipSuccess) {
         set_err(h, "hipMemset failed: %s", hipGetErrorString(e));
         return fail(PMENV_ERR_HIP);
@@ -846,18 +396,51 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
     p.action = a->action; p.prices = a->prices; p.bar = a->bar; p.obs = a->obs;
+    p.obs_out = a->obs_out ? a->obs_out : a->obs;
+    if (a->obs_out && a->bar) {
+        const size_t bytes = (size_t)h->cfg.num_envs * h->cfg.num_assets * h->cfg.window * h->cfg.features * 4;
+        const char *o0 = (const char*)a->obs, *o1 = (const char*)a->obs_out;
+        if (!aligned4(a->obs_out) || (o1 < o0 + bytes && o0 < o1 + bytes)) {
+            set_err(h, "obs_out must be 4-byte aligned and must not overlap obs");
+            return PMENV_ERR_ARG;
+        }
+    }
     p.reward = a->reward; p.ret = a->ret; p.weights = a->weights;
     const int B = h->cfg.num_envs;
-    if (a->bar) {
-        const bool vec = h->vec && (((uintptr_t)a->obs & 15u) == 0);
-        if (vec)
-            step_advance_kernel<true><<<B, kBlock, h->lds_advance, stream>>>(p);
-        else
-            step_advance_kernel<false><<<B, kBlock, h->lds_advance, stream>>>(p);
-        return check_launch(h, "step_advance_kernel");
+    if (!a->bar) {
+        if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
+        step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
+        return check_launch(h, "step_surface_kernel");
     }
-    step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
-    return check_launch(h, "step_surface_kernel");
+    const bool obs16 = (((uintptr_t)a->obs | (uintptr_t)p.obs_out) & 15u) == 0;
+    if (h->streaming && obs16) {
+        const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        if (ph & PMENV_PHASE_SCALAR) {
+            const int N = h->cfg.num_assets;
+            if (N <= 32) {
+                const int waves = (B + 1) / 2;
+                scalar_step_reg_kernel<32><<<(waves + 3) / 4, 256, 0, stream>>>(p);
+            } else if (N <= 64) {
+                scalar_step_reg_kernel<64><<<(B + 3) / 4, 256, 0, stream>>>(p);
+            } else {
+                scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar,
+                                     stream>>>(p, h->scalar_scratch_floats);
+            }
+            int rc = check_launch(h, "scalar_step_kernel");
+            if (rc) return rc;
+        }
+        if (ph & PMENV_PHASE_ADVANCE) {
+            launch_advance(h, p, stream);
+            return check_launch(h, "advance_rows_kernel");
+        }
+        return PMENV_OK;
+    }
+    if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single-launch path: all done in the scalar phase
+    if (h->vec && obs16)
+        step_advance_lds_kernel<true><<<B, kBlock, h->lds_tile, stream>>>(p);
+    else
+        step_advance_lds_kernel<false><<<B, kBlock, h->lds_tile, stream>>>(p);
+    return check_launch(h, "step_advance_lds_kernel");
 }
 
 int pmenv_step(pmenv* h, const float* action, const float* prices, const float* bar, float* obs, float* reward,
@@ -872,6 +455,11 @@ double* pmenv_value(pmenv* h) { return h ? h->value : nullptr; }
 float* pmenv_ring(pmenv* h) { return h ? h->ring : nullptr; }
 int32_t* pmenv_counter(pmenv* h) { return h ? h->k : nullptr; }
 size_t pmenv_state_bytes(const pmenv* h) { return h ? h->state_bytes : 0; }
+
+const char* pmenv_step_path(const pmenv* h) {
+    if (!h) return "";
+    return h->streaming ? "scalar_step_kernel+advance_rows_kernel" : "step_advance_lds_kernel";
+}
 
 int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
     if (!h || !dst) return PMENV_ERR_ARG;
@@ -905,7 +493,7 @@ int pmenv_synth_series(float* series, int32_t T, int32_t B, int32_t N, int64_t e
     if (!series || T < 1 || B < 1 || N < 1 || ((uintptr_t)series & 15u)) return PMENV_ERR_ARG;
     const int64_t threads = (int64_t)B * N;
     synth_series_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
-        reinterpret_cast<float4*>(series), T, B, N, env_offset, seed, (double)sigma);
+        reinterpret_cast<f4*>(series), T, B, N, env_offset, seed, (double)sigma);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -922,7 +510,7 @@ int pmenv_window_init(float* obs, const float* series, int32_t B, int32_t N, int
     if (!obs || !series || B < 1 || N < 1 || W < 1 || F != 5 || ((uintptr_t)series & 15u)) return PMENV_ERR_ARG;
     const int64_t threads = (int64_t)B * N * W;
     window_init_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
-        obs, reinterpret_cast<const float4*>(series), B, N, W, F);
+        obs, reinterpret_cast<const f4*>(series), B, N, W, F);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -935,9 +523,9 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
 
 int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream) {
     if (!x || !out || n < 0) return PMENV_ERR_ARG;
-    int64_t want = (n + kBlock * 4 - 1) / (kBlock * 4);
+    int64_t want = (n + kMomBlock * 4 - 1) / (kMomBlock * 4);
     int blocks = (int)(want < 1 ? 1 : (want > kMomBlocks ? kMomBlocks : want));
-    moments_partial_kernel<<<blocks, kBlock, 0, stream>>>(x, n);
+    moments_partial_kernel<<<blocks, kMomBlock, 0, stream>>>(x, n);
     moments_final_kernel<<<1, 64, 0, stream>>>(blocks, n, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }

@@ -20,6 +20,7 @@ REWARD_KINDS = {"log_returns": 0, "returns": 1, "sharpe_ratio": 2, "diff_sharpe"
 NORM_MODES = {"and": 0, "or": 1}
 RING_MODES = {"storage": 0, "chrono": 1}
 RET_MODES = {"gross": 0, "net": 1}
+STATE_FIELDS = 8   # value, stat_a, stat_b, counter, ring, nonfinite, last_close, w_new
 STATUS = {0: "OK", -1: "ERR_ARG", -2: "ERR_SHAPE", -3: "ERR_HIP", -4: "ERR_ALIGN"}
 
 
@@ -37,9 +38,13 @@ class PmenvCfg(ctypes.Structure):
 class PmenvStepArgs(ctypes.Structure):
     _fields_ = [
         ("action", ctypes.c_void_p), ("prices", ctypes.c_void_p), ("bar", ctypes.c_void_p),
-        ("obs", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("ret", ctypes.c_void_p),
-        ("weights", ctypes.c_void_p),
+        ("obs", ctypes.c_void_p), ("obs_out", ctypes.c_void_p), ("reward", ctypes.c_void_p),
+        ("ret", ctypes.c_void_p), ("weights", ctypes.c_void_p), ("phases", ctypes.c_uint32),
     ]
+
+
+PHASE_SCALAR = 1
+PHASE_ADVANCE = 2
 
 
 # (name, restype, argtypes) for every symbol include/pmenv.h declares
@@ -62,6 +67,7 @@ SIGNATURES = [
     ("pmenv_ring", _P, [_P]),
     ("pmenv_counter", _P, [_P]),
     ("pmenv_state_bytes", _SZ, [_P]),
+    ("pmenv_step_path", ctypes.c_char_p, [_P]),
     ("pmenv_get_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_set_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_nonfinite_count", ctypes.c_int, [_P, ctypes.POINTER(_U64), _P]),

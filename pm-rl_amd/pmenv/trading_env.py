@@ -96,7 +96,7 @@ class TradingEnv:
         nbytes = self._lib.pmenv_state_bytes_for(ctypes.byref(self._c))
         if nbytes == 0:
             raise ValueError("invalid env shape")
-        off = (ctypes.c_size_t * 6)()
+        off = (ctypes.c_size_t * _abi.STATE_FIELDS)()
         _abi.check(self._lib.pmenv_state_layout(ctypes.byref(self._c), off), None, "pmenv_state_layout")
         self._state = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
         h = ctypes.c_void_p()
@@ -112,6 +112,8 @@ class TradingEnv:
         self._counter = s[off[3]:off[3] + 4 * B].view(torch.int32)
         self._ring = s[off[4]:off[4] + 4 * B * W * N].view(torch.float32).view(B, W, N)
         self._nonfinite = s[off[5]:off[5] + 8].view(torch.int64)
+        self._last_close = s[off[6]:off[6] + 4 * B * N].view(torch.float32).view(B, N)
+        self._w_new = s[off[7]:off[7] + 4 * B * N].view(torch.float32).view(B, N)
         self.weights = RingView(self)
         self.track_info = track_info
         self._unbatched = False
@@ -181,7 +183,7 @@ class TradingEnv:
             self._reset_info()
         return features
 
-    def step(self, action, features, prices=None, bar=None):
+    def step(self, action, features, prices=None, bar=None, out=None):
         """trading_env.py:44-105 for all B envs in one kernel launch.
 
         prices given, bar None : the reference contract — `features` is the next
@@ -190,6 +192,10 @@ class TradingEnv:
                                  the previous reset/step) is advanced one day in
                                  place and `bar` [B, N, F-1] appended; prices
                                  default to bar.close / window[W-1].close.
+        out (fused path only)  : write the advanced window into `out` instead of
+                                 in place (double-buffered windows, as the
+                                 reference's data path hands the env a fresh
+                                 window every day); returns (r, out).
         Returns (r, features); r is f32 [B] (0-dim for unbatched single-env input).
         """
         cfg = self.cfg
@@ -208,6 +214,12 @@ class TradingEnv:
         args.prices = p.data_ptr() if p is not None else None
         args.bar = br.data_ptr() if br is not None else None
         args.obs = features.data_ptr()
+        if out is not None:
+            if bar is None:
+                raise ValueError("out= applies to the fused window advance (bar=...) only")
+            if self._obs_check(out, "out") != unb:
+                raise ValueError("out must have the same shape as features")
+            args.obs_out = out.data_ptr()
         args.reward = r.data_ptr()
         ret = w = None
         if self.track_info:
@@ -223,11 +235,11 @@ class TradingEnv:
             self.info["returns"].append(ret)
             self.info["rewards"].append(r)
         self._unbatched = unb
-        return (r[0] if unb else r), features
+        return (r[0] if unb else r), (features if out is None else out)
 
-    def advance(self, action, features, bar, prices=None):
+    def advance(self, action, features, bar, prices=None, out=None):
         """Fused step: window advance + bar append (see step)."""
-        return self.step(action, features, prices=prices, bar=bar)
+        return self.step(action, features, prices=prices, bar=bar, out=out)
 
     # ------------------------------------------------------------------ state
     def state_dict(self):
@@ -239,6 +251,11 @@ class TradingEnv:
         if st.numel() != self._state.numel():
             raise ValueError("state blob size mismatch (different env shape)")
         self._state.copy_(st.to(self.device))
+
+    @property
+    def step_path(self):
+        """Kernels the fused advance launches for this shape (diagnostics)."""
+        return self._lib.pmenv_step_path(self._h).decode()
 
     def nonfinite_count(self):
         return int(self._nonfinite.item())

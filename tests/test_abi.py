@@ -57,13 +57,13 @@ def test_state_layout_is_consistent():
     lib = _abi.load()
     for B, N, W in [(1, 5, 50), (4096, 30, 50), (3, 7, 6)]:
         c = EnvConfig(num_envs=B, num_assets=N, window=W).to_c()
-        off = (ctypes.c_size_t * 6)()
+        off = (ctypes.c_size_t * _abi.STATE_FIELDS)()
         assert lib.pmenv_state_layout(ctypes.byref(c), off) == 0
         up = lambda x: (x + 15) // 16 * 16  # noqa: E731
         assert list(off)[:4] == [0, up(8 * B), 2 * up(8 * B), 3 * up(8 * B)]
         assert all(o % 16 == 0 for o in off)
-        assert off[5] - off[4] >= 4 * B * W * N
-        assert lib.pmenv_state_bytes_for(ctypes.byref(c)) == off[5] + 16
+        assert off[5] - off[4] >= 4 * B * W * N and off[6] - off[5] >= 8 and off[7] - off[6] >= 4 * B * N
+        assert lib.pmenv_state_bytes_for(ctypes.byref(c)) >= off[7] + 4 * B * N
 
 
 def test_create_rejects_bad_config_without_touching_the_gpu():

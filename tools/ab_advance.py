@@ -1,0 +1,93 @@
+"""A/B the fused-step kernel variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24). Variant = PMENV_ADVANCE at env creation."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
+import torch  # noqa: E402
+from pmenv import TradingEnv, synth, _abi  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--variants", default="lds,reg256,reg512")
+ap.add_argument("--envs", type=int, default=65536)
+ap.add_argument("--assets", type=int, default=30)
+ap.add_argument("--window", type=int, default=50)
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--steps", type=int, default=40)
+ap.add_argument("--H", type=int, default=64)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+B, N, W = a.envs, a.assets, a.window
+lib = _abi.load()
+ser = synth.series(a.H + W, B, N, device=dev)
+act = synth.actions(a.H, B, N, device=dev)
+envs = {}
+for v in a.variants.split(","):
+    # "lds" -> single-launch LDS kernel, "uR" -> streaming with R rows per unit, else default
+    # "uR" -> R rows per unit, "aX" -> ablation X, combinable as "u16a3"; suffix "o" -> double-buffered
+    for knob in ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE"):
+        os.environ.pop(knob, None)
+    import re
+    m = re.fullmatch(r"(?:u(\d+))?(?:a(\d+))?o?", v)
+    if v != "stream" and m and (m.group(1) or m.group(2)):
+        if m.group(1):
+            os.environ["PMENV_UNIT_ROWS"] = m.group(1)
+        if m.group(2):
+            os.environ["PMENV_ABLATE"] = m.group(2)
+    elif v != "stream":
+        os.environ["PMENV_ADVANCE"] = v
+    obs = synth.window_from_series(ser, W)
+    e = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
+    e.reset(obs)
+    print(v, e.step_path, file=sys.stderr)
+    envs[v] = (e, obs, torch.empty(B, device=dev), obs.clone() if v.endswith("o") else None)
+for knob in ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE"):
+    os.environ.pop(knob, None)
+stream = torch.cuda.current_stream()
+sp = ctypes.c_void_p(stream.cuda_stream)
+times = {v: [] for v in envs}
+t_global = {v: 0 for v in envs}
+bytes_step = (8 * N * W * 5 + 20) * B
+for r in range(a.rounds):
+    for v, (e, obs, rew, obs2) in envs.items():
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record(stream)
+        for i in range(a.steps):
+            t = t_global[v] % a.H
+            t_global[v] += 1
+            args = _abi.PmenvStepArgs()
+            args.action = act[t].data_ptr()
+            args.bar = ser[W + t].data_ptr()
+            src, dst = (obs, obs2) if (obs2 is not None and t_global[v] % 2) else (obs2, obs) if obs2 is not None else (obs, None)
+            args.obs = src.data_ptr()
+            args.obs_out = dst.data_ptr() if dst is not None else None
+            args.reward = rew.data_ptr()
+            rc = lib.pmenv_step_ex(e._h, ctypes.byref(args), sp)
+            assert rc == 0
+        s1.record(stream)
+        torch.cuda.synchronize()
+        if r > 0:
+            times[v].append(s0.elapsed_time(s1) / a.steps * 1e3)
+# all variants saw identical inputs from identical states: results must agree
+ref = None
+for v, (e, obs, rew, obs2) in envs.items():
+    if obs2 is not None and t_global[v] % 2:
+        obs = obs2                    # latest window of a double-buffered run
+    if "a" in v and v != "lds":
+        continue                      # ablation builds compute wrong windows by design
+    if ref is None:
+        ref = (obs, rew, e.value)
+    else:
+        assert torch.equal(obs, ref[0]), f"{v}: obs differs"
+        assert torch.equal(rew, ref[1]), f"{v}: reward differs"
+        assert torch.equal(e.value, ref[2]), f"{v}: value differs"
+out = {}
+for v, ts in times.items():
+    med = statistics.median(ts)
+    out[v] = {"median_us": med, "min_us": min(ts), "GBs": bytes_step / med / 1e3, "frac_8TBs": bytes_step / med / 1e3 / 8000}
+print(json.dumps({"B": B, "N": N, "W": W, "variants": out}, indent=1))
