@@ -145,10 +145,17 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") over xGMI; PMENV_DIST_BACKEND=gloo lets several ranks share
+        # one GPU for functional rehearsal (RCCL refuses two ranks on one device)
+        backend = os.environ.get("PMENV_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from pmenv import TradingEnv, synth, _abi
     lib = _abi.load()
@@ -227,7 +234,8 @@ def main():
                    "ms_per_step": ip_el / args.inplace_steps * 1e3, "advance_kernel_avg_us": ip_k * 1e6}
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_avg_s = float(t[0]), float(t[1])
     nonfinite = env.nonfinite_count()
