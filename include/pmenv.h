@@ -215,6 +215,29 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones,
  * (the only cross-GPU exchange: a 24-byte all-reduce over xGMI). */
 int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream);
 
+/* ---- trainer-side twin: the differentiable batched portfolio reward of the
+ * PG / A2C agents (agent/pg/pg.py:40-82 `_reward`, agent/a2c.py/a2c.py:40-82 `_loss`
+ * = -_reward), forward and backward in f64 over a [B, N] batch. ---- */
+typedef enum pmenv_batch_norm {
+    PMENV_BNORM_GLOBAL_OR = 0, /* reference: softmax over assets iff !isclose(sum over the WHOLE batch, 1)
+                                  OR min < 0 (pg.py:52) */
+    PMENV_BNORM_ROW_OR = 1,    /* the same decision per row */
+    PMENV_BNORM_NONE = 2
+} pmenv_batch_norm;
+
+/* f64 scratch the forward fills and the backward reads: (6*B + 8) * 8 bytes. */
+size_t pmenv_batch_reward_workspace(int32_t B);
+/* a, p [B, N]; v_prev [B] (the _v of pg.py); reward_kind LOG_RETURN / RETURN / SHARPE
+ * (batch mean / std, pg.py:80); writes reward_out[0] (device) and optionally the
+ * per-row gross returns ret_out [B]. */
+int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                               int32_t reward_kind, int32_t norm, double scale, double* work,
+                               float* reward_out, float* ret_out, hipStream_t stream);
+/* grad_a [B, N] = grad_out[0] * dR/da (grad_out is a device scalar). */
+int pmenv_batch_reward_backward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                                int32_t reward_kind, double scale, const double* work,
+                                const float* grad_out, float* grad_a, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,9 @@ def load():
         lib.or_gae.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float]
         lib.or_moments.argtypes = [_P, ctypes.c_int64, _P]
         lib.or_philox4x32.argtypes = [ctypes.c_uint32] * 6 + [_P]
+        lib.or_batch_reward.restype = ctypes.c_double
+        lib.or_batch_reward.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_double, _P, _P]
         lib.or_synth_series.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                         ctypes.c_uint64, ctypes.c_float]
         lib.or_synth_actions.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
@@ -140,3 +143,22 @@ def synth_actions(T, B, N, env_offset=0, seed=43):
     out = np.empty((T, B, N), np.float32)
     load().or_synth_actions(_p(out), T, B, N, env_offset, seed)
     return out
+
+
+BATCH_REWARD_KINDS = {"log_returns": 0, "returns": 1, "sharpe_ratio": 2}
+BATCH_NORMS = {"global_or": 0, "row_or": 1, "none": 2}
+
+
+def batch_reward(a, v_prev, p, reward="log_returns", norm="global_or", scale=1.0):
+    """agent/pg/pg.py:40-82 restated: returns (R, ret [B], dR/da [B, N])."""
+    a = _f32(a)
+    B = a.shape[0]
+    a = a.reshape(B, -1)
+    N = a.shape[1]
+    v = _f32(v_prev).reshape(B)
+    pp = _f32(p).reshape(B, N)
+    ret = np.empty(B, np.float32)
+    grad = np.empty((B, N), np.float32)
+    R = load().or_batch_reward(_p(a), _p(v), _p(pp), B, N, BATCH_REWARD_KINDS[reward], BATCH_NORMS[norm],
+                               float(scale), _p(ret), _p(grad))
+    return R, ret, grad

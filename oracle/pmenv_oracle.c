@@ -255,6 +255,69 @@ void or_moments(const float* x, int64_t n, double* out) {
     out[0] = (double)n; out[1] = s; out[2] = q;
 }
 
+/* Batched trainer reward: agent/pg/pg.py:40-82 `_reward`, written straight from the
+ * reference text in f64; the gradient is the hand-derived chain rule of the same
+ * expression (checked against torch autograd of the reference in the tests). */
+double or_batch_reward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                       int32_t kind, int32_t norm, double scale, float* ret_out, float* grad_a) {
+    double tot = 0.0, mn = INFINITY;
+    int nan_seen = 0;
+    for (int64_t i = 0; i < (int64_t)B * N; ++i) {
+        tot += a[i];
+        if (isnan(a[i])) nan_seen = 1;
+        if (a[i] < mn) mn = a[i];
+    }
+    if (nan_seen) mn = NAN;
+    /* :52 if not isclose(sum(a), 1, atol=1e-6) or min(a) < 0: a = softmax(a, dim=1) */
+    int glob = !(fabs(tot - 1.0) <= 1e-6 + 1e-5) || mn < 0.0;
+    double* w = (double*)malloc(sizeof(double) * (size_t)B * N);
+    double* ret = (double*)malloc(sizeof(double) * (size_t)B);
+    int* nb = (int*)malloc(sizeof(int) * (size_t)B);
+    for (int b = 0; b < B; ++b) {
+        const float* ab = a + (size_t)b * N;
+        double rs = 0.0, rmn = INFINITY, mx = -INFINITY;
+        int rn = 0;
+        for (int n = 0; n < N; ++n) {
+            rs += ab[n];
+            if (isnan(ab[n])) rn = 1;
+            if (ab[n] < rmn) rmn = ab[n];
+            if (ab[n] > mx) mx = ab[n];
+        }
+        if (rn) rmn = NAN;
+        nb[b] = norm == 0 ? glob : norm == 1 ? (!(fabs(rs - 1.0) <= 1e-6 + 1e-5) || rmn < 0.0 || isnan(rmn)) : 0;
+        double z = 0.0;
+        for (int n = 0; n < N; ++n) z += exp(ab[n] - mx);
+        double v = v_prev[b], pv = 0.0;
+        for (int n = 0; n < N; ++n) {
+            w[(size_t)b * N + n] = nb[b] ? exp(ab[n] - mx) / z : (double)ab[n];
+            pv += v * (w[(size_t)b * N + n] * (double)p[(size_t)b * N + n]);   /* :68-69 */
+        }
+        ret[b] = pv / v;                                                        /* :72 */
+        if (ret_out) ret_out[b] = (float)ret[b];
+    }
+    double sf = 0.0, sr = 0.0;
+    for (int b = 0; b < B; ++b) { sf += kind == PMENV_REWARD_LOG_RETURN ? log(ret[b]) : ret[b]; sr += ret[b]; }
+    double mean = sr / B, dev = 0.0;
+    for (int b = 0; b < B; ++b) dev += (ret[b] - mean) * (ret[b] - mean);
+    double sd = B > 1 ? sqrt(dev / (B - 1)) : NAN;
+    double R = kind == PMENV_REWARD_SHARPE ? mean / sd * scale : sf / B * scale;   /* :75-80 */
+    if (grad_a) {
+        for (int b = 0; b < B; ++b) {
+            double dr = kind == PMENV_REWARD_LOG_RETURN ? scale / ((double)B * ret[b])
+                      : kind == PMENV_REWARD_RETURN ? scale / (double)B
+                      : scale * (1.0 / ((double)B * sd) - mean * (ret[b] - mean) / ((double)(B - 1) * sd * sd * sd));
+            double v = v_prev[b], wg = 0.0;
+            for (int n = 0; n < N; ++n) wg += w[(size_t)b * N + n] * (dr * (v * (double)p[(size_t)b * N + n]) / v);
+            for (int n = 0; n < N; ++n) {
+                double g = dr * (v * (double)p[(size_t)b * N + n]) / v;
+                grad_a[(size_t)b * N + n] = (float)(nb[b] ? w[(size_t)b * N + n] * (g - wg) : g);
+            }
+        }
+    }
+    free(w); free(ret); free(nb);
+    return R;
+}
+
 /* ---- Philox4x32-10 (Salmon et al., SC'11) ---- */
 static inline void mulhilo(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
     uint64_t p = (uint64_t)a * b;

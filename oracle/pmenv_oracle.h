@@ -46,6 +46,11 @@ void or_gae(const float* rewards, const float* values, const uint8_t* dones,
             float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam);
 void or_moments(const float* x, int64_t n, double* out);
 
+/* Batched trainer reward (agent/pg/pg.py:40-82) and its gradient wrt a for
+ * grad_out = 1; returns R. norm: 0 global OR (pg.py:52), 1 per row, 2 none. */
+double or_batch_reward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                       int32_t kind, int32_t norm, double scale, float* ret_out, float* grad_a);
+
 /* Philox4x32-10 and the synthetic generators (restating pmenv.hip's device code). */
 void or_philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                    uint32_t k0, uint32_t k1, uint32_t out[4]);

@@ -17,6 +17,7 @@
 #include "data.h"
 #include "env_step.h"
 #include "rollout.h"
+#include "trainer.h"
 
 using namespace pmenv_dev;
 
@@ -527,6 +528,30 @@ int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream) {
     int blocks = (int)(want < 1 ? 1 : (want > kMomBlocks ? kMomBlocks : want));
     moments_partial_kernel<<<blocks, kMomBlock, 0, stream>>>(x, n);
     moments_final_kernel<<<1, 64, 0, stream>>>(blocks, n, out);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
+size_t pmenv_batch_reward_workspace(int32_t B) { return B < 1 ? 0 : ((size_t)6 * B + 8) * 8; }
+
+int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                               int32_t reward_kind, int32_t norm, double scale, double* work,
+                               float* reward_out, float* ret_out, hipStream_t stream) {
+    if (!a || !v_prev || !p || !work || !reward_out || B < 1 || N < 1) return PMENV_ERR_ARG;
+    if (reward_kind != PMENV_REWARD_LOG_RETURN && reward_kind != PMENV_REWARD_RETURN &&
+        reward_kind != PMENV_REWARD_SHARPE)
+        return PMENV_ERR_ARG;
+    if (norm < PMENV_BNORM_GLOBAL_OR || norm > PMENV_BNORM_NONE) return PMENV_ERR_ARG;
+    batch_reward_rows_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, work);
+    batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out, ret_out);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
+int pmenv_batch_reward_backward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
+                                int32_t reward_kind, double scale, const double* work, const float* grad_out,
+                                float* grad_a, hipStream_t stream) {
+    if (!a || !v_prev || !p || !work || !grad_out || !grad_a || B < 1 || N < 1) return PMENV_ERR_ARG;
+    batch_reward_grad_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
+                                                              grad_out, grad_a);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

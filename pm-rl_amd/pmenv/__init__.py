@@ -6,6 +6,6 @@ this package is the host-side mirror of the reference's Python interface
 """
 from .config import EnvConfig  # noqa: F401
 from .trading_env import TradingEnv, RingView  # noqa: F401
-from . import synth, rollout, parallel  # noqa: F401
+from . import synth, rollout, parallel, trainer  # noqa: F401
 
-__all__ = ["EnvConfig", "TradingEnv", "RingView", "synth", "rollout", "parallel"]
+__all__ = ["EnvConfig", "TradingEnv", "RingView", "synth", "rollout", "parallel", "trainer"]

@@ -20,6 +20,7 @@ REWARD_KINDS = {"log_returns": 0, "returns": 1, "sharpe_ratio": 2, "diff_sharpe"
 NORM_MODES = {"and": 0, "or": 1}
 RING_MODES = {"storage": 0, "chrono": 1}
 RET_MODES = {"gross": 0, "net": 1}
+BATCH_NORM_MODES = {"global_or": 0, "row_or": 1, "none": 2}
 STATE_FIELDS = 8   # value, stat_a, stat_b, counter, ring, nonfinite, last_close, w_new
 STATUS = {0: "OK", -1: "ERR_ARG", -2: "ERR_SHAPE", -3: "ERR_HIP", -4: "ERR_ALIGN"}
 
@@ -76,6 +77,11 @@ SIGNATURES = [
     ("pmenv_window_init", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P]),
     ("pmenv_gae", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _P]),
     ("pmenv_moments", ctypes.c_int, [_P, _I64, _P, _P]),
+    ("pmenv_batch_reward_workspace", _SZ, [_I32]),
+    ("pmenv_batch_reward_forward", ctypes.c_int,
+     [_P, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _P, _P, _P]),
+    ("pmenv_batch_reward_backward", ctypes.c_int,
+     [_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, _P, _P, _P, _P]),
 ]
 
 _lib = None

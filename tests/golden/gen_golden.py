@@ -172,6 +172,44 @@ def reward_module_vectors():
     np.savez_compressed(os.path.join(OUT, "reward_module.npz"), **out)
 
 
+def trainer_vectors():
+    """agent/pg/pg.py:40-82 PG._reward and agent/a2c.py/a2c.py:40-82 A2C._loss, forward
+    and torch-autograd gradient wrt the policy output `a`, run from the reference."""
+    import importlib.util
+    import torch
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import agent.pg.pg as pg
+    spec = importlib.util.spec_from_file_location("a2c_ref", os.path.join(REF, "agent/a2c.py/a2c.py"))
+    a2c = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(a2c)
+    out = {}
+    rng = np.random.default_rng(11)
+    for dt in ("f64", "f32"):
+        torch.set_default_dtype(torch.float64 if dt == "f64" else torch.float32)
+        tdt = torch.get_default_dtype()
+        for (B, N) in ((32, 30), (16, 5), (3, 7), (1, 5), (2, 1)):
+            for akind in ("normal", "simplex"):
+                z = rng.standard_normal((B, N)).astype(np.float32)
+                a_np = z if akind == "normal" else (np.exp(z) / np.exp(z).sum(1, keepdims=True)).astype(np.float32)
+                v_np = (25000.0 * np.exp(0.1 * rng.standard_normal(B))).astype(np.float32)
+                p_np = (1.0 + 0.01 * rng.standard_normal((B, N))).astype(np.float32)
+                for kind in ("log_returns", "returns", "sharpe_ratio"):
+                    key = f"{dt}_{B}x{N}_{akind}_{kind}"
+                    for mod, fn, tag in ((pg, pg.PG._reward, "pg"), (a2c, a2c.A2C._loss, "a2c")):
+                        mod.REWARD, mod.REWARD_SCALE = kind, 1
+                        a = torch.tensor(a_np, dtype=tdt).reshape(B, N, 1).requires_grad_(True)
+                        v = torch.tensor(v_np, dtype=tdt).reshape(B, 1, 1)
+                        pp = torch.tensor(p_np, dtype=tdt).reshape(B, N, 1)
+                        r = fn(None, a, v, None, pp)
+                        r.backward()
+                        out[f"{key}_{tag}_r"] = np.array(float(r))
+                        out[f"{key}_{tag}_grad"] = a.grad.reshape(B, N).detach().numpy().astype(np.float64)
+                    out[f"{key}_a"], out[f"{key}_v"], out[f"{key}_p"] = a_np, v_np, p_np
+    pg.REWARD, a2c.REWARD = "log_returns", "log_returns"
+    np.savez_compressed(os.path.join(OUT, "trainer_reward.npz"), **out)
+
+
 CASES = [
     # name, N, W, T, dtype, kind, resets, chan_steps
     ("simplex_n5_w50_t64_f64", 5, 50, 64, "f64", "simplex", (), None),
@@ -198,6 +236,8 @@ def main():
         print("wrote", m["name"])
     reward_module_vectors()
     print("wrote reward_module")
+    trainer_vectors()
+    print("wrote trainer_reward")
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def cases():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not p.endswith("reward_module.npz"))
+                  if not p.endswith(("reward_module.npz", "trainer_reward.npz")))
 
 
 def load(name):

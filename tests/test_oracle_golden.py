@@ -140,3 +140,34 @@ def test_gae_oracle_vs_numpy():
     mo = moments(x)
     assert mo[0] == 1001 and np.isclose(mo[1], x.astype(np.float64).sum()) and \
         np.isclose(mo[2], (x.astype(np.float64) ** 2).sum())
+
+
+def _trainer_cases():
+    d = np.load(gu.GOLDEN_DIR + "/trainer_reward.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_a")})
+    return d, keys
+
+
+@pytest.mark.parametrize("norm", ["global_or"])
+def test_oracle_batch_reward_matches_reference_autograd(norm):
+    """PG._reward / A2C._loss (forward + torch autograd grad) run from the reference."""
+    from oracle import batch_reward
+    d, keys = _trainer_cases()
+    assert len(keys) == 60
+    for key in keys:
+        dt, shape, akind, kind = key.split("_", 3)
+        a, v, p = d[key + "_a"], d[key + "_v"], d[key + "_p"]
+        R, _, g = batch_reward(a, v, p, reward=kind, norm=norm)
+        for tag, sign in (("pg", 1.0), ("a2c", -1.0)):
+            r_ref, g_ref = float(d[f"{key}_{tag}_r"]), d[f"{key}_{tag}_grad"]
+            # fp32 references: the batch Sharpe divides by a tiny std (ill-conditioned)
+            rtol = 1e-9 if dt == "f64" else (1e-3 if kind == "sharpe_ratio" else 2e-5)
+            if np.isnan(r_ref):
+                assert np.isnan(R), key
+                continue
+            assert np.isclose(sign * R, r_ref, rtol=rtol, atol=1e-12 if dt == "f64" else 1e-7), (key, tag, R, r_ref)
+            scale = np.abs(g_ref).max() + 1e-30
+            loose = dt == "f32" and kind == "sharpe_ratio"
+            np.testing.assert_allclose(sign * g, g_ref, rtol=1e-6 if dt == "f64" else (3e-2 if loose else 1e-3),
+                                       atol=1e-7 * scale if dt == "f64" else (3e-2 if loose else 2e-4) * scale,
+                                       err_msg=f"{key} {tag}")
