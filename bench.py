@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--mae-steps", type=int, default=64)
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--windows", choices=["double", "inplace"], default="double")
+    ap.add_argument("--reward", default="log_returns",
+                    choices=["log_returns", "returns", "sharpe_ratio", "diff_sharpe"])
+    ap.add_argument("--commission", type=float, default=0.0)
     ap.add_argument("--inplace-steps", type=int, default=50, help="extra timed in-place steps (0: skip)")
     return ap.parse_args()
 
@@ -93,7 +96,8 @@ def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
     obs_h = obs.cpu().numpy().copy()
     ser_h, act_h = ser.cpu().numpy(), act.cpu().numpy()
     # HIP path on the sample
-    genv = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=dev)
+    genv = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=dev,
+                      reward=args.reward, commission=args.commission)
     genv.reset(obs)
     g_r = []
     for t in range(T):
@@ -103,16 +107,19 @@ def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
     g_v = genv.value.cpu().numpy()
     # CPU restatement on the same inputs
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F))
+    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F, reward=args.reward,
+                               commission=args.commission))
     cenv.reset(obs_h)
     c_r = np.stack([cenv.step(act_h[t], obs_h, bar=ser_h[W + t], threads=threads)[0] for t in range(T)])
-    mae = float(np.mean(np.abs(g_r - c_r)))
+    both_nan = np.isnan(g_r) & np.isnan(c_r)
+    mae = float(np.mean(np.where(both_nan, 0.0, np.abs(g_r - c_r))))
     max_rel_value = float(np.max(np.abs(g_v / cenv.value - 1.0)))
     obs_equal = bool(np.array_equal(obs.cpu().numpy(), obs_h))
 
     # timing: bounded sample of the same workload shape
     Sc = min(args.cpu_sample_envs, S)
-    tenv = OracleEnv(EnvConfig(num_envs=Sc, num_assets=N, window=W, features=F))
+    tenv = OracleEnv(EnvConfig(num_envs=Sc, num_assets=N, window=W, features=F, reward=args.reward,
+                               commission=args.commission))
     tobs = np.ascontiguousarray(obs_h[:Sc])
     tenv.reset(tobs)
     steps = 0
@@ -166,7 +173,8 @@ def main():
     series = synth.series(H + W, B, N, env_offset=lo, seed=args.seed, device=dev)      # [H+W, B, N, 4]
     actions = synth.actions(H, B, N, env_offset=lo, seed=args.seed + 1, device=dev)     # [H, B, N]
     obs = synth.window_from_series(series, W, F)                                         # [B, N, W, F]
-    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev,
+                     reward=args.reward, commission=args.commission)
     env.reset(obs)
     obs_b = torch.empty_like(obs) if args.windows == "double" else None
     reward = torch.empty(B, dtype=torch.float32, device=dev)
@@ -273,7 +281,7 @@ def main():
             "config": {
                 "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels",
                 "envs_per_gpu": B, "global_envs": world * B, "assets": N, "window": W, "features": F,
-                "reward": "log_returns", "commission": 0.0, "obs_dtype": "f32", "accumulate": "f64",
+                "reward": args.reward, "commission": args.commission, "obs_dtype": "f32", "accumulate": "f64",
                 "windows": args.windows,
                 "parallelism": f"env-sharded x{world} (no collective in the step)",
             },

@@ -134,7 +134,12 @@ int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream);
 typedef struct pmenv_step_args {
     const float* action;   /* [B, N]  target weights (raw policy output)            */
     const float* prices;   /* [B, N]  price relatives y_t, or NULL (needs bar)       */
-    const float* bar;      /* [B, N, F-1] new day's market channels, or NULL          */
+    const float* bar;      /* [B, N, F-1] new day's market channels, or NULL; with `day`
+                              set: a market series [series_days, N, F-1] shared by all envs */
+    const int32_t* day;    /* NULL, or [B] device day index: env b's bar is bar[day[b]]
+                              (resident-series data path; a day outside
+                              [0, series_days) reads NaN and is counted non-finite)   */
+    int32_t series_days;
     float* obs;            /* [B, N, W, F] in/out                                     */
     float* obs_out;        /* advance mode only: NULL = advance obs in place; else the
                               advanced window is written here and obs is left untouched
@@ -199,6 +204,12 @@ int pmenv_synth_actions(float* actions, int32_t T, int32_t B, int32_t N,
 /* obs[b, n, t, f] = series[t, b, n, f] for t < W, f < 4; channel F-1 left for reset. F must be 5. */
 int pmenv_window_init(float* obs, const float* series, int32_t B, int32_t N,
                       int32_t W, int32_t F, hipStream_t stream);
+/* Resident market series (data/instrument.py:339-356 windows over one shared series):
+ * obs[b, n, t, f] = series[start[b] + t, n, f] for t < W, f < F-1 (channel F-1 = 0,
+ * written by reset). series [T, N, F-1]; start [B] device int32 with
+ * 0 <= start[b] <= T - W (envs outside get NaN windows). */
+int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N, int32_t F,
+                           const int32_t* start, int32_t B, int32_t W, hipStream_t stream);
 
 /* ---- rollout returns (north star: replay/rollout_buffer.py's GAE / discounted
  * return pass as a device scan; the reference stores (s,a,v,r) but computes no

@@ -44,7 +44,9 @@ struct StepParams {
     double init_cash, commission, scale, rf, eta, mu_tol;
     const float* action;
     const float* prices;
-    const float* bar;
+    const float* bar;      // [B, N, F-1], or the series base when `day` is set
+    const int32_t* day;    // resident-series mode: env b's bar is series[day[b]] ([T, N, F-1] shared)
+    int32_t series_days;   // T of the resident series (days outside [0, T) read NaN)
     float* obs;
     float* obs_out;        // advance mode: destination window (== obs when in place)
     float* reward;
@@ -61,6 +63,17 @@ struct StepParams {
     unsigned long long* nonfinite;
     FastDiv div_wf, div_f, div_w, div_units;
 };
+
+// The day's bar [N, F-1] of env b: a row of the per-env bar batch, or — resident
+// series mode — day[b] of a market series shared by all envs. Returns null for an
+// out-of-range day (the caller then reads NaN: the env's reward turns non-finite
+// and is counted, no memory outside the series is touched).
+__device__ __forceinline__ const float* env_bar(const StepParams& p, int b) {
+    const size_t row = (size_t)p.N * (p.F - 1);
+    if (!p.day) return p.bar + (size_t)b * row;
+    const int32_t d = p.day[b];
+    return (d >= 0 && d < p.series_days) ? p.bar + (size_t)d * row : nullptr;
+}
 
 // ---------------------------------------------------------------- buffer access
 // Range-checked buffer loads/stores (CDNA SRSRC descriptors): a lane whose byte

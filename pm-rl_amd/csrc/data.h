@@ -94,4 +94,20 @@ __global__ void window_init_kernel(float* obs, const f4* series, int B, int N, i
     for (int f = 4; f < F; ++f) o[f] = 0.0f;
 }
 
+// obs[b, n, t, f] = series[start[b] + t, n, f]; one thread per (b, n, t) row of F floats
+__global__ void window_init_days_kernel(float* obs, const float* series, int T, int N, int F,
+                                        const int32_t* start, int B, int W) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over B*N*W
+    if (i >= (int64_t)B * N * W) return;
+    const int t = (int)(i % W);
+    const int64_t bn = i / W;
+    const int n = (int)(bn % N), b = (int)(bn / N);
+    const int Fm = F - 1;
+    const int64_t d = (int64_t)start[b] + t;
+    float* o = obs + (size_t)i * F;
+    const bool ok = start[b] >= 0 && d < T;
+    for (int f = 0; f < Fm; ++f) o[f] = ok ? series[((size_t)d * N + n) * Fm + f] : NAN;
+    o[Fm] = 0.0f;
+}
+
 }  // namespace pmenv_dev

@@ -67,6 +67,7 @@ __device__ __forceinline__ void gather_inputs(const StepParams& p, int b, Scratc
     // densely in w_new so no load depends on the step counter
     const float* wlast = p.w_new + (size_t)b * N;
     (void)W; (void)k;
+    const float* barb = p.bar ? env_bar(p, b) : nullptr;
     for (int n = lane; n < N; n += 64) {
         const size_t i = (size_t)b * N + n;
         const float a = p.action[i];
@@ -74,7 +75,7 @@ __device__ __forceinline__ void gather_inputs(const StepParams& p, int b, Scratc
         if (p.bar) {
             // instrument.py:79 divides float32 tensors: the relative is the correctly
             // rounded fp32 quotient of today's close over the window's last close
-            const float cn = p.bar[i * Fm + p.close_ch];
+            const float cn = barb ? barb[(size_t)n * Fm + p.close_ch] : NAN;
             y = p.prices ? (double)p.prices[i] : (double)(cn / p.last_close[i]);
             p.last_close[i] = cn;
         } else {
@@ -284,7 +285,8 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
     float cn = 0.0f;
     if (act) {
         if (p.bar) {
-            cn = p.bar[i * Fm + p.close_ch];
+            const float* barb = env_bar(p, b);
+            cn = barb ? barb[(size_t)n * Fm + p.close_ch] : NAN;
             y = p.prices ? (double)p.prices[i] : (double)(cn / p.last_close[i]);   // instrument.py:79
         } else {
             y = (double)p.prices[i];
@@ -419,7 +421,8 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
     const auto rs_env = make_rsrc(env_obs, (uint32_t)(N * WF) * 4u);
     float* env_out = p.obs_out + (size_t)b * N * WF;
     const auto rs_unit = make_rsrc(env_out + (size_t)r0 * WF, nf * 4u);
-    const auto rs_bar = make_rsrc(p.bar + (size_t)b * N * 4, (uint32_t)(rows + r0) * 16u);
+    const float* barb = env_bar(p, b);            // null: out-of-range day -> the descriptor reads 0
+    const auto rs_bar = make_rsrc(barb ? barb : p.bar, barb ? (uint32_t)(rows + r0) * 16u : 0u);
     const auto rs_wp = make_rsrc(p.w_new + (size_t)b * N, (uint32_t)(rows + r0) * 4u);
 
     f4 xs[V], xb[V];
@@ -524,8 +527,8 @@ __global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) 
     Scratch s = carve(lds, p.tile_floats, N, F);
     float* obs = p.obs + (size_t)b * N * WF;
 
-    const float* barg = p.bar + (size_t)b * N * Fm;
-    for (int i = tid; i < N * Fm; i += kBlock) s.bar[i] = barg[i];
+    const float* barg = env_bar(p, b);
+    for (int i = tid; i < N * Fm; i += kBlock) s.bar[i] = barg ? barg[i] : NAN;
     if (tid < 64) {
         const int32_t k = p.k[b];
         const double v_prev = p.value[b];

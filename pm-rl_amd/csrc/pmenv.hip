@@ -396,7 +396,12 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     }
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
+    if (a->day && (!a->bar || a->series_days < 1)) {
+        set_err(h, "day[] needs the series in bar and series_days >= 1");
+        return PMENV_ERR_ARG;
+    }
     p.action = a->action; p.prices = a->prices; p.bar = a->bar; p.obs = a->obs;
+    p.day = a->day; p.series_days = a->series_days;
     p.obs_out = a->obs_out ? a->obs_out : a->obs;
     if (a->obs_out && a->bar) {
         const size_t bytes = (size_t)h->cfg.num_envs * h->cfg.num_assets * h->cfg.window * h->cfg.features * 4;
@@ -512,6 +517,14 @@ int pmenv_window_init(float* obs, const float* series, int32_t B, int32_t N, int
     const int64_t threads = (int64_t)B * N * W;
     window_init_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
         obs, reinterpret_cast<const f4*>(series), B, N, W, F);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
+int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N, int32_t F, const int32_t* start,
+                           int32_t B, int32_t W, hipStream_t stream) {
+    if (!obs || !series || !start || T < 1 || B < 1 || N < 1 || W < 1 || F < 2) return PMENV_ERR_ARG;
+    const int64_t threads = (int64_t)B * N * W;
+    window_init_days_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(obs, series, T, N, F, start, B, W);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

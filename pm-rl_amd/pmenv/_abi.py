@@ -39,6 +39,7 @@ class PmenvCfg(ctypes.Structure):
 class PmenvStepArgs(ctypes.Structure):
     _fields_ = [
         ("action", ctypes.c_void_p), ("prices", ctypes.c_void_p), ("bar", ctypes.c_void_p),
+        ("day", ctypes.c_void_p), ("series_days", ctypes.c_int32),
         ("obs", ctypes.c_void_p), ("obs_out", ctypes.c_void_p), ("reward", ctypes.c_void_p),
         ("ret", ctypes.c_void_p), ("weights", ctypes.c_void_p), ("phases", ctypes.c_uint32),
     ]
@@ -75,6 +76,7 @@ SIGNATURES = [
     ("pmenv_synth_series", ctypes.c_int, [_P, _I32, _I32, _I32, _I64, _U64, _F, _P]),
     ("pmenv_synth_actions", ctypes.c_int, [_P, _I32, _I32, _I32, _I64, _U64, _P]),
     ("pmenv_window_init", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P]),
+    ("pmenv_window_init_days", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _I32, _P]),
     ("pmenv_gae", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _P]),
     ("pmenv_moments", ctypes.c_int, [_P, _I64, _P, _P]),
     ("pmenv_batch_reward_workspace", _SZ, [_I32]),

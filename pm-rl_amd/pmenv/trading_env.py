@@ -183,7 +183,7 @@ class TradingEnv:
             self._reset_info()
         return features
 
-    def step(self, action, features, prices=None, bar=None, out=None):
+    def step(self, action, features, prices=None, bar=None, out=None, series=None, day=None):
         """trading_env.py:44-105 for all B envs in one kernel launch.
 
         prices given, bar None : the reference contract — `features` is the next
@@ -192,6 +192,9 @@ class TradingEnv:
                                  the previous reset/step) is advanced one day in
                                  place and `bar` [B, N, F-1] appended; prices
                                  default to bar.close / window[W-1].close.
+        series, day            : resident data path — `series` is a pmenv.data.MarketSeries
+                                 (or a [T, N, F-1] tensor) and env b takes day[b]'s
+                                 bar from it (instead of `bar`)
         out (fused path only)  : write the advanced window into `out` instead of
                                  in place (double-buffered windows, as the
                                  reference's data path hands the env a fresh
@@ -203,8 +206,21 @@ class TradingEnv:
         unb = self._obs_check(features)
         a = self._vec(action, N, "action")
         p = self._vec(prices, N, "prices") if prices is not None else None
-        br = None
-        if bar is not None:
+        br = dy = None
+        days = 0
+        if series is not None:
+            sb = series.bars if hasattr(series, "bars") else series
+            if sb.dim() != 3 or sb.shape[1] != N or sb.shape[2] != cfg.features - 1 or sb.dtype != torch.float32 \
+                    or not sb.is_contiguous() or sb.device != self.device:
+                raise ValueError(f"series must be a contiguous float32 [T, {N}, {cfg.features - 1}] on {self.device}")
+            if day is None:
+                raise ValueError("series= needs day= (one day index per env)")
+            dy = torch.as_tensor(day, device=self.device).to(torch.int32).reshape(-1).contiguous()
+            if dy.numel() != B:
+                raise ValueError("day must hold one index per env")
+            br, days = sb, sb.shape[0]
+            bar = sb
+        elif bar is not None:
             br = self._vec(bar, N * (cfg.features - 1), "bar")
         elif p is None:
             raise ValueError("step needs prices (reference contract) or bar (fused window advance)")
@@ -213,6 +229,9 @@ class TradingEnv:
         args.action = a.data_ptr()
         args.prices = p.data_ptr() if p is not None else None
         args.bar = br.data_ptr() if br is not None else None
+        if dy is not None:
+            args.day = dy.data_ptr()
+            args.series_days = days
         args.obs = features.data_ptr()
         if out is not None:
             if bar is None:

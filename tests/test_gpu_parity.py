@@ -339,3 +339,35 @@ def test_gpu_step_is_graph_capturable():
     ref = torch.stack([ea.step(act[t], obs_a, bar=ser[W + t])[0] for t in range(T)])
     torch.cuda.synchronize()
     assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)
+
+
+def test_gpu_resident_series_equals_bar_batch():
+    """Resident-series data path (env b reads series[day[b]]) == stepping with the
+    gathered bar batch, bit for bit; windows initialised from per-env start days."""
+    from pmenv import TradingEnv, MarketSeries
+    rng = np.random.default_rng(2)
+    T, N, W, B, S = 300, 30, 50, 97, 40
+    closes = 100 * np.exp(np.cumsum(0.01 * rng.standard_normal((T, N)), axis=0))
+    bars = np.stack([closes * np.exp(0.002 * rng.standard_normal((T, N))) for _ in range(3)] + [closes], -1)
+    m = MarketSeries(bars.astype(np.float32), device=DEV)
+    start = m.random_starts(B, W, S, generator=torch.Generator().manual_seed(0))
+    obs_a = m.initial_window(start, W)
+    ref = np.stack([bars[int(s):int(s) + W].transpose(1, 0, 2) for s in start.cpu()]).astype(np.float32)
+    assert np.array_equal(obs_a[..., :4].cpu().numpy(), ref)
+    obs_b = obs_a.clone()
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    act = torch.softmax(torch.randn(S, B, N, device=DEV), -1)
+    for t in range(S):
+        day = start + W + t
+        ra, _ = ea.step(act[t], obs_a, series=m, day=day)
+        rb, _ = eb.step(act[t], obs_b, bar=m.bars[day.long()].contiguous())
+        assert torch.equal(ra, rb)
+    assert torch.equal(obs_a, obs_b) and torch.equal(ea.value, eb.value)
+    # a day outside the series is reported, not read
+    bad = start + W + S
+    bad[3] = T + 5
+    ea.step(act[0], obs_a, series=m, day=bad)
+    assert ea.nonfinite_count() == 1
