@@ -249,6 +249,28 @@ int pmenv_batch_reward_backward(const float* a, const float* v_prev, const float
                                 int32_t reward_kind, double scale, const double* work,
                                 const float* grad_out, float* grad_a, hipStream_t stream);
 
+/* ---- device replay and trajectory metrics ---- */
+
+/* replay/buffer.py:39-79 ReplayBuffer.sample for vectorised envs over a ring of H
+ * recorded steps (days [H, B] int32 = last day of the window acted on, actions
+ * [H, B, N], rewards [H, B]): for each of the S samples (h0[j], env[j]) writes
+ * s, s_next [S, N, W, F] (market channels from series [T, N, F-1], channel F-1 = the
+ * W actions h0..h0+W-1, resp. h0+1..h0+W), a_out [S, N] = actions[h0+W],
+ * r_out [S] = rewards[h0+W-1]. Days outside the series read NaN. */
+int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W,
+                        const int32_t* days, const float* actions, const float* rewards,
+                        int32_t H, int32_t B, const int32_t* h0, const int32_t* env, int32_t S,
+                        float* s, float* s_next, float* a_out, float* r_out, hipStream_t stream);
+
+/* util/eval.py:14-37 per env over a trajectory: returns [T, B] (simple returns),
+ * values [T+1, B] f64, weights [T+1, B, N]; out [B, 5] f64 =
+ * {sharpe, sortino, max drawdown, average turnover, final value} from f64 simple
+ * returns [T, B], values [T+1, B] f64 and weights [T+1, B, N] f32, quantstats
+ * definitions with per-period risk-free (1+rf)^(1/periods)-1 (parity unpinned:
+ * quantstats is absent). */
+int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B,
+                  int32_t N, double risk_free_rate, double periods, double* out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -162,3 +162,42 @@ def batch_reward(a, v_prev, p, reward="log_returns", norm="global_or", scale=1.0
     R = load().or_batch_reward(_p(a), _p(v), _p(pp), B, N, BATCH_REWARD_KINDS[reward], BATCH_NORMS[norm],
                                float(scale), _p(ret), _p(grad))
     return R, ret, grad
+
+
+def replay_gather(series, days, actions, rewards, h0, env, W):
+    """replay/buffer.py:53-79 restated in numpy for a ring of recorded steps."""
+    T, N, Fm = series.shape
+    H = days.shape[0]
+    S = len(h0)
+    s = np.empty((S, N, W, Fm + 1), np.float32)
+    s2 = np.empty_like(s)
+    a = np.empty((S, N), np.float32)
+    r = np.empty(S, np.float32)
+    for j in range(S):
+        b, h = int(env[j]), int(h0[j])
+        hist = np.stack([actions[(h + t) % H, b] for t in range(W + 1)], 1)      # [N, W+1]  (:59, :62)
+        d = int(days[(h + W - 1) % H, b])                                           # (:65)
+        for dd, out, ch in ((d, s, hist[:, :-1]), (d + 1, s2, hist[:, 1:])):        # (:66-70)
+            for t in range(W):
+                day = dd - (W - 1) + t
+                out[j, :, t, :Fm] = series[day] if 0 <= day < T else np.nan
+            out[j, :, :, Fm] = ch
+        a[j] = hist[:, -1]                                                           # (:72)
+        r[j] = rewards[(h + W - 1) % H, b]                                           # (:60)
+    return s, a, r, s2
+
+
+def trajectory_metrics(returns, values, weights, rf=0.04, periods=252):
+    """util/eval.py:14-37 with quantstats' published formulas (sharpe, sortino,
+    max_drawdown) and the reference's turnover loop, per env column."""
+    returns = np.asarray(returns, np.float64)
+    values = np.asarray(values, np.float64)
+    weights = np.asarray(weights, np.float64)
+    rfp = (1 + rf) ** (1 / periods) - 1 if rf else 0.0
+    x = returns - rfp
+    T = x.shape[0]
+    sharpe = x.mean(0) / x.std(0, ddof=1) * np.sqrt(periods)
+    sortino = x.mean(0) / np.sqrt((np.minimum(x, 0) ** 2).sum(0) / T) * np.sqrt(periods)
+    mdd = (values / np.maximum.accumulate(values, 0) - 1).min(0)
+    turn = np.abs(np.diff(weights, axis=0)).sum((0, 2)) / T
+    return np.stack([sharpe, sortino, np.minimum(mdd, 0.0), turn, values[-1]], 1)

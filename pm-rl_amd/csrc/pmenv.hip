@@ -17,6 +17,7 @@
 #include "data.h"
 #include "env_step.h"
 #include "rollout.h"
+#include "replay.h"
 #include "trainer.h"
 
 using namespace pmenv_dev;
@@ -531,7 +532,14 @@ int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N
 int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
               int32_t B, float gamma, float lam, hipStream_t stream) {
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
-    gae_kernel<<<(B + 255) / 256, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+    // few envs x long horizon: wave-per-env chunked scan; otherwise one thread per env
+    // (coalesced across envs, already bandwidth-bound)
+    const char* knob = getenv("PMENV_GAE");
+    const bool scan = knob ? !strcmp(knob, "scan") : (B < 4096 && T >= 256);
+    if (scan)
+        gae_scan_kernel<<<(B + 3) / 4, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+    else
+        gae_kernel<<<(B + 255) / 256, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -541,6 +549,27 @@ int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream) {
     int blocks = (int)(want < 1 ? 1 : (want > kMomBlocks ? kMomBlocks : want));
     moments_partial_kernel<<<blocks, kMomBlock, 0, stream>>>(x, n);
     moments_final_kernel<<<1, 64, 0, stream>>>(blocks, n, out);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
+int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W, const int32_t* days,
+                        const float* actions, const float* rewards, int32_t H, int32_t B, const int32_t* h0,
+                        const int32_t* env, int32_t S, float* s, float* s_next, float* a_out, float* r_out,
+                        hipStream_t stream) {
+    if (!series || !days || !actions || !rewards || !h0 || !env || !s || !s_next || !a_out || !r_out || T < 1 ||
+        N < 1 || F < 2 || W < 1 || H < W + 1 || B < 1 || S < 1)
+        return PMENV_ERR_ARG;
+    const int64_t threads = (int64_t)S * N * W * F;
+    replay_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
+        series, T, N, F, W, days, actions, rewards, H, B, h0, env, S, s, s_next, a_out, r_out);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
+int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B, int32_t N,
+                  double risk_free_rate, double periods, double* out, hipStream_t stream) {
+    if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;
+    metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, weights, T, B, N, risk_free_rate, periods,
+                                                        out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

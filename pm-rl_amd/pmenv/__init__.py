@@ -6,7 +6,7 @@ this package is the host-side mirror of the reference's Python interface
 """
 from .config import EnvConfig  # noqa: F401
 from .trading_env import TradingEnv, RingView  # noqa: F401
-from . import synth, rollout, parallel, trainer, data  # noqa: F401
+from . import synth, rollout, parallel, trainer, data, replay  # noqa: F401
 from .data import MarketSeries  # noqa: F401
 
-__all__ = ["EnvConfig", "TradingEnv", "RingView", "synth", "rollout", "parallel", "trainer", "data", "MarketSeries"]
+__all__ = ["EnvConfig", "TradingEnv", "RingView", "synth", "rollout", "parallel", "trainer", "data", "MarketSeries", "replay"]

@@ -79,6 +79,9 @@ SIGNATURES = [
     ("pmenv_window_init_days", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _I32, _P]),
     ("pmenv_gae", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _P]),
     ("pmenv_moments", ctypes.c_int, [_P, _I64, _P, _P]),
+    ("pmenv_replay_gather", ctypes.c_int,
+     [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P]),
+    ("pmenv_metrics", ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P]),
     ("pmenv_batch_reward_workspace", _SZ, [_I32]),
     ("pmenv_batch_reward_forward", ctypes.c_int,
      [_P, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _P, _P, _P]),

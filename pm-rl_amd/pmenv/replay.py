@@ -1,0 +1,96 @@
+"""Device replay for vectorised envs.
+
+`DeviceReplay` mirrors replay/buffer.py (`ReplayBuffer.add` :23-37, `.sample` :39-79):
+per recorded step it keeps only the day index of the window the agent acted on,
+the action and the reward; `sample` re-materialises the observation windows s, s'
+on device from the resident market series (pmenv.data.MarketSeries) with the last W
+actions as the weight channel, exactly as the reference rebuilds them from its
+dataset. `trajectory_metrics` restates util/eval.py:14-37 (Sharpe, Sortino, max
+drawdown, average turnover) per env on device.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+from .config import RISK_FREE_RATE
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class DeviceReplay:
+    def __init__(self, num_envs, num_assets, window, capacity, series, features=5):
+        if capacity < window + 2:
+            raise ValueError("capacity must hold at least window + 2 steps")
+        self.B, self.N, self.W, self.F, self.H = num_envs, num_assets, window, features, capacity
+        self.series = series
+        dev = series.device
+        self.days = torch.zeros(capacity, num_envs, dtype=torch.int32, device=dev)
+        self.actions = torch.zeros(capacity, num_envs, num_assets, dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros(capacity, num_envs, dtype=torch.float32, device=dev)
+        self.head = 0
+        self.count = 0
+
+    def __len__(self):
+        return self.count
+
+    def add(self, day, action, reward):
+        """buffer.py:23-37: one recorded step for every env."""
+        h = self.head
+        self.days[h].copy_(torch.as_tensor(day).reshape(self.B))
+        self.actions[h].copy_(torch.as_tensor(action).reshape(self.B, self.N))
+        self.rewards[h].copy_(torch.as_tensor(reward).reshape(self.B))
+        self.head = (h + 1) % self.H
+        self.count = min(self.count + 1, self.H)
+
+    def indices(self, batch_size, generator=None):
+        """Random (start, env) pairs with W+1 consecutive recorded steps (buffer.py:47-51)."""
+        span = self.count - self.W - 1
+        if span < 1:
+            raise ValueError("not enough recorded steps to sample a window")
+        st = torch.randint(0, span, (batch_size,), generator=generator)
+        env = torch.randint(0, self.B, (batch_size,), generator=generator)
+        oldest = (self.head - self.count) % self.H
+        h0 = (oldest + st) % self.H
+        dev = self.days.device
+        return h0.to(dev, torch.int32), env.to(dev, torch.int32)
+
+    def gather(self, h0, env):
+        """buffer.py:53-79 for the given samples: (s, a, r, s_next) shaped like the reference."""
+        lib = _abi.load()
+        S = h0.numel()
+        dev = self.days.device
+        s = torch.empty(S, self.N, self.W, self.F, device=dev)
+        s2 = torch.empty_like(s)
+        a = torch.empty(S, self.N, device=dev)
+        r = torch.empty(S, device=dev)
+        sb = self.series.bars
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _abi.check(lib.pmenv_replay_gather(_p(sb), sb.shape[0], self.N, self.F, self.W, _p(self.days),
+                                           _p(self.actions), _p(self.rewards), self.H, self.B,
+                                           _p(h0.contiguous()), _p(env.contiguous()), S, _p(s), _p(s2), _p(a), _p(r),
+                                           st), None, "pmenv_replay_gather")
+        return s, a.reshape(S, self.N, 1), r.reshape(S, 1, 1), s2
+
+    def sample(self, batch_size, generator=None):
+        return self.gather(*self.indices(batch_size, generator))
+
+
+def trajectory_metrics(returns, values, weights, risk_free_rate=RISK_FREE_RATE, periods=252):
+    """Per-env {sharpe, sortino, max_drawdown, average_turnover, final_value} over a
+    trajectory: returns [T, B] simple returns, values [T+1, B], weights [T+1, B, N]."""
+    lib = _abi.load()
+    r = returns.to(torch.float64).contiguous()
+    T, B = r.shape
+    v = values.to(device=r.device, dtype=torch.float64).contiguous()
+    w = weights.to(device=r.device, dtype=torch.float32).contiguous()
+    if tuple(v.shape) != (T + 1, B) or w.shape[:2] != (T + 1, B):
+        raise ValueError("values must be [T+1, B] and weights [T+1, B, N]")
+    out = torch.empty(B, 5, dtype=torch.float64, device=r.device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+    _abi.check(lib.pmenv_metrics(_p(r), _p(v), _p(w), T, B, w.shape[2], float(risk_free_rate), float(periods),
+                                 _p(out), st), None, "pmenv_metrics")
+    keys = ("sharpe", "sortino", "max_drawdown", "average_turnover", "final_value")
+    return {k: out[:, i] for i, k in enumerate(keys)}

@@ -267,6 +267,23 @@ def test_gpu_synth_matches_oracle():
     np.testing.assert_allclose(a, synth_actions(6, 9, 7, env_offset=5, seed=4), rtol=1e-6)
 
 
+@pytest.mark.parametrize("T,B,path", [(5000, 3, "scan"), (257, 64, "scan"), (64, 65536, "loop"), (300, 10, "loop"),
+                                      (1, 5, "scan"), (63, 2, "scan")])
+def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
+    """GAE(gamma, lambda) over a [T, B] rollout: chunked wave scan and per-env loop
+    vs the oracle's sequential recursion (parity unpinned by the reference)."""
+    from pmenv import rollout
+    monkeypatch.setenv("PMENV_GAE", path)
+    rng = np.random.default_rng(T + B)
+    r = rng.standard_normal((T, B)).astype(np.float32)
+    v = rng.standard_normal((T + 1, B)).astype(np.float32)
+    d = rng.random((T, B)) < 0.02
+    adv, ret = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
+    oadv, oret = or_gae(r, v, d, 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
+
+
 def test_gpu_gae_and_moments_match_oracle():
     from pmenv import rollout
     rng = np.random.default_rng(1)
@@ -371,3 +388,47 @@ def test_gpu_resident_series_equals_bar_batch():
     bad[3] = T + 5
     ea.step(act[0], obs_a, series=m, day=bad)
     assert ea.nonfinite_count() == 1
+
+
+def test_gpu_replay_gather_matches_restatement():
+    """replay/buffer.py:39-79 sample on device vs the numpy restatement
+    (the reference module is not importable: parity restated from its text)."""
+    from pmenv import MarketSeries
+    from pmenv.replay import DeviceReplay
+    from oracle import replay_gather
+    rng = np.random.default_rng(4)
+    T, N, W, B, H = 200, 30, 12, 33, 40
+    bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
+    m = MarketSeries(bars, device=DEV)
+    rb = DeviceReplay(B, N, W, H, m)
+    for h in range(H + 17):                      # wraps the ring
+        rb.add(torch.full((B,), W + h % (T - W - 2), dtype=torch.int32, device=DEV),
+               torch.rand(B, N, device=DEV), torch.randn(B, device=DEV))
+    h0, env = rb.indices(64, generator=torch.Generator().manual_seed(1))
+    s, a, r, s2 = rb.gather(h0, env)
+    es, ea, er, es2 = replay_gather(bars, rb.days.cpu().numpy(), rb.actions.cpu().numpy(), rb.rewards.cpu().numpy(),
+                                    h0.cpu().numpy(), env.cpu().numpy(), W)
+    assert np.array_equal(s.cpu().numpy(), es, equal_nan=True)
+    assert np.array_equal(s2.cpu().numpy(), es2, equal_nan=True)
+    assert np.array_equal(a.cpu().numpy()[..., 0], ea) and np.array_equal(r.cpu().numpy()[:, 0, 0], er)
+
+
+def test_gpu_trajectory_metrics_match_restatement():
+    from pmenv import TradingEnv, synth
+    from pmenv.replay import trajectory_metrics
+    from oracle import trajectory_metrics as ref_metrics
+    B, N, W, T = 300, 30, 20, 80
+    ser = synth.series(W + T, B, N, device=DEV)
+    act = synth.actions(T, B, N, device=DEV)
+    obs = synth.window_from_series(ser, W)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, track_info=True)
+    env.reset(obs)
+    for t in range(T):
+        env.step(act[t], obs, bar=ser[W + t])
+    rets = torch.stack(env.info["returns"][1:]) - 1.0
+    vals = torch.stack(env.info["values"])
+    wts = torch.stack(env.info["actions"])
+    got = trajectory_metrics(rets, vals, wts)
+    exp = ref_metrics(rets.cpu().numpy(), vals.cpu().numpy(), wts.cpu().numpy())
+    for i, k in enumerate(("sharpe", "sortino", "max_drawdown", "average_turnover", "final_value")):
+        np.testing.assert_allclose(got[k].cpu().numpy(), exp[:, i], rtol=1e-6, atol=1e-9, err_msg=k)

@@ -41,3 +41,24 @@ def test_wrapper_refuses_cpu_device():
     from pmenv import TradingEnv
     with pytest.raises(ValueError):
         TradingEnv(num_envs=2, num_assets=5, window=8, device="cpu")
+
+
+def test_device_replay_ring_indices_cpu():
+    """DeviceReplay.add/indices host logic (replay/buffer.py:23-51) without a GPU."""
+    import types
+    import torch
+    from pmenv.replay import DeviceReplay
+    B, N, W, H = 3, 2, 4, 10
+    rb = DeviceReplay(B, N, W, H, types.SimpleNamespace(device=torch.device("cpu")))
+    with pytest.raises(ValueError):
+        rb.indices(4)
+    for k in range(H + 3):                              # wraps: oldest recorded step is k=3
+        rb.add(torch.full((B,), k, dtype=torch.int32), torch.full((B, N), float(k)), torch.full((B,), float(k)))
+    assert len(rb) == H and rb.head == 3
+    h0, env = rb.indices(500, generator=torch.Generator().manual_seed(0))
+    # every sample's W+1 consecutive steps are recorded and in chronological order
+    ks = torch.stack([rb.days[(h0.long() + t) % H, env.long()] for t in range(W + 1)], 1)
+    assert torch.all(ks[:, 1:] - ks[:, :-1] == 1) and ks.min() >= 3 and ks.max() <= H + 2
+    assert set(env.tolist()) == set(range(B))
+    with pytest.raises(ValueError):
+        DeviceReplay(B, N, W, W + 1, None)
