@@ -265,31 +265,99 @@ __device__ __forceinline__ double group_min(double v, int lane) {
     return lane < 32 ? fmin(r0, r1) : fmin(r2, r3);
 }
 
+// The per-env step of lane group (b, lane % L) in two halves, so a caller can put
+// other loads between them: a load half issues every load (none dependent on
+// another, no data-dependent branch), scalar_finish computes and returns the
+// lane's w' (0 past N) and the counter before the step.
+struct ScalarIn {
+    int32_t k;
+    int bar_ok;      // bar4: the day is inside the series
+    double v_prev;
+    double sa, sb;   // reward statistics (Sharpe moments / differential-Sharpe EMAs)
+    float a, wlf;
+    float cn;        // today's close (not bar4)
+    float pl;        // caller prices (advance with prices / surface) or the window's last close
+    f4 bar;          // bar4: the lane's whole bar row
+};
+
+// K1 form: plain loads, L lanes per env
 template <int L>
-__global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
-    constexpr int EPW = 64 / L;                   // envs per wave
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ ScalarIn scalar_load(const StepParams& p, int b, int lane) {
     const int n = lane % L;
-    const int b = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * EPW + lane / L;
-    const int N = p.N, W = p.W, Fm = p.F - 1;
+    const int N = p.N, Fm = p.F - 1;
     const bool env_ok = b < p.B;
     const bool act = env_ok && n < N;
     const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
+    ScalarIn in;
+    in.k = env_ok ? p.k[env_ok ? b : 0] : 0;
+    in.v_prev = env_ok ? p.value[env_ok ? b : 0] : 1.0;
+    in.sa = p.sa[env_ok ? b : 0];
+    in.sb = p.sb[env_ok ? b : 0];
+    in.a = act ? p.action[i] : 0.0f;
+    in.wlf = act ? p.w_new[i] : 0.0f;                                  // get_last() (weight_buffer.py:28-30)
+    in.cn = 0.0f;
+    in.pl = 1.0f;
+    in.bar_ok = 0;
+    in.bar = f4{0.f, 0.f, 0.f, 0.f};
+    if (act) {
+        if (p.bar) {
+            const float* barb = env_bar(p, b);
+            in.cn = barb ? barb[(size_t)n * Fm + p.close_ch] : NAN;
+            in.pl = p.prices ? p.prices[i] : p.last_close[i];
+        } else {
+            in.pl = p.prices[i];
+        }
+    }
+    return in;
+}
 
-    // every load up front, none dependent on another
-    const int32_t k = env_ok ? p.k[env_ok ? b : 0] : 0;
-    const double v_prev = env_ok ? p.value[env_ok ? b : 0] : 1.0;
-    const double a = act ? (double)p.action[i] : 0.0;
-    const float wlf = act ? p.w_new[i] : 0.0f;                       // get_last() (weight_buffer.py:28-30)
+// fused form (advance mode, F = 5, one env per wave): branch-free buffer loads
+// (lanes past N read 0) and the lane's whole bar row (16 B)
+__device__ __forceinline__ ScalarIn scalar_load_row(const StepParams& p, int b, int lane) {
+    const int N = p.N;
+    const uint32_t nb = (uint32_t)N * 4u, off = (uint32_t)lane * 4u;
+    ScalarIn in;
+    in.k = p.k[b];
+    in.v_prev = p.value[b];
+    in.sa = p.sa[b];
+    in.sb = p.sb[b];
+    in.a = buf_load1(make_rsrc(p.action + (size_t)b * N, nb), off);
+    in.wlf = buf_load1(make_rsrc(p.w_new + (size_t)b * N, nb), off);
+    in.pl = buf_load1(make_rsrc((p.prices ? p.prices : p.last_close) + (size_t)b * N, nb), off);
+    const float* barb = env_bar(p, b);            // null: out-of-range day -> the descriptor reads 0
+    in.bar = buf_load4(make_rsrc(barb ? barb : p.bar, barb ? nb * 4u : 0u), off * 4u);
+    in.bar_ok = barb != nullptr;
+    in.cn = 0.0f;
+    return in;
+}
+
+template <int L, bool ROW = false>
+__device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int lane, const ScalarIn& in,
+                                               int32_t& k_before) {
+    const int n = lane % L;
+    const int N = p.N, W = p.W;
+    const bool env_ok = b < p.B;
+    const bool act = env_ok && n < N;
+    const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
+    const int32_t k = in.k;
+    const double v_prev = in.v_prev;
+    const double a = (double)in.a;
+    const float wlf = in.wlf;
+    // instrument.py:79 divides float32 tensors: the relative is the correctly
+    // rounded fp32 quotient of today's close over the window's last close
     double y = 1.0;
     float cn = 0.0f;
     if (act) {
         if (p.bar) {
-            const float* barb = env_bar(p, b);
-            cn = barb ? barb[(size_t)n * Fm + p.close_ch] : NAN;
-            y = p.prices ? (double)p.prices[i] : (double)(cn / p.last_close[i]);   // instrument.py:79
+            if (ROW) {
+                const int c = p.close_ch;
+                cn = in.bar_ok ? (c == 0 ? in.bar.x : c == 1 ? in.bar.y : c == 2 ? in.bar.z : in.bar.w) : NAN;
+            } else {
+                cn = in.cn;
+            }
+            y = p.prices ? (double)in.pl : (double)(cn / in.pl);
         } else {
-            y = (double)p.prices[i];
+            y = (double)in.pl;
         }
     }
 
@@ -339,7 +407,7 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
     const double value = group_sum<L>(pv, lane);
     const int slot = (int)((1 + (int64_t)k) % W);
     if (act) {
-        const float wp = (float)(pv / value);
+        const float wp = (float)(pv / value);     // the value returned below
         p.ring[(size_t)b * W * N + (size_t)slot * N + n] = wp;
         p.w_new[i] = wp;
         if (p.weights) p.weights[i] = wp;
@@ -355,7 +423,7 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
             break;
         case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
             double m = (double)(k + 1);
-            double mean = p.sa[b], m2 = p.sb[b];
+            double mean = in.sa, m2 = in.sb;
             double d = ret - mean;
             mean += d / m;
             m2 += d * (ret - mean);
@@ -365,7 +433,7 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
             break;
         }
         case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
-            double R = ret - 1.0, A = p.sa[b], Bm = p.sb[b];
+            double R = ret - 1.0, A = in.sa, Bm = in.sb;
             double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
             r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
             p.sa[b] = A + p.eta * dA;
@@ -381,6 +449,17 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
         if (p.ret) p.ret[b] = ret;
         if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
     }
+    k_before = k;
+    return act ? (float)(pv / value) : 0.0f;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
+    constexpr int EPW = 64 / L;                   // envs per wave
+    const int lane = threadIdx.x & 63;
+    const int b = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * EPW + lane / L;
+    int32_t k;
+    (void)scalar_finish<L>(p, b, lane, scalar_load<L>(p, b, lane), k);
 }
 
 // ---------------------------------------------------------------- K2: window advance
@@ -402,7 +481,10 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
 // what bounds this kernel (bytes in flight per CU = residency x unit size).
 // ABL (timing-only ablation builds, tools/ab_advance.py; 0 in the product):
 //   1 = skip the bar / w' loads, 2 = skip the unshifted-weight load, 4 = store xs as is.
-template <int BLOCK, int V, bool INPLACE, int ABL = 0>
+// FUSED (whole-env units, N <= 64): the workgroup also runs the env's scalar step
+// on its first wave, after every streaming load is in flight, and hands w' and the
+// counter to the other waves through LDS — one launch per step instead of two.
+template <int BLOCK, int V, bool INPLACE, int ABL = 0, bool FUSED = false>
 __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
     constexpr int F = 5;
     const int tid = threadIdx.x;
@@ -428,6 +510,9 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
     f4 xs[V], xb[V];
     float xwp[V], xun[V];
     int kk0[V];
+    // FUSED: the first wave's scalar loads go out ahead of its streaming loads
+    ScalarIn sin;
+    if (FUSED && tid < 64) sin = scalar_load_row(p, b, tid);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const uint32_t q = (uint32_t)(tid + i * BLOCK);
@@ -441,17 +526,42 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
         xb[i] = f4{0.f, 0.f, 0.f, 0.f};
         xwp[i] = 0.f;
         xun[i] = 0.f;
-        if (!(ABL & 1)) {
+        if (FUSED) {
+            kk0[i] |= (int)min(row, 63u) << 16;                             // asset: bar and w' from LDS
+        } else if (!(ABL & 1)) {
             xb[i] = buf_load4(rs_bar, (uint32_t)(r0 + (int)row) * 16u);     // the asset's new bar
             xwp[i] = buf_load1(rs_wp, (uint32_t)(r0 + (int)row) * 4u);      // its new weight w'
         }
         if (!(ABL & 2)) xun[i] = buf_load1(rs_env, unit_off + (j0 + (uint32_t)ew) * 4u);   // unshifted weight
     }
-    const int32_t k = p.k[b] - 1;                    // scalar_step_kernel already counted this step
-    if (INPLACE) {
-        // in place: every load of the unit lands before the unit's first store
-        __builtin_amdgcn_s_waitcnt(0);
+    int32_t k;
+    if (FUSED) {
+        __shared__ f4 sh_bar[64];
+        __shared__ float sh_wp[64];
+        __shared__ int32_t sh_k;
+        if (tid < 64) {
+            int32_t kb;
+            const float wp = scalar_finish<64, true>(p, b, tid, sin, kb);
+            sh_wp[tid] = wp;
+            sh_bar[tid] = sin.bar;
+            if (tid == 0) sh_k = kb;
+        }
+        if (INPLACE) __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
+        k = sh_k;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            xwp[i] = sh_wp[kk0[i] >> 16];
+            xb[i] = sh_bar[kk0[i] >> 16];
+            kk0[i] &= 0xFFFF;
+        }
+    } else {
+        k = p.k[b] - 1;                              // scalar_step_kernel already counted this step
+        if (INPLACE) {
+            // in place: every load of the unit lands before the unit's first store
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        }
     }
 
     const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);

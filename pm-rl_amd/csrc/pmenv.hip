@@ -45,6 +45,7 @@ struct pmenv {
     int unit_rows, units_per_env, stream_vec;          // in-place advance
     int unit_rows_db, units_per_env_db, stream_vec_db; // double-buffered advance (obs_out)
     int scalar_scratch_floats;
+    int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
     int ablate;           // PMENV_ABLATE timing-only variants of advance_rows_kernel (0 = product)
     size_t lds_scalar, lds_stream;
     char err[512];
@@ -155,6 +156,25 @@ void launch_advance_a(int vec, const StepParams& p, unsigned grid, hipStream_t s
     if (vec == 1) launch_advance_v<1, ABL>(p, grid, stream);
     else if (vec == 2) launch_advance_v<2, ABL>(p, grid, stream);
     else launch_advance_v<4, ABL>(p, grid, stream);
+}
+
+constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
+
+// one launch per step: whole-env units (the double-buffered geometry), scalar step
+// inside the workgroup (N <= 64)
+void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
+    p.unit_rows = h->unit_rows_db;
+    p.units_per_env = 1;
+    p.div_units = make_fastdiv(1u);
+    const unsigned grid = (unsigned)h->cfg.num_envs;
+    const bool inplace = p.obs_out == p.obs;
+#define PMENV_FUSED_LAUNCH(V)                                                                        \
+    if (inplace) advance_rows_kernel<kStreamBlock, V, true, 0, true><<<grid, kStreamBlock, 0, stream>>>(p); \
+    else advance_rows_kernel<kStreamBlock, V, false, 0, true><<<grid, kStreamBlock, 0, stream>>>(p);
+    if (h->stream_vec_db == 1) { PMENV_FUSED_LAUNCH(1) }
+    else if (h->stream_vec_db == 2) { PMENV_FUSED_LAUNCH(2) }
+    else { PMENV_FUSED_LAUNCH(4) }
+#undef PMENV_FUSED_LAUNCH
 }
 
 // ablation builds are selected only by the PMENV_ABLATE knob (timing studies)
@@ -299,6 +319,19 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
         h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
         h->lds_stream = 0;
+        // fused one-launch step (whole-env units, one wave for the env's assets). The
+        // scalar step inside the streaming workgroup lengthens every workgroup's life
+        // by its compute, so it only pays where the launch is latency-bound: measured
+        // on MI355X at N = 30, W = 50 (tools/gpu_ab_envs.sh) it wins at B = 1024
+        // (18.5 vs 20.2 us in place) and loses from B = 4096 up (57.9 vs 52.9 us;
+        // 764 vs 712 us at B = 65536).
+        const bool fusable = h->units_per_env_db == 1 && c.num_assets <= 64 && !h->ablate;
+        if (fusable && c.num_envs <= 1024) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
+        if (const char* knob = getenv("PMENV_FUSED")) {    // A/B knob: 0 | db | all
+            if (!strcmp(knob, "0") || !fusable) h->fused = 0;
+            else if (!strcmp(knob, "db")) h->fused = PMENV_FUSE_DB;
+            else if (!strcmp(knob, "all")) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
+        }
     }
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
@@ -422,6 +455,11 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     const bool obs16 = (((uintptr_t)a->obs | (uintptr_t)p.obs_out) & 15u) == 0;
     if (h->streaming && obs16) {
         const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        const int fuse_bit = p.obs_out == p.obs ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
+        if (ph == (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE) && (h->fused & fuse_bit)) {
+            launch_fused(h, p, stream);
+            return check_launch(h, "advance_rows_kernel<fused>");
+        }
         if (ph & PMENV_PHASE_SCALAR) {
             const int N = h->cfg.num_assets;
             if (N <= 32) {
@@ -465,7 +503,10 @@ size_t pmenv_state_bytes(const pmenv* h) { return h ? h->state_bytes : 0; }
 
 const char* pmenv_step_path(const pmenv* h) {
     if (!h) return "";
-    return h->streaming ? "scalar_step_kernel+advance_rows_kernel" : "step_advance_lds_kernel";
+    if (!h->streaming) return "step_advance_lds_kernel";
+    if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
+    if (h->fused) return "advance_rows_kernel<fused> (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
+    return "scalar_step_kernel+advance_rows_kernel";
 }
 
 int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {

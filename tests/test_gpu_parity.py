@@ -163,6 +163,25 @@ def test_gpu_double_buffered_advance(N, W, F):
     _run_both(kw, B=9, N=N, W=W, T=W + 7, kind="mixed", F=F, seed=N, double_buffer=True)
 
 
+@pytest.mark.parametrize("fused", ["0", "db", "all"])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+@pytest.mark.parametrize("kw", MODES[:1] + MODES[4:8], ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+def test_gpu_fused_and_two_launch_agree_with_oracle(monkeypatch, fused, db, kw):
+    """PMENV_FUSED picks the one-launch step (scalar step inside the streaming
+    workgroup) or the two-launch path; both must match the oracle, in place and
+    double-buffered."""
+    monkeypatch.setenv("PMENV_FUSED", fused)
+    _run_both(kw, B=37, N=30, W=50, T=56, kind="mixed", seed=zlib.crc32(f"{kw}{fused}{db}".encode()),
+              double_buffer=db)
+
+
+@pytest.mark.parametrize("N,W", [(64, 16), (33, 20), (8, 50), (1, 4)])
+def test_gpu_fused_shapes(monkeypatch, N, W):
+    monkeypatch.setenv("PMENV_FUSED", "all")
+    for db in (False, True):
+        _run_both({}, B=11, N=N, W=W, T=W + 9, kind="mixed", seed=N + W, double_buffer=db)
+
+
 def test_gpu_out_must_not_overlap():
     from pmenv import TradingEnv
     env = TradingEnv(num_envs=2, num_assets=5, window=8, device=DEV)

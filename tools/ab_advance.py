@@ -27,26 +27,33 @@ lib = _abi.load()
 ser = synth.series(a.H + W, B, N, device=dev)
 act = synth.actions(a.H, B, N, device=dev)
 envs = {}
+KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED")
 for v in a.variants.split(","):
+    # "base+KNOB=val+...": extra env knobs at creation (e.g. "o+PMENV_FUSED=0")
+    base, *extra = v.split("+")
     # "lds" -> single-launch LDS kernel, "uR" -> streaming with R rows per unit, else default
     # "uR" -> R rows per unit, "aX" -> ablation X, combinable as "u16a3"; suffix "o" -> double-buffered
-    for knob in ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE"):
+    for knob in KNOBS:
         os.environ.pop(knob, None)
+    for kv in extra:
+        os.environ[kv.split("=")[0]] = kv.split("=")[1]
     import re
-    m = re.fullmatch(r"(?:u(\d+))?(?:a(\d+))?o?", v)
-    if v != "stream" and m and (m.group(1) or m.group(2)):
+    m = re.fullmatch(r"(?:u(\d+))?(?:a(\d+))?o?", base)
+    if base in ("stream", "o", "so"):
+        pass
+    elif m and (m.group(1) or m.group(2)):
         if m.group(1):
             os.environ["PMENV_UNIT_ROWS"] = m.group(1)
         if m.group(2):
             os.environ["PMENV_ABLATE"] = m.group(2)
-    elif v != "stream":
-        os.environ["PMENV_ADVANCE"] = v
+    else:
+        os.environ["PMENV_ADVANCE"] = base
     obs = synth.window_from_series(ser, W)
     e = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
     e.reset(obs)
     print(v, e.step_path, file=sys.stderr)
-    envs[v] = (e, obs, torch.empty(B, device=dev), obs.clone() if v.endswith("o") else None)
-for knob in ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE"):
+    envs[v] = (e, obs, torch.empty(B, device=dev), obs.clone() if base.endswith("o") else None)
+for knob in KNOBS:
     os.environ.pop(knob, None)
 stream = torch.cuda.current_stream()
 sp = ctypes.c_void_p(stream.cuda_stream)
@@ -78,7 +85,7 @@ ref = None
 for v, (e, obs, rew, obs2) in envs.items():
     if obs2 is not None and t_global[v] % 2:
         obs = obs2                    # latest window of a double-buffered run
-    if "a" in v and v != "lds":
+    if "a" in v.split("+")[0] and v != "lds":
         continue                      # ablation builds compute wrong windows by design
     if ref is None:
         ref = (obs, rew, e.value)
