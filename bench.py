@@ -136,7 +136,8 @@ def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
     return {
         "value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
         "sample": f"{Sc} envs x {steps} steps of the same N={N} W={W} F={F} fused step "
-                  f"(oracle/pmenv_oracle.c, OpenMP over envs) in {el:.2f} s on {cpu_model()}",
+                  f"(oracle/pmenv_oracle.c, OpenMP over envs) in {el:.2f} s wall on {threads} threads "
+                  f"(~{el * threads:.0f} CPU-s) of {cpu_model()}",
     }, {"reward_mae": mae, "value_max_rel": max_rel_value, "obs_bit_exact": obs_equal,
         "sample": f"{S} envs x {T} steps, HIP vs CPU restatement"}
 

@@ -223,8 +223,11 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones,
               hipStream_t stream);
 
 /* Per-rank advantage moments {count, sum, sum of squares} in f64 into out[3]
- * (the only cross-GPU exchange: a 24-byte all-reduce over xGMI). */
-int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream);
+ * (the only cross-GPU exchange: a 24-byte all-reduce over xGMI). `work` is
+ * caller-owned device scratch of pmenv_moments_workspace() bytes (per-block
+ * partials; two calls in flight need two workspaces). Deterministic. */
+size_t pmenv_moments_workspace(void);
+int pmenv_moments(const float* x, int64_t n, double* out, double* work, hipStream_t stream);
 
 /* ---- trainer-side twin: the differentiable batched portfolio reward of the
  * PG / A2C agents (agent/pg/pg.py:40-82 `_reward`, agent/a2c.py/a2c.py:40-82 `_loss`
@@ -236,7 +239,7 @@ typedef enum pmenv_batch_norm {
     PMENV_BNORM_NONE = 2
 } pmenv_batch_norm;
 
-/* f64 scratch the forward fills and the backward reads: (6*B + 8) * 8 bytes. */
+/* f64 scratch the forward fills and the backward reads: (6*B + 8 + 16*ceil(B/16)) * 8 bytes. */
 size_t pmenv_batch_reward_workspace(int32_t B);
 /* a, p [B, N]; v_prev [B] (the _v of pg.py); reward_kind LOG_RETURN / RETURN / SHARPE
  * (batch mean / std, pg.py:80); writes reward_out[0] (device) and optionally the

@@ -280,34 +280,34 @@ struct ScalarIn {
     f4 bar;          // bar4: the lane's whole bar row
 };
 
-// K1 form: plain loads, L lanes per env
+// K1 form: L lanes per env, every load unconditional from a clamped (always
+// valid) address and masked afterwards, so several envs' loads can be in flight
+// together without control-flow joins between them
 template <int L>
 __device__ __forceinline__ ScalarIn scalar_load(const StepParams& p, int b, int lane) {
     const int n = lane % L;
     const int N = p.N, Fm = p.F - 1;
     const bool env_ok = b < p.B;
     const bool act = env_ok && n < N;
-    const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
+    const int bc = env_ok ? b : 0;
+    const int nc = act ? n : 0;
+    const size_t i = (size_t)bc * N + nc;
     ScalarIn in;
-    in.k = env_ok ? p.k[env_ok ? b : 0] : 0;
-    in.v_prev = env_ok ? p.value[env_ok ? b : 0] : 1.0;
-    in.sa = p.sa[env_ok ? b : 0];
-    in.sb = p.sb[env_ok ? b : 0];
-    in.a = act ? p.action[i] : 0.0f;
-    in.wlf = act ? p.w_new[i] : 0.0f;                                  // get_last() (weight_buffer.py:28-30)
-    in.cn = 0.0f;
-    in.pl = 1.0f;
+    in.k = p.k[bc];
+    in.v_prev = p.value[bc];
+    in.sa = p.sa[bc];
+    in.sb = p.sb[bc];
+    const float a = p.action[i];
+    const float wl = p.w_new[i];                                       // get_last() (weight_buffer.py:28-30)
+    const float* barb = p.bar ? env_bar(p, bc) : nullptr;
+    const float cv = *(barb ? barb + (size_t)nc * Fm + p.close_ch : p.action + i);
+    const float pl = *((p.prices ? p.prices : p.last_close) + i);
+    in.a = act ? a : 0.0f;
+    in.wlf = act ? wl : 0.0f;
+    in.cn = barb ? cv : NAN;
+    in.pl = act ? pl : 1.0f;
     in.bar_ok = 0;
     in.bar = f4{0.f, 0.f, 0.f, 0.f};
-    if (act) {
-        if (p.bar) {
-            const float* barb = env_bar(p, b);
-            in.cn = barb ? barb[(size_t)n * Fm + p.close_ch] : NAN;
-            in.pl = p.prices ? p.prices[i] : p.last_close[i];
-        } else {
-            in.pl = p.prices[i];
-        }
-    }
     return in;
 }
 
@@ -453,13 +453,21 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
     return act ? (float)(pv / value) : 0.0f;
 }
 
-template <int L>
+// P env groups per wave in sequence, all their loads issued first: P times the
+// bytes in flight per wave for a latency-bound kernel
+template <int L, int P>
 __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
-    constexpr int EPW = 64 / L;                   // envs per wave
+    constexpr int EPW = 64 / L;                   // envs per wave and group
     const int lane = threadIdx.x & 63;
-    const int b = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * EPW + lane / L;
-    int32_t k;
-    (void)scalar_finish<L>(p, b, lane, scalar_load<L>(p, b, lane), k);
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    ScalarIn in[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) in[j] = scalar_load<L>(p, (w * P + j) * EPW + lane / L, lane);
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        int32_t k;
+        (void)scalar_finish<L>(p, (w * P + j) * EPW + lane / L, lane, in[j], k);
+    }
 }
 
 // ---------------------------------------------------------------- K2: window advance

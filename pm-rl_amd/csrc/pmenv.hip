@@ -45,6 +45,7 @@ struct pmenv {
     int unit_rows, units_per_env, stream_vec;          // in-place advance
     int unit_rows_db, units_per_env_db, stream_vec_db; // double-buffered advance (obs_out)
     int scalar_scratch_floats;
+    int k1_groups;        // env groups per wave in scalar_step_reg_kernel
     int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
     int ablate;           // PMENV_ABLATE timing-only variants of advance_rows_kernel (0 = product)
     size_t lds_scalar, lds_stream;
@@ -159,6 +160,22 @@ void launch_advance_a(int vec, const StepParams& p, unsigned grid, hipStream_t s
 }
 
 constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
+
+template <int L>
+void launch_scalar_reg_l(int groups, const StepParams& p, hipStream_t stream) {
+    const int per_wave = (64 / L) * groups;
+    const unsigned waves = (unsigned)((p.B + per_wave - 1) / per_wave);
+    const unsigned grid = (waves + 3) / 4;
+    if (groups == 4) scalar_step_reg_kernel<L, 4><<<grid, 256, 0, stream>>>(p);
+    else if (groups == 2) scalar_step_reg_kernel<L, 2><<<grid, 256, 0, stream>>>(p);
+    else scalar_step_reg_kernel<L, 1><<<grid, 256, 0, stream>>>(p);
+}
+
+// K1 register form (N <= 64): two envs per wave up to 32 assets
+void launch_scalar_reg(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    if (p.N <= 32) launch_scalar_reg_l<32>(h->k1_groups, p, stream);
+    else launch_scalar_reg_l<64>(h->k1_groups, p, stream);
+}
 
 // one launch per step: whole-env units (the double-buffered geometry), scalar step
 // inside the workgroup (N <= 64)
@@ -315,6 +332,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     if (const char* knob = getenv("PMENV_ADVANCE"))   // A/B knob: force the single-launch LDS kernel
         if (!strcmp(knob, "lds")) h->streaming = false;
     if (const char* knob = getenv("PMENV_ABLATE")) h->ablate = atoi(knob);
+    h->k1_groups = 1;
+    if (const char* knob = getenv("PMENV_K1_GROUPS")) h->k1_groups = atoi(knob);   // A/B knob: 1 | 2 | 4
+    if (h->k1_groups != 2 && h->k1_groups != 4) h->k1_groups = 1;
     if (h->streaming) {
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
         h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
@@ -462,11 +482,8 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         }
         if (ph & PMENV_PHASE_SCALAR) {
             const int N = h->cfg.num_assets;
-            if (N <= 32) {
-                const int waves = (B + 1) / 2;
-                scalar_step_reg_kernel<32><<<(waves + 3) / 4, 256, 0, stream>>>(p);
-            } else if (N <= 64) {
-                scalar_step_reg_kernel<64><<<(B + 3) / 4, 256, 0, stream>>>(p);
+            if (N <= 64) {
+                launch_scalar_reg(h, p, stream);
             } else {
                 scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar,
                                      stream>>>(p, h->scalar_scratch_floats);
@@ -573,23 +590,36 @@ int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N
 int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
               int32_t B, float gamma, float lam, hipStream_t stream) {
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
-    // few envs x long horizon: wave-per-env chunked scan; otherwise one thread per env
-    // (coalesced across envs, already bandwidth-bound)
-    const char* knob = getenv("PMENV_GAE");
-    const bool scan = knob ? !strcmp(knob, "scan") : (B < 4096 && T >= 256);
-    if (scan)
+    // measured on MI355X (tools/bench_rows.py, profiles/rows_r01.json): the tiled scan
+    // beats the per-env loop 2.7x at T = 256 x B = 65536 and 14x at 2048 x 8192; the
+    // wave-per-env scan only for a handful of envs with long horizons
+    const char* knob = getenv("PMENV_GAE");        // A/B knob: loop | scan | tile
+    const bool fits = (size_t)(T + 1) * (size_t)B * 4u < (1ull << 31);   // gae_tile_kernel's buffer offsets
+    const bool scan = knob ? !strcmp(knob, "scan") : (B < 64 && T >= 256);
+    const bool tile = fits && (knob ? !strcmp(knob, "tile") : !scan);
+    const char* uknob = getenv("PMENV_GAE_U");    // A/B knob: steps per lane and segment (8 | 16)
+    const int U = uknob ? atoi(uknob) : (B >= 16384 ? 8 : 16);
+    if (tile && U == 16)
+        gae_tile_kernel<8, 16><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                 lam);
+    else if (tile)
+        gae_tile_kernel<8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                lam);
+    else if (scan)
         gae_scan_kernel<<<(B + 3) / 4, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
     else
         gae_kernel<<<(B + 255) / 256, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
-int pmenv_moments(const float* x, int64_t n, double* out, hipStream_t stream) {
-    if (!x || !out || n < 0) return PMENV_ERR_ARG;
-    int64_t want = (n + kMomBlock * 4 - 1) / (kMomBlock * 4);
-    int blocks = (int)(want < 1 ? 1 : (want > kMomBlocks ? kMomBlocks : want));
-    moments_partial_kernel<<<blocks, kMomBlock, 0, stream>>>(x, n);
-    moments_final_kernel<<<1, 64, 0, stream>>>(blocks, n, out);
+size_t pmenv_moments_workspace(void) { return (size_t)kMomBlocks * 2 * sizeof(double); }
+
+int pmenv_moments(const float* x, int64_t n, double* out, double* work, hipStream_t stream) {
+    if ((!x && n > 0) || !out || !work || n < 0) return PMENV_ERR_ARG;
+    const int64_t want = (n + kMomBlock * 16 - 1) / (kMomBlock * 16);   // >= 16 floats per thread
+    const int blocks = (int)(want < 1 ? 1 : (want > kMomBlocks ? kMomBlocks : want));
+    moments_partial_kernel<<<blocks, kMomBlock, 0, stream>>>(x, n, work);
+    moments_final_kernel<<<1, kMomBlock, 0, stream>>>(blocks, n, work, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -600,21 +630,30 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     if (!series || !days || !actions || !rewards || !h0 || !env || !s || !s_next || !a_out || !r_out || T < 1 ||
         N < 1 || F < 2 || W < 1 || H < W + 1 || B < 1 || S < 1)
         return PMENV_ERR_ARG;
-    const int64_t threads = (int64_t)S * N * W * F;
-    replay_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
-        series, T, N, F, W, days, actions, rewards, H, B, h0, env, S, s, s_next, a_out, r_out);
+    // one workgroup per sample with the W+1 staged days in LDS when they fit in 64 KiB
+    // (N = 30, W = 50: 30.6 KiB), else one thread per output float
+    const size_t lds = (size_t)N * (W + 1) * F * sizeof(float);
+    if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
+        replay_gather_lds_kernel<<<(unsigned)S, 256, lds, stream>>>(series, T, N, F, W, days, actions, rewards, H, B,
+                                                                   h0, env, s, s_next, a_out, r_out);
+    } else {
+        const int64_t threads = (int64_t)S * N * W * F;
+        replay_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
+            series, T, N, F, W, days, actions, rewards, H, B, h0, env, S, s, s_next, a_out, r_out);
+    }
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
 int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B, int32_t N,
                   double risk_free_rate, double periods, double* out, hipStream_t stream) {
     if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;
-    metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, weights, T, B, N, risk_free_rate, periods,
-                                                        out);
+    metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
+    const int tpe = N <= 256 ? N : 256, eb = 256 / tpe;
+    metrics_turnover_kernel<<<(unsigned)((B + eb - 1) / eb), 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
-size_t pmenv_batch_reward_workspace(int32_t B) { return B < 1 ? 0 : ((size_t)6 * B + 8) * 8; }
+size_t pmenv_batch_reward_workspace(int32_t B) { return B < 1 ? 0 : batch_reward_work_doubles(B) * 8; }
 
 int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
                                int32_t reward_kind, int32_t norm, double scale, double* work,
@@ -624,8 +663,10 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         reward_kind != PMENV_REWARD_SHARPE)
         return PMENV_ERR_ARG;
     if (norm < PMENV_BNORM_GLOBAL_OR || norm > PMENV_BNORM_NONE) return PMENV_ERR_ARG;
-    batch_reward_rows_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, work);
-    batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out, ret_out);
+    batch_reward_rows_kernel<<<(unsigned)batch_reward_blocks(B), kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
+                                                                                          reward_kind, work);
+    batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out);
+    batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

@@ -55,8 +55,8 @@ __global__ void replay_gather_kernel(const float* series, int T, int N, int F, i
 
 // one thread per env walks its column of the trajectory (coalesced across envs)
 //   out[b] = {sharpe, sortino, max drawdown, average turnover, final value}
-__global__ void metrics_kernel(const double* returns, const double* values, const float* weights, int T, int B,
-                               int N, double rf, double periods, double* out) {
+__global__ void metrics_kernel(const double* returns, const double* values, int T, int B, double rf,
+                               double periods, double* out) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     // qs.stats.sharpe / sortino: excess returns over the per-period rate
@@ -80,16 +80,105 @@ __global__ void metrics_kernel(const double* returns, const double* values, cons
         peak = fmax(peak, v);
         mdd = fmin(mdd, v / peak - 1.0);
     }
-    // util/eval.py:32-37 average turnover over the weight history
-    double turn = 0.0;
-    for (int t = 1; t <= T; ++t)
-        for (int n = 0; n < N; ++n)
-            turn += fabs((double)weights[((size_t)t * B + b) * N + n] - (double)weights[((size_t)(t - 1) * B + b) * N + n]);
     out[(size_t)b * 5 + 0] = sharpe;
     out[(size_t)b * 5 + 1] = sortino;
     out[(size_t)b * 5 + 2] = mdd;
-    out[(size_t)b * 5 + 3] = T > 0 ? turn / T : NAN;
     out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
+}
+
+
+// util/eval.py:32-37 average turnover, element-parallel: a workgroup owns `eb` whole
+// envs (N <= 256: one thread per (env, asset), so each day's read is eb*N contiguous
+// floats) and every thread walks the days keeping the previous weight in a
+// register; the env's assets are then summed in a fixed order. N > 256: one env
+// per workgroup, threads stride over the assets.
+__global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
+                                                               int eb, double* out) {
+    __shared__ double sh[256];
+    const int tid = threadIdx.x;
+    const int el = tid % tpe, le = tid / tpe;
+    const int b = blockIdx.x * eb + le;
+    double acc = 0.0;
+    if (le < eb && b < B) {
+        for (int n = el; n < N; n += tpe) {
+            const float* w = weights + (size_t)b * N + n;
+            const size_t step = (size_t)B * N;
+            float prev = w[0];
+            int t = 1;
+            for (; t + 3 <= T; t += 4) {
+                const float x1 = w[(size_t)t * step], x2 = w[(size_t)(t + 1) * step];
+                const float x3 = w[(size_t)(t + 2) * step], x4 = w[(size_t)(t + 3) * step];
+                acc += fabs((double)x1 - (double)prev) + fabs((double)x2 - (double)x1) +
+                       fabs((double)x3 - (double)x2) + fabs((double)x4 - (double)x3);
+                prev = x4;
+            }
+            for (; t <= T; ++t) {
+                const float x = w[(size_t)t * step];
+                acc += fabs((double)x - (double)prev);
+                prev = x;
+            }
+        }
+    }
+    sh[tid] = acc;
+    __syncthreads();
+    if (el == 0 && le < eb && b < B) {
+        double tot = 0.0;
+        for (int i = 0; i < tpe; ++i) tot += sh[le * tpe + i];
+        out[(size_t)b * 5 + 3] = tot / T;
+    }
+}
+
+// replay/buffer.py:53-79, one workgroup per sample: the W+1 days the pair (s, s')
+// spans — market channels from the series, channel F-1 from the recorded actions —
+// are staged in LDS as [N][W+1][F], then s (days 0..W-1) and s' (days 1..W) are
+// written as whole 16-B chunks when the sample block is 16-B granular.
+__global__ __launch_bounds__(256) void replay_gather_lds_kernel(const float* series, int T, int N, int F, int W,
+                                                                const int32_t* days, const float* actions,
+                                                                const float* rewards, int H, int B,
+                                                                const int32_t* h0, const int32_t* env, float* s,
+                                                                float* s_next, float* a_out, float* r_out) {
+    extern __shared__ __attribute__((aligned(16))) float ext[];
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const int b = env[j], hj = h0[j];
+    const int Fm = F - 1, W1 = W + 1;
+    const int dlast = days[(size_t)((hj + W - 1) % H) * B + b];
+    for (int it = tid; it < N * W1; it += 256) {                 // t-major: a day's assets are contiguous
+        const int t = it / N, n = it - t * N;
+        const int d = dlast - (W - 1) + t;
+        float* dst = ext + ((size_t)n * W1 + t) * F;
+        const bool in = d >= 0 && d < T;
+        const float* src = series + ((size_t)(in ? d : 0) * N + n) * Fm;
+        for (int f = 0; f < Fm; ++f) dst[f] = in ? src[f] : NAN;
+        dst[Fm] = actions[((size_t)((hj + t) % H) * B + b) * N + n];
+    }
+    if (tid < N) a_out[(size_t)j * N + tid] = actions[((size_t)((hj + W) % H) * B + b) * N + tid];
+    if (tid == 0) r_out[j] = rewards[(size_t)((hj + W - 1) % H) * B + b];
+    __syncthreads();
+    const int WF = W * F, per = N * WF;
+    float* so = s + (size_t)j * per;
+    float* sn = s_next + (size_t)j * per;
+    if ((per & 3) == 0) {
+        for (int q = tid; q < per / 4; q += 256) {
+            float v0[4], v1[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = 4 * q + k;
+                const int n = e / WF, rem = e - n * WF;
+                const float* x = ext + (size_t)n * W1 * F + rem;
+                v0[k] = x[0];
+                v1[k] = x[F];
+            }
+            reinterpret_cast<f4*>(so)[q] = f4{v0[0], v0[1], v0[2], v0[3]};
+            reinterpret_cast<f4*>(sn)[q] = f4{v1[0], v1[1], v1[2], v1[3]};
+        }
+    } else {
+        for (int e = tid; e < per; e += 256) {
+            const int n = e / WF, rem = e - n * WF;
+            const float* x = ext + (size_t)n * W1 * F + rem;
+            so[e] = x[0];
+            sn[e] = x[F];
+        }
+    }
 }
 
 }  // namespace pmenv_dev

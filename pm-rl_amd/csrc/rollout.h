@@ -73,37 +73,154 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const flo
     }
 }
 
+// GAE as a tiled scan for many envs: a workgroup owns 64 envs (one per lane, so
+// every load and store is a coalesced 256-B row of the time-major rollout) and
+// walks the horizon backwards in segments of NW x U steps; wave w holds sub-chunk
+// w of the segment in registers (each input read exactly once), reduces it to its
+// affine map (C, D), and after one LDS exchange composes the later sub-chunks'
+// maps onto the segment's carry to get its own carry-in, then re-walks its
+// registers writing adv / ret. f64 throughout, like the sequential recursion.
+// Loads are buffer loads with the lane's env as the (only) VGPR offset and the
+// wave-uniform row as the SGPR offset, so U rows in flight cost no address VGPRs.
+// Needs every array below 2 GiB (the host checks).
+template <int NW, int U>
+__global__ __launch_bounds__(64 * NW) void gae_tile_kernel(const float* r, const float* v, const uint8_t* dones,
+                                                          float* adv, float* ret, int T, int B, float gamma,
+                                                          float lam) {
+    __shared__ double shC[NW][64], shD[NW][64];
+    constexpr int S = NW * U;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: rows go in SGPRs
+    const int b = blockIdx.x * 64 + lane;
+    const bool ok = b < B;
+    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
+    const uint32_t row = (uint32_t)B * 4u;
+    const auto rs_r = make_rsrc(r, (uint32_t)T * row);
+    const auto rs_v = make_rsrc(v, (uint32_t)(T + 1) * row);
+    const auto rs_d = make_rsrc(dones ? (const void*)dones : (const void*)r, dones ? (uint32_t)T * (uint32_t)B : 0u);
+    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
+    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
+    const uint32_t voff_st = ok ? voff : 0x80000000u;
+    const double g = (double)gamma, gl = (double)gamma * (double)lam;
+    double carry = 0.0;                           // advantage just after the current segment
+    for (int seg_end = T; seg_end > 0; seg_end -= S) {
+        const int seg_start = max(seg_end - S, 0);
+        const int t0 = seg_start + w * U;
+        float vv[U + 1], rr[U];
+        uint32_t alive = 0;                       // bit u: 1 - done_t
+#pragma unroll
+        for (int u = 0; u <= U; ++u) {            // v has T + 1 rows: row seg_end is the bootstrap
+            const uint32_t t = (uint32_t)min(t0 + u, seg_end);
+            vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
+            rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
+            // no dones: the descriptor has no records and every load reads 0 (alive)
+            const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
+            alive |= (dn ? 0u : 1u) << u;
+        }
+        double dl[U];                             // delta_t, kept for the second walk
+        double C = 1.0, D = 0.0;
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u) {
+            const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+            dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
+            if (t0 + u < seg_end) {
+                D = dl[u] + gl * n * D;
+                C = gl * n * C;
+            }
+        }
+        shC[w][lane] = C;
+        shD[w][lane] = D;
+        __syncthreads();
+        double a = carry;
+        for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u) {
+            const int t = t0 + u;
+            if (t < seg_end) {
+                const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+                a = dl[u] + gl * n * a;
+                // lanes past B: voff is out of range for the store descriptors -> dropped
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret, voff_st,
+                                                      (uint32_t)t * row, 0);
+            }
+        }
+        for (int j = NW - 1; j >= 0; --j) carry = shD[j][lane] + shC[j][lane] * carry;
+        __syncthreads();                          // the LDS maps are rewritten next segment
+    }
+}
+
 constexpr int kMomBlock = 256;
 constexpr int kMomBlocks = 1024;
-__device__ double g_mom_partial[kMomBlocks * 3];
 
-__global__ __launch_bounds__(kMomBlock) void moments_partial_kernel(const float* x, int64_t n) {
+// {sum, sum of squares} per block into work[2 * block]: 16-B loads (after a scalar
+// head up to the first 16-B boundary), four in flight per thread, f64 accumulation,
+// fixed thread -> element assignment (deterministic for a given n).
+__global__ __launch_bounds__(kMomBlock) void moments_partial_kernel(const float* x, int64_t n, double* work) {
     __shared__ double sh[2][kMomBlock / 64];
-    double s = 0.0, q = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kMomBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kMomBlock) {
-        double v = (double)x[i];
-        s += v;
-        q += v * v;
+    const int64_t head = min<int64_t>(n, (int64_t)(((16u - ((uintptr_t)x & 15u)) & 15u) / 4u));
+    const f4* x4 = reinterpret_cast<const f4*>(x + head);
+    const int64_t n4 = (n - head) / 4;
+    const int64_t tail0 = head + n4 * 4;
+    const int64_t stride = (int64_t)gridDim.x * kMomBlock;
+    double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+    auto add4 = [&](f4 v) {
+        const double a = v.x, b = v.y, c = v.z, d = v.w;
+        s0 += a + b;
+        s1 += c + d;
+        q0 += a * a + b * b;
+        q1 += c * c + d * d;
+    };
+    int64_t i = (int64_t)blockIdx.x * kMomBlock + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const f4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+        add4(a);
+        add4(b);
+        add4(c);
+        add4(d);
     }
+    for (; i < n4; i += stride) add4(x4[i]);
+    if (blockIdx.x == 0) {                        // head and tail elements
+        const int64_t k = threadIdx.x;
+        if (k < head) { const double v = x[k]; s0 += v; q0 += v * v; }
+        if (tail0 + k < n) { const double v = x[tail0 + k]; s1 += v; q1 += v * v; }
+    }
+    double s = s0 + s1, q = q0 + q1;
     for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { sh[0][w] = s; sh[1][w] = q; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double ts = 0.0, tq = 0.0;
-        for (int i = 0; i < kMomBlock / 64; ++i) { ts += sh[0][i]; tq += sh[1][i]; }
-        g_mom_partial[blockIdx.x * 3 + 0] = ts;
-        g_mom_partial[blockIdx.x * 3 + 1] = tq;
+        for (int j = 0; j < kMomBlock / 64; ++j) { ts += sh[0][j]; tq += sh[1][j]; }
+        work[blockIdx.x * 2 + 0] = ts;
+        work[blockIdx.x * 2 + 1] = tq;
     }
 }
 
-__global__ void moments_final_kernel(int nblocks, int64_t n, double* out) {
-    if (threadIdx.x != 0) return;
+// one workgroup folds the block partials in a fixed shape: thread t adds partials
+// t, t + 256, ... in order, then a DPP/shuffle tree per wave and the 4 wave totals
+// in order
+__global__ __launch_bounds__(kMomBlock) void moments_final_kernel(int nblocks, int64_t n, const double* work,
+                                                                  double* out) {
+    __shared__ double sh[2][kMomBlock / 64];
     double s = 0.0, q = 0.0;
-    for (int i = 0; i < nblocks; ++i) { s += g_mom_partial[i * 3 + 0]; q += g_mom_partial[i * 3 + 1]; }
-    out[0] = (double)n;
-    out[1] = s;
-    out[2] = q;
+    for (int i = threadIdx.x; i < nblocks; i += kMomBlock) { s += work[i * 2 + 0]; q += work[i * 2 + 1]; }
+    for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = s; sh[1][w] = q; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double ts = 0.0, tq = 0.0;
+        for (int j = 0; j < kMomBlock / 64; ++j) { ts += sh[0][j]; tq += sh[1][j]; }
+        out[0] = (double)n;
+        out[1] = ts;
+        out[2] = tq;
+    }
 }
 
 }  // namespace pmenv_dev

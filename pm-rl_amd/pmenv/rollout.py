@@ -38,6 +38,7 @@ def moments(x):
     lib = _abi.load()
     x = x.to(torch.float32).contiguous().reshape(-1)
     out = torch.empty(3, dtype=torch.float64, device=x.device)
+    work = torch.empty(lib.pmenv_moments_workspace() // 8, dtype=torch.float64, device=x.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    _abi.check(lib.pmenv_moments(_p(x), x.numel(), _p(out), s), None, "pmenv_moments")
+    _abi.check(lib.pmenv_moments(_p(x), x.numel(), _p(out), _p(work), s), None, "pmenv_moments")
     return out

@@ -287,12 +287,18 @@ def test_gpu_synth_matches_oracle():
 
 
 @pytest.mark.parametrize("T,B,path", [(5000, 3, "scan"), (257, 64, "scan"), (64, 65536, "loop"), (300, 10, "loop"),
-                                      (1, 5, "scan"), (63, 2, "scan")])
+                                      (1, 5, "scan"), (63, 2, "scan"),
+                                      # tiled: T below / across / not a multiple of the segment, ragged B
+                                      (1, 5, "tile"), (37, 100, "tile"), (64, 64, "tile"), (129, 4099, "tile"),
+                                      (1000, 200, "tile"), (256, 65536, "tile"), (300, 130, "tile16")])
 def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
-    """GAE(gamma, lambda) over a [T, B] rollout: chunked wave scan and per-env loop
-    vs the oracle's sequential recursion (parity unpinned by the reference)."""
+    """GAE(gamma, lambda) over a [T, B] rollout: tiled scan, chunked wave scan and
+    per-env loop vs the oracle's sequential recursion (parity unpinned by the
+    reference)."""
     from pmenv import rollout
-    monkeypatch.setenv("PMENV_GAE", path)
+    monkeypatch.setenv("PMENV_GAE", path.rstrip("16"))
+    if path.endswith("16"):
+        monkeypatch.setenv("PMENV_GAE_U", "16")
     rng = np.random.default_rng(T + B)
     r = rng.standard_normal((T, B)).astype(np.float32)
     v = rng.standard_normal((T + 1, B)).astype(np.float32)
@@ -319,6 +325,18 @@ def test_gpu_gae_and_moments_match_oracle():
     om = or_moments(x)
     assert m[0] == om[0]
     np.testing.assert_allclose(m[1:], om[1:], rtol=1e-9)
+
+
+@pytest.mark.parametrize("n,off", [(0, 0), (1, 0), (3, 1), (5, 2), (1000, 3), (4099, 1), (3_000_001, 2)])
+def test_gpu_moments_alignment_and_ragged_sizes(n, off):
+    """16-B vector body + scalar head/tail: any start alignment and length."""
+    from pmenv import rollout
+    rng = np.random.default_rng(n + off)
+    x = rng.standard_normal(n + off).astype(np.float32)
+    m = rollout.moments(_t(x)[off:]).cpu().numpy()
+    om = or_moments(np.ascontiguousarray(x[off:]))
+    assert m[0] == om[0] == n
+    np.testing.assert_allclose(m[1:], om[1:], rtol=1e-9, atol=1e-9)
 
 
 def test_gpu_errors_mirror_reference():
@@ -409,19 +427,21 @@ def test_gpu_resident_series_equals_bar_batch():
     assert ea.nonfinite_count() == 1
 
 
-def test_gpu_replay_gather_matches_restatement():
+@pytest.mark.parametrize("T,N,W,B,H", [(200, 30, 12, 33, 40),    # LDS-staged, 16-B stores
+                                       (60, 3, 5, 4, 9),          # LDS-staged, sample block not 16-B granular
+                                       (120, 300, 50, 3, 60)])    # staged days > 64 KiB: per-float kernel
+def test_gpu_replay_gather_matches_restatement(T, N, W, B, H):
     """replay/buffer.py:39-79 sample on device vs the numpy restatement
     (the reference module is not importable: parity restated from its text)."""
     from pmenv import MarketSeries
     from pmenv.replay import DeviceReplay
     from oracle import replay_gather
     rng = np.random.default_rng(4)
-    T, N, W, B, H = 200, 30, 12, 33, 40
     bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
     m = MarketSeries(bars, device=DEV)
     rb = DeviceReplay(B, N, W, H, m)
-    for h in range(H + 17):                      # wraps the ring
-        rb.add(torch.full((B,), W + h % (T - W - 2), dtype=torch.int32, device=DEV),
+    for h in range(H + 17):                      # wraps the ring; some windows run off the series ends
+        rb.add(torch.full((B,), (W + h) % (T + 3) - 2, dtype=torch.int32, device=DEV),
                torch.rand(B, N, device=DEV), torch.randn(B, device=DEV))
     h0, env = rb.indices(64, generator=torch.Generator().manual_seed(1))
     s, a, r, s2 = rb.gather(h0, env)
@@ -432,11 +452,13 @@ def test_gpu_replay_gather_matches_restatement():
     assert np.array_equal(a.cpu().numpy()[..., 0], ea) and np.array_equal(r.cpu().numpy()[:, 0, 0], er)
 
 
-def test_gpu_trajectory_metrics_match_restatement():
+@pytest.mark.parametrize("B,N,W,T", [(300, 30, 20, 80), (5, 300, 4, 9), (70, 1, 3, 2), (9, 257, 2, 5)])
+def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
+    """util/eval.py:14-37 metrics over an env trajectory vs the numpy restatement
+    (quantstats is absent: parity unpinned by the reference)."""
     from pmenv import TradingEnv, synth
     from pmenv.replay import trajectory_metrics
     from oracle import trajectory_metrics as ref_metrics
-    B, N, W, T = 300, 30, 20, 80
     ser = synth.series(W + T, B, N, device=DEV)
     act = synth.actions(T, B, N, device=DEV)
     obs = synth.window_from_series(ser, W)

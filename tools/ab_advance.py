@@ -20,6 +20,7 @@ ap.add_argument("--window", type=int, default=50)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--H", type=int, default=64)
+ap.add_argument("--phases", type=int, default=0, help="pmenv_step_args.phases (1: scalar step only)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 B, N, W = a.envs, a.assets, a.window
@@ -27,7 +28,7 @@ lib = _abi.load()
 ser = synth.series(a.H + W, B, N, device=dev)
 act = synth.actions(a.H, B, N, device=dev)
 envs = {}
-KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED")
+KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED", "PMENV_K1_GROUPS")
 for v in a.variants.split(","):
     # "base+KNOB=val+...": extra env knobs at creation (e.g. "o+PMENV_FUSED=0")
     base, *extra = v.split("+")
@@ -74,6 +75,7 @@ for r in range(a.rounds):
             args.obs = src.data_ptr()
             args.obs_out = dst.data_ptr() if dst is not None else None
             args.reward = rew.data_ptr()
+            args.phases = a.phases
             rc = lib.pmenv_step_ex(e._h, ctypes.byref(args), sp)
             assert rc == 0
         s1.record(stream)
