@@ -9,7 +9,7 @@ price relatives from the close channel, action normalisation, portfolio value
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
 assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
 Philox OHLC series and softmax actions already resident in HBM. The step runs as
-two launches (scalar_step_kernel, then the streaming advance_rows_kernel); the
+two launches (scalar_step_kernel, then the streaming advance_flat_kernel); the
 window is double-buffered by default (each day's window is a fresh buffer, as the
 reference's data path hands the env a new window every day — instrument.py:339-356),
 and the in-place advance is timed as well and reported under "inplace".
@@ -249,6 +249,13 @@ def main():
         elapsed, kern_avg_s = float(t[0]), float(t[1])
     nonfinite = env.nonfinite_count()
 
+    path = env.step_path
+    if double and "advance_flat_kernel" in path:
+        advance_kernel = "advance_flat_kernel"
+    elif "step_advance_lds_kernel" in path:
+        advance_kernel = "step_advance_lds_kernel"
+    else:
+        advance_kernel = "advance_rows_kernel"
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
     bstep = step_bytes(N, W, F)
@@ -289,7 +296,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "advance_rows_kernel", "kernel_avg_us": kern_avg_s * 1e6,
+                "kernel": advance_kernel, "kernel_avg_us": kern_avg_s * 1e6,
                 "bytes_per_env_step": bstep,
             },
             "cpu_baseline": cpu,

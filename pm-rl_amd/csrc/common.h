@@ -85,16 +85,19 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
+// AUX = the instruction's cache-policy bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+template <int AUX = 0>
 __device__ __forceinline__ f4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
     return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
 }
 __device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+template <int AUX = 0>
 __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, uint32_t off, f4 v) {
     const u4v u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX);
 }
 
 // ---------------------------------------------------------------- wave reductions

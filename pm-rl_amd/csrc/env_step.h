@@ -492,8 +492,13 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
 // FUSED (whole-env units, N <= 64): the workgroup also runs the env's scalar step
 // on its first wave, after every streaming load is in flight, and hands w' and the
 // counter to the other waves through LDS — one launch per step instead of two.
-template <int BLOCK, int V, bool INPLACE, int ABL = 0, bool FUSED = false>
+// POL: cache policy of the 16-B window stream (the shifted-source loads and the
+// stores), every byte of which is touched once per step: 0 = default, 1 = nt,
+// 2 = sc0 nt (aux bits 2 / 3). The small bar / w' / unshifted-weight loads re-read
+// lines other lanes fetch and keep the default policy.
+template <int BLOCK, int V, bool INPLACE, int ABL = 0, bool FUSED = false, int POL = 0>
 __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
+    constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
     constexpr int F = 5;
     const int tid = threadIdx.x;
     const int N = p.N, W = p.W;
@@ -511,7 +516,7 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
     const auto rs_env = make_rsrc(env_obs, (uint32_t)(N * WF) * 4u);
     float* env_out = p.obs_out + (size_t)b * N * WF;
     const auto rs_unit = make_rsrc(env_out + (size_t)r0 * WF, nf * 4u);
-    const float* barb = env_bar(p, b);            // null: out-of-range day -> the descriptor reads 0
+    const float* barb = env_bar(p, b);            // null: out-of-range day -> NaN bar (wave-uniform)
     const auto rs_bar = make_rsrc(barb ? barb : p.bar, barb ? (uint32_t)(rows + r0) * 16u : 0u);
     const auto rs_wp = make_rsrc(p.w_new + (size_t)b * N, (uint32_t)(rows + r0) * 4u);
 
@@ -530,14 +535,15 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
         const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
         const int ew = min(F - 1 - f0, 3);                // element holding the weight channel
         kk0[i] = kk;
-        xs[i] = buf_load4(rs_env, unit_off + (j0 + F) * 4u);                 // shifted source
+        xs[i] = buf_load4<kAux>(rs_env, unit_off + (j0 + F) * 4u);           // shifted source
         xb[i] = f4{0.f, 0.f, 0.f, 0.f};
         xwp[i] = 0.f;
         xun[i] = 0.f;
         if (FUSED) {
             kk0[i] |= (int)min(row, 63u) << 16;                             // asset: bar and w' from LDS
         } else if (!(ABL & 1)) {
-            xb[i] = buf_load4(rs_bar, (uint32_t)(r0 + (int)row) * 16u);     // the asset's new bar
+            xb[i] = barb ? buf_load4(rs_bar, (uint32_t)(r0 + (int)row) * 16u)   // the asset's new bar
+                         : f4{NAN, NAN, NAN, NAN};                              // day outside the series
             xwp[i] = buf_load1(rs_wp, (uint32_t)(r0 + (int)row) * 4u);      // its new weight w'
         }
         if (!(ABL & 2)) xun[i] = buf_load1(rs_env, unit_off + (j0 + (uint32_t)ew) * 4u);   // unshifted weight
@@ -551,7 +557,7 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
             int32_t kb;
             const float wp = scalar_finish<64, true>(p, b, tid, sin, kb);
             sh_wp[tid] = wp;
-            sh_bar[tid] = sin.bar;
+            sh_bar[tid] = sin.bar_ok ? sin.bar : f4{NAN, NAN, NAN, NAN};
             if (tid == 0) sh_k = kb;
         }
         if (INPLACE) __builtin_amdgcn_s_waitcnt(0);
@@ -596,9 +602,117 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
             if (kk == WF) kk = 0;
         }
         if (ABL & 4) v[0] += bv[0] + xwp[i] + xun[i];
-        buf_store4(rs_unit, q * 16u, f4{v[0], v[1], v[2], v[3]});        // lanes past the unit: dropped
+        buf_store4<kAux>(rs_unit, q * 16u, f4{v[0], v[1], v[2], v[3]});  // lanes past the unit: dropped
     }
     (void)nq;
+}
+
+// ---------------------------------------------------------------- K2, double-buffered: flat stream
+// The out-of-place advance as a flat 16-B stream over the whole [B, N, W, F] tensor
+// (obs -> obs_out): lane q of the grid owns output chunk q (floats 4q..4q+3) and
+// loads only the ALIGNED input chunk q. The shifted source of chunk q, floats
+// 4q+5..4q+8, is elements 1..3 of chunk q+1 and element 0 of chunk q+2 — the own
+// chunks of lanes l+1 and l+2, moved across the wave with ds_bpermute; lanes 62 and
+// 63 take chunks wbase+64 and wbase+65 from one wave-uniform 32-B load. Each input
+// line is thus fetched by one wave instruction and the workgroup holds one chunk per
+// thread (4 KiB at 256 threads): the shape of the fastest plain copy measured on this
+// chip (tools/copybench.hip). Per element, at row position pos = kk + e of the
+// chunk's asset row (pos >= WF: the chunk has wrapped into the next row, whose
+// positions 0..2 are never a last day or a weight slot for W >= 2, so they take the
+// shifted value):
+//   market:  pos >= WF-F (last day) ? bar[f] : shifted
+//   weight:  shift mode: last day ? w' : shifted;  storage mode: pos == slot ? w' : own
+// The bar is fetched only by lanes whose chunk touches the row's last day (the other
+// lanes' offsets are out of the descriptor's range: no traffic).
+// Requirements (host-checked): F == 5, W >= 2, N*W*F % 4 == 0, B*N*W*F/4 < 2^31.
+// branch-free float select (bit masks: keeps the element loop free of control flow)
+__device__ __forceinline__ float pick(bool c, float a, float b) {
+    const int m = -(int)c;
+    return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+}
+
+template <int BLOCK, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint32_t qtot) {
+    constexpr int F = 5;
+    constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform by construction; readfirstlane lets the descriptors live in SGPRs
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(blockIdx.x * BLOCK + (threadIdx.x & ~63u));
+    if (wbase >= qtot) return;
+    const int N = p.N, W = p.W, WF = W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;                        // chunks per env
+    const uint32_t nwave = min(64u, qtot - wbase);
+    const auto rs_src = make_rsrc(p.obs + (size_t)wbase * 4, nwave * 16u);
+    const f4 own = buf_load4<kAux>(rs_src, (uint32_t)lane * 16u);
+    // chunks wbase+64 and wbase+65, into lanes 62 and 63 (range-checked: past the
+    // tensor's end they read 0 — only last-day positions, which the bar replaces,
+    // would take them)
+    const uint32_t qx = wbase + 64u;
+    const auto rs_ext = make_rsrc(p.obs + (size_t)qx * 4, qx < qtot ? min(2u, qtot - qx) * 16u : 0u);
+    const f4 ext = buf_load4<0>(rs_ext, lane >= 62 ? (uint32_t)(lane - 62) * 16u : 0xFFFFFFF0u);
+    // lanes past the tensor's end (last wave) index as its last chunk: loads stay in
+    // bounds, their stores are dropped by the range check
+    const uint32_t q = min(wbase + (uint32_t)lane, qtot - 1u);
+    const uint32_t b = fdiv(q, p.div_units);                              // div_units: per4 here
+    const uint32_t j0 = 4u * (q - b * per4);
+    const uint32_t row = fdiv(j0, p.div_wf);
+    const int kk = (int)(j0 - row * (uint32_t)WF);
+    const bool touch_last = kk + 3 >= WF - F;
+    // the row's bar — only lanes whose chunk touches the last day; the others' offsets
+    // are out of range (no traffic) — through one descriptor over the whole bar
+    // batch, or over the resident series (day mode, out-of-range days read 0)
+    uint32_t bar_off = 0xFFFFFFF0u, bar_bytes;
+    bool bar_nan = false;                                                 // a day outside the series: NaN bar
+    if (p.day) {
+        const int32_t d = p.day[b];
+        bar_bytes = (uint32_t)p.series_days * (uint32_t)N * 16u;
+        bar_nan = d < 0 || d >= p.series_days;
+        if (touch_last && !bar_nan) bar_off = ((uint32_t)d * (uint32_t)N + row) * 16u;
+    } else {
+        bar_bytes = (uint32_t)p.B * (uint32_t)N * 16u;
+        if (touch_last) bar_off = (b * (uint32_t)N + row) * 16u;
+    }
+    const f4 xb = buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
+    const float xwp = p.w_new[(size_t)b * N + row];
+    const int32_t k = p.k[b] - 1;                                         // scalar_step_kernel counted this step
+    // every load is in flight before the first cross-lane move waits on one
+    __builtin_amdgcn_sched_barrier(0);
+    // neighbours' chunks
+    const int l1 = min(lane + 1, 63) * 4, l2 = min(lane + 2, 63) * 4;
+    float n1y = __int_as_float(__builtin_amdgcn_ds_bpermute(l1, __float_as_int(own.y)));
+    float n1z = __int_as_float(__builtin_amdgcn_ds_bpermute(l1, __float_as_int(own.z)));
+    float n1w = __int_as_float(__builtin_amdgcn_ds_bpermute(l1, __float_as_int(own.w)));
+    float n2x = __int_as_float(__builtin_amdgcn_ds_bpermute(l2, __float_as_int(own.x)));
+    const float x62 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ext.x), 62));
+    const float y62 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ext.y), 62));
+    const float z62 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ext.z), 62));
+    const float w62 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ext.w), 62));
+    const float x63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ext.x), 63));
+    n1y = pick(lane == 63, y62, n1y);
+    n1z = pick(lane == 63, z62, n1z);
+    n1w = pick(lane == 63, w62, n1w);
+    n2x = pick(lane == 63, x63, pick(lane == 62, x62, n2x));
+    const float sh[4] = {n1y, n1z, n1w, n2x};
+    const float un[4] = {own.x, own.y, own.z, own.w};
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
+    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
+    int f = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int pos = kk + e;
+        const bool in_row = pos < WF;
+        const bool lastday = in_row && pos >= WF - F;
+        const bool is_w = in_row && f == F - 1;
+        const float bsel = pick(bar_nan, __int_as_float(0x7fc00000),
+                                pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w))));
+        const bool w_here = shift_w ? lastday : pos == slot_w;
+        const float wv = pick(w_here, xwp, pick(shift_w, sh[e], un[e]));
+        v[e] = pick(is_w, wv, pick(lastday, bsel, sh[e]));
+        f = f == F - 1 ? 0 : f + 1;
+    }
+    const auto rs_dst = make_rsrc(p.obs_out + (size_t)wbase * 4, nwave * 16u);
+    buf_store4<kAux>(rs_dst, (uint32_t)lane * 16u, f4{v[0], v[1], v[2], v[3]});
 }
 
 // ---------------------------------------------------------------- single-launch fallback

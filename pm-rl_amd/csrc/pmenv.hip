@@ -44,6 +44,11 @@ struct pmenv {
     bool streaming;       // scalar_step_kernel + advance_rows_kernel
     int unit_rows, units_per_env, stream_vec;          // in-place advance
     int unit_rows_db, units_per_env_db, stream_vec_db; // double-buffered advance (obs_out)
+    int stream_block, stream_block_db;                 // threads per advance workgroup (128 | 256 | 512)
+    int stream_pol;       // cache policy of the window stream (advance_rows_kernel POL)
+    int fused_vec;        // float4 per thread of the fused one-launch step (512 threads, whole env)
+    bool flat;            // double-buffered advance as the flat 16-B stream (advance_flat_kernel)
+    int flat_block, flat_pol;
     int scalar_scratch_floats;
     int k1_groups;        // env groups per wave in scalar_step_reg_kernel
     int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
@@ -111,23 +116,24 @@ int check_launch(pmenv* h, const char* what) {
     return PMENV_OK;
 }
 
-// Geometry of the streaming path: units of R whole asset rows per 512-thread
-// workgroup, R*W*F floats <= 2048*V (V float4 per thread) and R*W*F % 4 == 0 so
-// every unit starts 16-B aligned. Measured on MI355X at the BASELINE shape
-// (tools/ab_advance.py, interleaved rounds in one process): in place, 16 KiB units
-// (V = 2) beat 32 KiB (V = 4) by ~3 % and 8 KiB (V = 1) by ~20 %; double-buffered,
-// 32 KiB units win by ~3 %. `v_order` lists V in preference order. Returns false
-// when the shape needs the LDS fallback.
-bool plan_streaming(const pmenv_cfg& c, const int* v_order, int* unit_rows, int* vec_per_thread) {
+// Geometry of the streaming path: units of R whole asset rows per `block`-thread
+// workgroup, R*W*F floats <= 4*block*V (V float4 per thread) and R*W*F % 4 == 0 so
+// every unit starts 16-B aligned. `v_order` lists V in preference order. Returns
+// false when the shape needs the LDS fallback. Measured on MI355X at the BASELINE
+// shape (tools/ab_advance.py, interleaved rounds in one process): see the defaults
+// chosen in pmenv_create.
+bool plan_streaming(const pmenv_cfg& c, const int* v_order, int block, int* unit_rows, int* vec_per_thread) {
     const int64_t WF = (int64_t)c.window * c.features;
     if (c.features != 5 || ((int64_t)c.num_assets * WF) % 4 != 0) return false;
     int align = 1;                       // rows per unit must be a multiple of this
     while ((align * WF) % 4 != 0) ++align;
     int want = 0;
     if (const char* knob = getenv("PMENV_UNIT_ROWS")) want = atoi(knob);   // tuning knob
+    static const int kAscending[3] = {1, 2, 4};
+    if (want > 0) v_order = kAscending;   // a forced unit takes the fewest float4 per thread that hold it
     for (int vi = 0; vi < 3; ++vi) {
         const int V = v_order[vi];
-        const int64_t cap = (int64_t)kStreamBlock * 4 * V;
+        const int64_t cap = (int64_t)block * 4 * V;
         int R = (int)(cap / WF);
         if (R >= c.num_assets) R = c.num_assets;
         else R -= R % align;
@@ -144,19 +150,45 @@ bool plan_streaming(const pmenv_cfg& c, const int* v_order, int* unit_rows, int*
     return false;
 }
 
-template <int V, int ABL>
-void launch_advance_v(const StepParams& p, unsigned grid, hipStream_t stream) {
+template <int BLOCK, int V, int ABL, int POL>
+void launch_advance_bv(const StepParams& p, unsigned grid, hipStream_t stream) {
     if (p.obs_out == p.obs)
-        advance_rows_kernel<kStreamBlock, V, true, ABL><<<grid, kStreamBlock, 0, stream>>>(p);
+        advance_rows_kernel<BLOCK, V, true, ABL, false, POL><<<grid, BLOCK, 0, stream>>>(p);
     else
-        advance_rows_kernel<kStreamBlock, V, false, ABL><<<grid, kStreamBlock, 0, stream>>>(p);
+        advance_rows_kernel<BLOCK, V, false, ABL, false, POL><<<grid, BLOCK, 0, stream>>>(p);
 }
 
-template <int ABL>
-void launch_advance_a(int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
-    if (vec == 1) launch_advance_v<1, ABL>(p, grid, stream);
-    else if (vec == 2) launch_advance_v<2, ABL>(p, grid, stream);
-    else launch_advance_v<4, ABL>(p, grid, stream);
+template <int BLOCK, int ABL, int POL>
+void launch_advance_b(int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
+    if (vec == 1) launch_advance_bv<BLOCK, 1, ABL, POL>(p, grid, stream);
+    else if (vec == 2) launch_advance_bv<BLOCK, 2, ABL, POL>(p, grid, stream);
+    else launch_advance_bv<BLOCK, 4, ABL, POL>(p, grid, stream);
+}
+
+template <int BLOCK>
+void launch_flat_b(int pol, const StepParams& p, unsigned grid, uint32_t qtot, hipStream_t stream) {
+    if (pol == 1) advance_flat_kernel<BLOCK, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else if (pol == 2) advance_flat_kernel<BLOCK, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else advance_flat_kernel<BLOCK, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
+}
+
+void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
+    const pmenv_cfg& c = h->cfg;
+    const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
+    const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
+    p.div_units = make_fastdiv(per4);
+    const int bk = h->flat_block;
+    const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
+    if (bk == 128) launch_flat_b<128>(h->flat_pol, p, grid, qtot, stream);
+    else if (bk == 512) launch_flat_b<512>(h->flat_pol, p, grid, qtot, stream);
+    else launch_flat_b<256>(h->flat_pol, p, grid, qtot, stream);
+}
+
+template <int POL>
+void launch_advance_p(int block, int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
+    if (block == 128) launch_advance_b<128, 0, POL>(vec, p, grid, stream);
+    else if (block == 256) launch_advance_b<256, 0, POL>(vec, p, grid, stream);
+    else launch_advance_b<512, 0, POL>(vec, p, grid, stream);
 }
 
 constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
@@ -180,7 +212,7 @@ void launch_scalar_reg(const pmenv* h, const StepParams& p, hipStream_t stream) 
 // one launch per step: whole-env units (the double-buffered geometry), scalar step
 // inside the workgroup (N <= 64)
 void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
-    p.unit_rows = h->unit_rows_db;
+    p.unit_rows = h->cfg.num_assets;
     p.units_per_env = 1;
     p.div_units = make_fastdiv(1u);
     const unsigned grid = (unsigned)h->cfg.num_envs;
@@ -188,8 +220,8 @@ void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
 #define PMENV_FUSED_LAUNCH(V)                                                                        \
     if (inplace) advance_rows_kernel<kStreamBlock, V, true, 0, true><<<grid, kStreamBlock, 0, stream>>>(p); \
     else advance_rows_kernel<kStreamBlock, V, false, 0, true><<<grid, kStreamBlock, 0, stream>>>(p);
-    if (h->stream_vec_db == 1) { PMENV_FUSED_LAUNCH(1) }
-    else if (h->stream_vec_db == 2) { PMENV_FUSED_LAUNCH(2) }
+    if (h->fused_vec == 1) { PMENV_FUSED_LAUNCH(1) }
+    else if (h->fused_vec == 2) { PMENV_FUSED_LAUNCH(2) }
     else { PMENV_FUSED_LAUNCH(4) }
 #undef PMENV_FUSED_LAUNCH
 }
@@ -197,17 +229,25 @@ void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
 // ablation builds are selected only by the PMENV_ABLATE knob (timing studies)
 void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
     const bool db = p.obs_out != p.obs;
+    if (db && h->flat && !h->ablate) {
+        launch_flat(h, p, stream);
+        return;
+    }
     p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
     p.units_per_env = db ? h->units_per_env_db : h->units_per_env;
     p.div_units = make_fastdiv((uint32_t)p.units_per_env);
     const int vec = db ? h->stream_vec_db : h->stream_vec;
+    const int block = db ? h->stream_block_db : h->stream_block;
     const unsigned grid = (unsigned)(h->cfg.num_envs * p.units_per_env);
-    switch (h->ablate) {
-    case 1: launch_advance_a<1>(vec, p, grid, stream); break;
-    case 2: launch_advance_a<2>(vec, p, grid, stream); break;
-    case 3: launch_advance_a<3>(vec, p, grid, stream); break;
-    case 7: launch_advance_a<7>(vec, p, grid, stream); break;
-    default: launch_advance_a<0>(vec, p, grid, stream);
+    switch (h->ablate) {     // timing-only builds: 512-thread geometry, default policy
+    case 1: launch_advance_b<kStreamBlock, 1, 0>(vec, p, grid, stream); break;
+    case 2: launch_advance_b<kStreamBlock, 2, 0>(vec, p, grid, stream); break;
+    case 3: launch_advance_b<kStreamBlock, 3, 0>(vec, p, grid, stream); break;
+    case 7: launch_advance_b<kStreamBlock, 7, 0>(vec, p, grid, stream); break;
+    default:
+        if (h->stream_pol == 1) launch_advance_p<1>(block, vec, p, grid, stream);
+        else if (h->stream_pol == 2) launch_advance_p<2>(block, vec, p, grid, stream);
+        else launch_advance_p<0>(block, vec, p, grid, stream);
     }
 }
 
@@ -327,8 +367,41 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
     // streaming geometry
     static const int kInplaceOrder[3] = {2, 4, 1}, kDoubleOrder[3] = {4, 2, 1};
-    h->streaming = plan_streaming(c, kInplaceOrder, &h->unit_rows, &h->stream_vec) &&
-                   plan_streaming(c, kDoubleOrder, &h->unit_rows_db, &h->stream_vec_db);
+    h->stream_block = h->stream_block_db = kStreamBlock;
+    h->stream_pol = h->flat_pol = 0;
+    if (const char* knob = getenv("PMENV_STREAM_BLOCK")) {        // A/B knob: 128 | 256 | 512
+        const int bk = atoi(knob);
+        if (bk == 128 || bk == 256 || bk == 512) h->stream_block = h->stream_block_db = bk;
+    }
+    if (const char* knob = getenv("PMENV_STREAM_POL")) {          // A/B knob: 0 | 1 (nt) | 2 (sc0 nt)
+        const int pol = atoi(knob);
+        if (pol >= 0 && pol <= 2) h->stream_pol = h->flat_pol = pol;
+    }
+    int fused_rows = 0;
+    h->streaming = plan_streaming(c, kInplaceOrder, h->stream_block, &h->unit_rows, &h->stream_vec) &&
+                   plan_streaming(c, kDoubleOrder, h->stream_block_db, &h->unit_rows_db, &h->stream_vec_db);
+    const bool fused_geom = h->streaming &&
+                            plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
+                            fused_rows == c.num_assets;
+    // flat double-buffered stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31):
+    // the default for obs_out. Measured on MI355X at the BASELINE shape (tools/gpu_ab_pol.sh,
+    // interleaved rounds, profiles/ab_r01/flat_*.log): 512-thread workgroups with nt loads
+    // and stores 665 us per step against 685 us for whole-env units; 256 threads and the
+    // sc0 nt policy within 1 %; the default cache policy 2 % slower.
+    h->flat = false;
+    h->flat_block = 512;
+    {
+        const int64_t per = (int64_t)c.num_assets * c.window * c.features;
+        const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
+                             (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
+        h->flat = flat_ok;
+        if (getenv("PMENV_STREAM_POL") == nullptr) h->flat_pol = 1;
+        if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;   // A/B knob
+        if (const char* knob = getenv("PMENV_FLAT_BLOCK")) {
+            const int bk = atoi(knob);
+            if (bk == 128 || bk == 256 || bk == 512) h->flat_block = bk;
+        }
+    }
     if (const char* knob = getenv("PMENV_ADVANCE"))   // A/B knob: force the single-launch LDS kernel
         if (!strcmp(knob, "lds")) h->streaming = false;
     if (const char* knob = getenv("PMENV_ABLATE")) h->ablate = atoi(knob);
@@ -345,7 +418,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         // on MI355X at N = 30, W = 50 (tools/gpu_ab_envs.sh) it wins at B = 1024
         // (18.5 vs 20.2 us in place) and loses from B = 4096 up (57.9 vs 52.9 us;
         // 764 vs 712 us at B = 65536).
-        const bool fusable = h->units_per_env_db == 1 && c.num_assets <= 64 && !h->ablate;
+        const bool fusable = fused_geom && c.num_assets <= 64 && !h->ablate;
         if (fusable && c.num_envs <= 1024) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
         if (const char* knob = getenv("PMENV_FUSED")) {    // A/B knob: 0 | db | all
             if (!strcmp(knob, "0") || !fusable) h->fused = 0;
@@ -523,6 +596,7 @@ const char* pmenv_step_path(const pmenv* h) {
     if (!h->streaming) return "step_advance_lds_kernel";
     if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
     if (h->fused) return "advance_rows_kernel<fused> (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
+    if (h->flat) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
     return "scalar_step_kernel+advance_rows_kernel";
 }
 

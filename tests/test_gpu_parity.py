@@ -163,6 +163,69 @@ def test_gpu_double_buffered_advance(N, W, F):
     _run_both(kw, B=9, N=N, W=W, T=W + 7, kind="mixed", F=F, seed=N, double_buffer=True)
 
 
+@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+@pytest.mark.parametrize("kind", ["simplex", "mixed"])
+def test_gpu_flat_obs_out_vs_oracle_modes(monkeypatch, kw, kind):
+    """The double-buffered flat stream (advance_flat_kernel, the default obs_out path
+    above B = 1024; forced here at small B by turning the one-launch step off) against
+    the oracle in every reward / ring / norm / commission mode, through the ring wrap."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    from pmenv import TradingEnv
+    assert "advance_flat_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
+    _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flat{kw}{kind}".encode()),
+              double_buffer=True)
+
+
+@pytest.mark.parametrize("N,W,B", [
+    (30, 50, 37),     # env = 1875 chunks: waves straddle envs and rows
+    (5, 4, 13),       # rows of 20 floats: several rows per wave, chunks straddle rows
+    (4, 2, 7),        # W = 2 (the smallest flat window): every other day is a last day
+    (1, 4, 9),        # one asset, envs of 5 chunks
+    (64, 16, 3),      # grid tail: chunk count not a multiple of 64
+    (129, 50, 2),     # long envs
+    (12, 10, 1),      # single env
+])
+@pytest.mark.parametrize("knobs", ["", "PMENV_STREAM_POL=0", "PMENV_STREAM_POL=2+PMENV_FLAT_BLOCK=128",
+                                   "PMENV_FLAT_BLOCK=256"])
+def test_gpu_flat_obs_out_shapes(monkeypatch, N, W, B, knobs):
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    for kv in filter(None, knobs.split("+")):
+        monkeypatch.setenv(*kv.split("="))
+    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 7 + W, double_buffer=True)
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + W, double_buffer=True)
+
+
+def test_gpu_flat_resident_series_obs_out(monkeypatch):
+    """Day-indexed bars (resident series) through the flat stream == the bar batch,
+    bit for bit; an out-of-range day reads NaN market channels, counted, not read."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    from pmenv import TradingEnv, MarketSeries
+    rng = np.random.default_rng(5)
+    T, N, W, B, S = 200, 30, 20, 41, 30
+    closes = 100 * np.exp(np.cumsum(0.01 * rng.standard_normal((T, N)), axis=0))
+    bars = np.stack([closes * np.exp(0.002 * rng.standard_normal((T, N))) for _ in range(3)] + [closes], -1)
+    m = MarketSeries(bars.astype(np.float32), device=DEV)
+    start = m.random_starts(B, W, S + 1, generator=torch.Generator().manual_seed(3))
+    obs_a = m.initial_window(start, W)
+    obs_b = obs_a.clone()
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    act = torch.softmax(torch.randn(S, B, N, device=DEV), -1)
+    for t in range(S):
+        day = start + W + t
+        ra, obs_a = ea.step(act[t], obs_a, series=m, day=day, out=torch.empty_like(obs_a))
+        rb, obs_b = eb.step(act[t], obs_b, bar=m.bars[day.long()].contiguous(), out=torch.empty_like(obs_b))
+        assert torch.equal(ra, rb)
+    assert torch.equal(obs_a, obs_b) and torch.equal(ea.value, eb.value)
+    bad = start + W + S
+    bad[7] = -3
+    _, nxt = ea.step(act[0], obs_a, series=m, day=bad, out=torch.empty_like(obs_a))
+    assert ea.nonfinite_count() == 1
+    assert bool(torch.isnan(nxt[7, :, -1, :4]).all()) and not bool(torch.isnan(nxt[6]).any())
+
+
 @pytest.mark.parametrize("fused", ["0", "db", "all"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES[:1] + MODES[4:8], ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
@@ -247,8 +310,14 @@ def test_gpu_full_size_properties():
     env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV)
     env.reset(obs)
     logv = torch.full((B,), float(np.log(25000.0)), dtype=torch.float64, device=DEV)
+    spare = torch.empty_like(obs)
     for t in range(T):
-        r, _ = env.step(act[t], obs, bar=ser[W + t])
+        # even steps in place, odd steps double-buffered (the flat stream)
+        if t % 2:
+            r, nxt = env.step(act[t], obs, bar=ser[W + t], out=spare)
+            obs, spare = nxt, obs
+        else:
+            r, _ = env.step(act[t], obs, bar=ser[W + t])
         y = (ser[W + t, ..., 3] / ser[W + t - 1, ..., 3]).double()
         ref = torch.log((act[t].double() * y).sum(-1))
         err = (r.double() - ref).abs()
