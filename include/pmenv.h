@@ -221,6 +221,14 @@ int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N
 int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones,
               float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam,
               hipStream_t stream);
+/* The same pass with caller-owned device scratch of pmenv_gae_workspace(T, B) bytes
+ * (0 when the shape does not use it): rollouts with few envs (B < 16384) and long
+ * horizons also split the horizon across workgroups (two launches, the chunks'
+ * affine maps kept in `work`). work == NULL or work_bytes too small: as pmenv_gae. */
+size_t pmenv_gae_workspace(int32_t T, int32_t B);
+int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones,
+                 float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam,
+                 double* work, size_t work_bytes, hipStream_t stream);
 
 /* Per-rank advantage moments {count, sum, sum of squares} in f64 into out[3]
  * (the only cross-GPU exchange: a 24-byte all-reduce over xGMI). `work` is

@@ -61,6 +61,10 @@ struct StepParams {
     double* sa;
     double* sb;
     unsigned long long* nonfinite;
+    // in-place flat advance: the scalar step kernel copies every flat workgroup's
+    // first two chunks here (advance_flat_inplace_kernel's halo); null: no copy
+    float* halo;
+    uint32_t halo_wgs, halo_block, halo_qtot;
     FastDiv div_wf, div_f, div_w, div_units;
 };
 
@@ -142,6 +146,22 @@ __device__ __forceinline__ double wave_min(double v) {
     v = fmin(v, dpp_shift<kRowShr4>(v, INFINITY));
     v = fmin(v, dpp_shift<kRowShr8>(v, INFINITY));
     return fmin(fmin(lane_value(v, 15), lane_value(v, 31)), fmin(lane_value(v, 47), lane_value(v, 63)));
+}
+
+// quad (4-lane group) reductions by DPP quad_perm: xor 1 then xor 2. Every lane of
+// the quad ends with bitwise the same value ((a0+a1)+(a2+a3) in each, by commutativity).
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E;
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_shift<kQuadXor1>(v, 0.0);
+    return v + dpp_shift<kQuadXor2>(v, 0.0);
+}
+__device__ __forceinline__ double quad_max(double v) {
+    v = fmax(v, dpp_shift<kQuadXor1>(v, -INFINITY));
+    return fmax(v, dpp_shift<kQuadXor2>(v, -INFINITY));
+}
+__device__ __forceinline__ double quad_min(double v) {
+    v = fmin(v, dpp_shift<kQuadXor1>(v, INFINITY));
+    return fmin(v, dpp_shift<kQuadXor2>(v, INFINITY));
 }
 
 }  // namespace pmenv_dev

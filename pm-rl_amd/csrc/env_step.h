@@ -214,8 +214,11 @@ __device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scrat
 
 // ---------------------------------------------------------------- K1: scalar step
 // One wave per env, kScalarWaves envs per workgroup, no barriers.
+__device__ __forceinline__ void copy_halo(const StepParams& p);
+
 __global__ __launch_bounds__(64 * kScalarWaves) void scalar_step_kernel(StepParams p, int scratch_floats) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    copy_halo(p);
     const int wave = threadIdx.x >> 6;
     const int b = blockIdx.x * kScalarWaves + wave;
     if (b >= p.B) return;
@@ -457,6 +460,7 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
 // bytes in flight per wave for a latency-bound kernel
 template <int L, int P>
 __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
+    copy_halo(p);
     constexpr int EPW = 64 / L;                   // envs per wave and group
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
@@ -631,16 +635,79 @@ __device__ __forceinline__ float pick(bool c, float a, float b) {
     return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
 }
 
+// What chunk q of the flat stream needs besides its input chunks: its position in
+// its asset row, the row's bar (only lanes whose chunk touches the last day load it;
+// the others' offsets are out of range: no traffic), w' and the env's counter.
+struct FlatSide {
+    int kk;            // row position of the chunk's first float
+    bool bar_nan;      // resident series: a day outside the series -> NaN bar
+    f4 xb;
+    float xwp;
+    int32_t k;
+};
+
+__device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t q) {
+    constexpr int F = 5;
+    const int N = p.N, WF = p.W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;                        // chunks per env
+    FlatSide sd;
+    const uint32_t b = fdiv(q, p.div_units);                              // div_units: per4 here
+    const uint32_t j0 = 4u * (q - b * per4);
+    const uint32_t row = fdiv(j0, p.div_wf);
+    sd.kk = (int)(j0 - row * (uint32_t)WF);
+    const bool touch_last = sd.kk + 3 >= WF - F;
+    // branch-free: without a day index the day descriptor has no records (reads 0), so
+    // no control flow can hold the streaming loads behind the day's latency
+    const bool by_day = p.day != nullptr;
+    const int32_t d = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
+        make_rsrc(by_day ? (const void*)p.day : (const void*)p.obs, by_day ? (uint32_t)p.B * 4u : 0u), b * 4u, 0, 0);
+    sd.bar_nan = by_day && (d < 0 || d >= p.series_days);
+    const uint32_t bar_bytes = (uint32_t)(by_day ? p.series_days : p.B) * (uint32_t)N * 16u;
+    const uint32_t bar_row = by_day ? (uint32_t)d : b;
+    const uint32_t bar_off = touch_last && !sd.bar_nan ? (bar_row * (uint32_t)N + row) * 16u : 0xFFFFFFF0u;
+    sd.xb = buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
+    sd.xwp = p.w_new[(size_t)b * N + row];
+    sd.k = p.k[b] - 1;                                                    // scalar_step_kernel counted this step
+    return sd;
+}
+
+// the output chunk from the unshifted input un (chunk q) and the shifted source sh
+// (floats 4q+5 .. 4q+8), per element at row position pos = kk + e (pos >= WF: the
+// chunk has wrapped into the next row, whose positions 0..2 are never a last day or
+// a weight slot for W >= 2, so they take the shifted value):
+//   market:  last day ? bar[f] : shifted
+//   weight:  shift mode: last day ? w' : shifted;  storage mode: pos == slot ? w' : own
+__device__ __forceinline__ f4 flat_compose(const StepParams& p, const FlatSide& sd, const float (&un)[4],
+                                           const float (&sh)[4]) {
+    constexpr int F = 5;
+    const int W = p.W, WF = W * F;
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && sd.k >= W - 1);
+    const int slot_w = (int)(((uint32_t)(1 + sd.k) - fdiv((uint32_t)(1 + sd.k), p.div_w) * (uint32_t)W) * F + (F - 1));
+    int f = sd.kk - (int)fdiv((uint32_t)sd.kk, p.div_f) * F;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int pos = sd.kk + e;
+        const bool in_row = pos < WF;
+        const bool lastday = in_row && pos >= WF - F;
+        const bool is_w = in_row && f == F - 1;
+        const float bsel = pick(sd.bar_nan, __int_as_float(0x7fc00000),
+                                pick(f == 0, sd.xb.x, pick(f == 1, sd.xb.y, pick(f == 2, sd.xb.z, sd.xb.w))));
+        const bool w_here = shift_w ? lastday : pos == slot_w;
+        const float wv = pick(w_here, sd.xwp, pick(shift_w, sh[e], un[e]));
+        v[e] = pick(is_w, wv, pick(lastday, bsel, sh[e]));
+        f = f == F - 1 ? 0 : f + 1;
+    }
+    return f4{v[0], v[1], v[2], v[3]};
+}
+
 template <int BLOCK, int POL>
 __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint32_t qtot) {
-    constexpr int F = 5;
     constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
     const int lane = threadIdx.x & 63;
     // wave-uniform by construction; readfirstlane lets the descriptors live in SGPRs
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(blockIdx.x * BLOCK + (threadIdx.x & ~63u));
     if (wbase >= qtot) return;
-    const int N = p.N, W = p.W, WF = W * F;
-    const uint32_t per4 = (uint32_t)(N * WF) >> 2;                        // chunks per env
     const uint32_t nwave = min(64u, qtot - wbase);
     const auto rs_src = make_rsrc(p.obs + (size_t)wbase * 4, nwave * 16u);
     const f4 own = buf_load4<kAux>(rs_src, (uint32_t)lane * 16u);
@@ -652,29 +719,8 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint3
     const f4 ext = buf_load4<0>(rs_ext, lane >= 62 ? (uint32_t)(lane - 62) * 16u : 0xFFFFFFF0u);
     // lanes past the tensor's end (last wave) index as its last chunk: loads stay in
     // bounds, their stores are dropped by the range check
-    const uint32_t q = min(wbase + (uint32_t)lane, qtot - 1u);
-    const uint32_t b = fdiv(q, p.div_units);                              // div_units: per4 here
-    const uint32_t j0 = 4u * (q - b * per4);
-    const uint32_t row = fdiv(j0, p.div_wf);
-    const int kk = (int)(j0 - row * (uint32_t)WF);
-    const bool touch_last = kk + 3 >= WF - F;
-    // the row's bar — only lanes whose chunk touches the last day; the others' offsets
-    // are out of range (no traffic) — through one descriptor over the whole bar
-    // batch, or over the resident series (day mode, out-of-range days read 0)
-    uint32_t bar_off = 0xFFFFFFF0u, bar_bytes;
-    bool bar_nan = false;                                                 // a day outside the series: NaN bar
-    if (p.day) {
-        const int32_t d = p.day[b];
-        bar_bytes = (uint32_t)p.series_days * (uint32_t)N * 16u;
-        bar_nan = d < 0 || d >= p.series_days;
-        if (touch_last && !bar_nan) bar_off = ((uint32_t)d * (uint32_t)N + row) * 16u;
-    } else {
-        bar_bytes = (uint32_t)p.B * (uint32_t)N * 16u;
-        if (touch_last) bar_off = (b * (uint32_t)N + row) * 16u;
-    }
-    const f4 xb = buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
-    const float xwp = p.w_new[(size_t)b * N + row];
-    const int32_t k = p.k[b] - 1;                                         // scalar_step_kernel counted this step
+    __builtin_amdgcn_sched_barrier(0);
+    const FlatSide sd = flat_side_load(p, min(wbase + (uint32_t)lane, qtot - 1u));
     // every load is in flight before the first cross-lane move waits on one
     __builtin_amdgcn_sched_barrier(0);
     // neighbours' chunks
@@ -694,25 +740,53 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint3
     n2x = pick(lane == 63, x63, pick(lane == 62, x62, n2x));
     const float sh[4] = {n1y, n1z, n1w, n2x};
     const float un[4] = {own.x, own.y, own.z, own.w};
-    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
-    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
-    int f = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int pos = kk + e;
-        const bool in_row = pos < WF;
-        const bool lastday = in_row && pos >= WF - F;
-        const bool is_w = in_row && f == F - 1;
-        const float bsel = pick(bar_nan, __int_as_float(0x7fc00000),
-                                pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w))));
-        const bool w_here = shift_w ? lastday : pos == slot_w;
-        const float wv = pick(w_here, xwp, pick(shift_w, sh[e], un[e]));
-        v[e] = pick(is_w, wv, pick(lastday, bsel, sh[e]));
-        f = f == F - 1 ? 0 : f + 1;
-    }
     const auto rs_dst = make_rsrc(p.obs_out + (size_t)wbase * 4, nwave * 16u);
-    buf_store4<kAux>(rs_dst, (uint32_t)lane * 16u, f4{v[0], v[1], v[2], v[3]});
+    buf_store4<kAux>(rs_dst, (uint32_t)lane * 16u, flat_compose(p, sd, un, sh));
+}
+
+// ---------------------------------------------------------------- K2, in place: flat stream + halo
+// The same flat stream advancing the window IN PLACE. A workgroup owns chunks
+// [c0, c0 + BLOCK): every lane loads its chunk into LDS, one barrier (every load of
+// the workgroup lands before any of its stores), then each lane composes its chunk
+// from LDS neighbours. The two chunks past the workgroup's end belong to the next
+// workgroup, which may already have advanced them: they come from `halo`, a copy of
+// every workgroup's first two chunks taken by the scalar step kernel of the same step
+// (copy_halo below), before any advance store.
+template <int BLOCK, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams p, uint32_t qtot) {
+    constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
+    __shared__ f4 sh4[BLOCK + 2];
+    const int tid = threadIdx.x;
+    const uint32_t c0 = blockIdx.x * BLOCK;
+    const uint32_t nblk = min((uint32_t)BLOCK, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    const f4 own = buf_load4<kAux>(rs, (uint32_t)tid * 16u);
+    // halo of this workgroup = first two chunks of the next one (none for the last)
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? 2u : 0u;
+    const f4 hal = buf_load4<0>(make_rsrc(p.halo + (size_t)blockIdx.x * 8, nh * 16u),
+                                tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    const FlatSide sd = flat_side_load(p, min(c0 + (uint32_t)tid, qtot - 1u));
+    sh4[tid] = own;
+    if (tid < 2) sh4[BLOCK + tid] = hal;
+    __syncthreads();
+    const f4 n1 = sh4[tid + 1], n2 = sh4[tid + 2];
+    const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+    const float un[4] = {own.x, own.y, own.z, own.w};
+    buf_store4<kAux>(rs, (uint32_t)tid * 16u, flat_compose(p, sd, un, sh));
+}
+
+// Taken by the scalar step kernels before the in-place flat advance of the same step:
+// halo[i] = chunks (i+1)*B_flat and (i+1)*B_flat + 1 of the window (0 past its end).
+__device__ __forceinline__ void copy_halo(const StepParams& p) {
+    if (!p.halo) return;
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    const f4* src = reinterpret_cast<const f4*>(p.obs);
+    f4* dst = reinterpret_cast<f4*>(p.halo);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.halo_wgs; i += nthr) {
+        const uint32_t q = (i + 1) * p.halo_block;
+        dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
+        dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
+    }
 }
 
 // ---------------------------------------------------------------- single-launch fallback

@@ -49,6 +49,10 @@ struct pmenv {
     int fused_vec;        // float4 per thread of the fused one-launch step (512 threads, whole env)
     bool flat;            // double-buffered advance as the flat 16-B stream (advance_flat_kernel)
     int flat_block, flat_pol;
+    bool flat_inplace;    // in-place advance as the flat stream + halo (advance_flat_inplace_kernel)
+    int flat_ip_block;
+    float* halo;          // [halo_wgs][2] float4: first two chunks of every in-place flat workgroup
+    uint32_t halo_wgs, flat_qtot;
     int scalar_scratch_floats;
     int k1_groups;        // env groups per wave in scalar_step_reg_kernel
     int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
@@ -184,6 +188,25 @@ void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
     else launch_flat_b<256>(h->flat_pol, p, grid, qtot, stream);
 }
 
+template <int BLOCK>
+void launch_flat_ip_b(int pol, const StepParams& p, unsigned grid, uint32_t qtot, hipStream_t stream) {
+    if (pol == 1) advance_flat_inplace_kernel<BLOCK, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else if (pol == 2) advance_flat_inplace_kernel<BLOCK, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else advance_flat_inplace_kernel<BLOCK, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
+}
+
+void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
+    const pmenv_cfg& c = h->cfg;
+    const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
+    p.div_units = make_fastdiv(per4);
+    p.halo = h->halo;
+    const int bk = h->flat_ip_block;
+    const unsigned grid = (unsigned)((h->flat_qtot + bk - 1) / bk);
+    if (bk == 256) launch_flat_ip_b<256>(h->flat_pol, p, grid, h->flat_qtot, stream);
+    else if (bk == 1024) launch_flat_ip_b<1024>(h->flat_pol, p, grid, h->flat_qtot, stream);
+    else launch_flat_ip_b<512>(h->flat_pol, p, grid, h->flat_qtot, stream);
+}
+
 template <int POL>
 void launch_advance_p(int block, int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
     if (block == 128) launch_advance_b<128, 0, POL>(vec, p, grid, stream);
@@ -231,6 +254,10 @@ void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
     const bool db = p.obs_out != p.obs;
     if (db && h->flat && !h->ablate) {
         launch_flat(h, p, stream);
+        return;
+    }
+    if (!db && h->flat_inplace && !h->ablate) {
+        launch_flat_inplace(h, p, stream);
         return;
     }
     p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
@@ -325,6 +352,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         // no handle reaches the caller: pmenv_last_error(NULL) reports this one
         snprintf(g_create_err, sizeof(g_create_err), "%s", h->err);
         if (h->state && h->owns_state) (void)hipFree(h->state);
+        if (h->halo) (void)hipFree(h->halo);
         free(h);
         return code;
     };
@@ -383,8 +411,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     const bool fused_geom = h->streaming &&
                             plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
                             fused_rows == c.num_assets;
-    // flat double-buffered stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31):
-    // the default for obs_out. Measured on MI355X at the BASELINE shape (tools/gpu_ab_pol.sh,
+    // flat stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31): the default
+    // for obs_out and, with the halo, in place. Measured on MI355X at the BASELINE shape (tools/gpu_ab_pol.sh,
     // interleaved rounds, profiles/ab_r01/flat_*.log): 512-thread workgroups with nt loads
     // and stores 665 us per step against 685 us for whole-env units; 256 threads and the
     // sc0 nt policy within 1 %; the default cache policy 2 % slower.
@@ -395,8 +423,18 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
                              (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
         h->flat = flat_ok;
+        // in place: 711 us per step against 802 us for the whole-row units (same A/B);
+        // 256 / 1024-thread workgroups 8-9 % slower, the default cache policy 5 %
+        h->flat_inplace = flat_ok;
+        h->flat_ip_block = 512;
+        h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         if (getenv("PMENV_STREAM_POL") == nullptr) h->flat_pol = 1;
         if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;   // A/B knob
+        if (const char* knob = getenv("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
+        if (const char* knob = getenv("PMENV_FLAT_IP_BLOCK")) {
+            const int bk = atoi(knob);
+            if (bk == 256 || bk == 512 || bk == 1024) h->flat_ip_block = bk;
+        }
         if (const char* knob = getenv("PMENV_FLAT_BLOCK")) {
             const int bk = atoi(knob);
             if (bk == 128 || bk == 256 || bk == 512) h->flat_block = bk;
@@ -459,6 +497,16 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
         h->owns_state = true;
     }
+    if (h->flat_inplace) {
+        const uint32_t wgs = (h->flat_qtot + h->flat_ip_block - 1) / h->flat_ip_block;
+        h->halo_wgs = wgs > 0 ? wgs - 1 : 0;
+        hipError_t ae = hipMalloc(&h->halo, (size_t)(h->halo_wgs + 1) * 32);
+        if (ae != hipSuccess) {
+            set_err(h, "hipMalloc(halo) failed: %s", hipGetErrorString(ae));
+            h->halo = nullptr;
+            return fail(PMENV_ERR_HIP);
+        }
+    }
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
     h->sa = (double*)(base + off[1]);
@@ -497,6 +545,7 @@ int pmenv_destroy(pmenv* h) {
     if (!h) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
     if (h->state && h->owns_state) (void)hipFree(h->state);
+    if (h->halo) (void)hipFree(h->halo);
     free(h);
     return PMENV_OK;
 }
@@ -554,6 +603,12 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
             return check_launch(h, "advance_rows_kernel<fused>");
         }
         if (ph & PMENV_PHASE_SCALAR) {
+            if (p.obs_out == p.obs && h->flat_inplace && !h->ablate) {   // the in-place advance's halo
+                p.halo = h->halo;
+                p.halo_wgs = h->halo_wgs;
+                p.halo_block = (uint32_t)h->flat_ip_block;
+                p.halo_qtot = h->flat_qtot;
+            }
             const int N = h->cfg.num_assets;
             if (N <= 64) {
                 launch_scalar_reg(h, p, stream);
@@ -596,6 +651,7 @@ const char* pmenv_step_path(const pmenv* h) {
     if (!h->streaming) return "step_advance_lds_kernel";
     if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
     if (h->fused) return "advance_rows_kernel<fused> (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
+    if (h->flat && h->flat_inplace) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_flat_inplace_kernel (in place)";
     if (h->flat) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
     return "scalar_step_kernel+advance_rows_kernel";
 }
@@ -686,6 +742,48 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
+// Horizon split of the tiled GAE scan (gae_chunk_kernel): used when the B / 64 env
+// blocks leave CUs idle; chunks sized so blocks x chunks ~ 1024 workgroups, each
+// chunk a whole number of 128-day segments (NW = 8, U = 16) and at least 2 of them.
+namespace {
+constexpr int kGaeSeg = 8 * 16;
+int gae_chunks(int32_t T, int32_t B, int* Lc) {
+    const int blocks = (B + 63) / 64;
+    if (B >= 16384 || T < 4 * kGaeSeg) return 0;
+    if ((size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
+    int want = (1024 + blocks - 1) / blocks;                    // chunks for ~1024 workgroups
+    int lc = (T + want - 1) / want;
+    lc = (lc + kGaeSeg - 1) / kGaeSeg * kGaeSeg;
+    lc = lc < 2 * kGaeSeg ? 2 * kGaeSeg : lc;
+    const int n = (T + lc - 1) / lc;
+    if (n < 2) return 0;
+    *Lc = lc;
+    return n;
+}
+}  // namespace
+
+size_t pmenv_gae_workspace(int32_t T, int32_t B) {
+    int lc = 0;
+    const int n = (T < 1 || B < 1) ? 0 : gae_chunks(T, B, &lc);
+    return n ? (size_t)2 * n * B * sizeof(double) : 0;
+}
+
+int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
+                 int32_t B, float gamma, float lam, double* work, size_t work_bytes, hipStream_t stream) {
+    if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
+    int lc = 0;
+    const int n = gae_chunks(T, B, &lc);
+    const char* knob = getenv("PMENV_GAE");        // an explicit kernel choice wins (A/B)
+    if (!n || knob || !work || work_bytes < (size_t)2 * n * B * sizeof(double))
+        return pmenv_gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream);
+    const dim3 grid((unsigned)((B + 63) / 64), (unsigned)n);
+    gae_chunk_kernel<8, 16, true><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
+                                                            work);
+    gae_chunk_kernel<8, 16, false><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
+                                                             work);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
 size_t pmenv_moments_workspace(void) { return (size_t)kMomBlocks * 2 * sizeof(double); }
 
 int pmenv_moments(const float* x, int64_t n, double* out, double* work, hipStream_t stream) {
@@ -721,7 +819,12 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
 int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B, int32_t N,
                   double risk_free_rate, double periods, double* out, hipStream_t stream) {
     if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;
-    metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
+    // measured on MI355X (tools/bench_rows.py): the horizon split over four waves per
+    // 64 envs against the thread-per-env walk — see profiles/rows_r01*/
+    if (getenv("PMENV_METRICS_WALK"))   // A/B knob: the thread-per-env walk
+        metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
+    else
+        metrics_seg_kernel<<<(B + 63) / 64, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
     const int tpe = N <= 256 ? N : 256, eb = 256 / tpe;
     metrics_turnover_kernel<<<(unsigned)((B + eb - 1) / eb), 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
@@ -737,10 +840,27 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         reward_kind != PMENV_REWARD_SHARPE)
         return PMENV_ERR_ARG;
     if (norm < PMENV_BNORM_GLOBAL_OR || norm > PMENV_BNORM_NONE) return PMENV_ERR_ARG;
-    batch_reward_rows_kernel<<<(unsigned)batch_reward_blocks(B), kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
-                                                                                          reward_kind, work);
-    batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out);
-    batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+    int nparts;
+    if (N <= kQuadMaxN) {         // a quad of lanes per row
+        nparts = (B + kQuadRows - 1) / kQuadRows;
+        if (N <= 32)
+            batch_reward_rows_quad_kernel<8><<<(unsigned)nparts, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
+                                                                                           reward_kind, work);
+        else
+            batch_reward_rows_quad_kernel<16><<<(unsigned)nparts, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
+                                                                                            reward_kind, work);
+    } else {                      // wave per row, registers up to N = 512
+        nparts = (int)batch_reward_blocks(B);
+        const unsigned g = (unsigned)nparts;
+        if (N <= 128) batch_reward_rows_kernel<2><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
+        else if (N <= 256) batch_reward_rows_kernel<4><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
+        else if (N <= 512) batch_reward_rows_kernel<8><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
+        else batch_reward_rows_kernel<0><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
+    }
+    batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out, nparts);
+    // the chosen per-row return (and the row flags of the N > 64 backward)
+    if (ret_out || N > kQuadMaxN)
+        batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -748,8 +868,25 @@ int pmenv_batch_reward_backward(const float* a, const float* v_prev, const float
                                 int32_t reward_kind, double scale, const double* work, const float* grad_out,
                                 float* grad_a, hipStream_t stream) {
     if (!a || !v_prev || !p || !work || !grad_out || !grad_a || B < 1 || N < 1) return PMENV_ERR_ARG;
-    batch_reward_grad_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
-                                                              grad_out, grad_a);
+    const unsigned qgrid = (unsigned)((B + kQuadRows - 1) / kQuadRows);
+    if (N <= 32)
+        batch_reward_grad_quad_kernel<8><<<qgrid, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale,
+                                                                           work, grad_out, grad_a);
+    else if (N <= kQuadMaxN)
+        batch_reward_grad_quad_kernel<16><<<qgrid, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale,
+                                                                            work, grad_out, grad_a);
+    else if (N <= 128)
+        batch_reward_grad_kernel<2><<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
+                                                                     grad_out, grad_a);
+    else if (N <= 256)
+        batch_reward_grad_kernel<4><<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
+                                                                     grad_out, grad_a);
+    else if (N <= 512)
+        batch_reward_grad_kernel<8><<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
+                                                                     grad_out, grad_a);
+    else
+        batch_reward_grad_kernel<0><<<(B + 3) / 4, 256, 0, stream>>>(a, v_prev, p, B, N, reward_kind, scale, work,
+                                                                     grad_out, grad_a);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

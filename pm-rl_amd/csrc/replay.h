@@ -87,6 +87,83 @@ __global__ void metrics_kernel(const double* returns, const double* values, int 
 }
 
 
+// The same per-env metrics with the horizon split over the four waves of a
+// workgroup (lane = env: every load is a coalesced 512-B row; four times the waves
+// in flight of the thread-per-env walk). Wave w walks days [w*T/4, (w+1)*T/4):
+//   sharpe / sortino: shifted sums S1 = sum(x - K), S2 = sum((x - K)^2) with K the
+//   env's first excess return (no division in the loop), and sum(min(x, 0)^2);
+//   max drawdown: each wave's segment maximum goes through LDS, then the wave
+//   re-walks its segment (an L2 re-read) with the running peak seeded by the
+//   maximum of every earlier segment.
+// Wave 0 adds the four segments' sums in wave order: deterministic.
+__global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
+                                                          double rf, double periods, double* out) {
+    __shared__ double sh[5][4][64];              // S1, S2, down, segment max (of values), mdd
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = blockIdx.x * 64 + lane;
+    const bool ok = b < B;
+    const int bb = ok ? b : B - 1;
+    const double rfp = rf != 0.0 ? pow(1.0 + rf, 1.0 / periods) - 1.0 : 0.0;
+    const double K = returns[bb] - rfp;
+    // returns: T rows, values: T + 1 rows; split both the same way
+    const int r0 = (int)((int64_t)T * w / 4), r1 = (int)((int64_t)T * (w + 1) / 4);
+    double s1 = 0.0, s2 = 0.0, dn = 0.0;
+    int t = r0;
+    for (; t + 4 <= r1; t += 4) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = returns[(size_t)(t + u) * B + bb] - rfp;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double d = x[u] - K;
+            s1 += d;
+            s2 += d * d;
+            dn += x[u] < 0.0 ? x[u] * x[u] : 0.0;
+        }
+    }
+    for (; t < r1; ++t) {
+        const double x = returns[(size_t)t * B + bb] - rfp;
+        const double d = x - K;
+        s1 += d;
+        s2 += d * d;
+        dn += x < 0.0 ? x * x : 0.0;
+    }
+    const int v0 = (int)((int64_t)(T + 1) * w / 4), v1 = (int)((int64_t)(T + 1) * (w + 1) / 4);
+    double vmax = -INFINITY;
+    for (t = v0; t < v1; ++t) vmax = fmax(vmax, values[(size_t)t * B + bb]);
+    sh[0][w][lane] = s1;
+    sh[1][w][lane] = s2;
+    sh[2][w][lane] = dn;
+    sh[3][w][lane] = vmax;
+    __syncthreads();
+    // qs.stats.max_drawdown: min_t (V_t / max_{s<=t} V_s - 1), the peak seeded by
+    // every earlier segment
+    double peak = -INFINITY;
+    for (int j = 0; j < w; ++j) peak = fmax(peak, sh[3][j][lane]);
+    double mdd = 0.0;
+    for (t = v0; t < v1; ++t) {
+        const double v = values[(size_t)t * B + bb];
+        peak = fmax(peak, v);
+        mdd = fmin(mdd, v / peak - 1.0);
+    }
+    sh[4][w][lane] = mdd;
+    __syncthreads();
+    if (w != 0 || !ok) return;
+    double S1 = 0.0, S2 = 0.0, DN = 0.0, MDD = 0.0;
+    for (int j = 0; j < 4; ++j) {
+        S1 += sh[0][j][lane];
+        S2 += sh[1][j][lane];
+        DN += sh[2][j][lane];
+        MDD = fmin(MDD, sh[4][j][lane]);
+    }
+    const double mean = K + S1 / T;
+    const double sd = T > 1 ? sqrt(fmax(S2 - S1 * S1 / T, 0.0) / (T - 1)) : NAN;
+    out[(size_t)b * 5 + 0] = mean / sd * sqrt(periods);
+    out[(size_t)b * 5 + 1] = mean / sqrt(DN / T) * sqrt(periods);
+    out[(size_t)b * 5 + 2] = MDD;
+    out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
+}
+
 // util/eval.py:32-37 average turnover, element-parallel: a workgroup owns `eb` whole
 // envs (N <= 256: one thread per (env, asset), so each day's read is eb*N contiguous
 // floats) and every thread walks the days keeping the previous weight in a

@@ -17,8 +17,9 @@ namespace pmenv_dev {
 
 // work layout (f64): [0,B) ret chosen, [B,2B) row sum, [2B,3B) row min, [3B,4B) ret raw,
 // [4B,5B) ret softmax, [5B,6B) row normalised flag, [6B..6B+8) globals:
-// +0 normalised (global), +1 mean, +2 std, +3 reward; then one partial record of
-// kPartStride doubles per block of kRowsPerBlock rows.
+// +0 normalised (global), +1 mean, +2 std, +3 reward, +4 norm mode; then the partial
+// records of the row blocks (kRowsPerBlock or kQuadRows rows each), field-major:
+// field i of block k at [6B+8 + i*nblocks + k].
 constexpr int kTrainBlock = 256;
 constexpr int kRowsPerBlock = 16;   // 4 waves x 4 rows
 constexpr int kPartStride = 16;     // sum a, min a, nan, then 3 x {n, mean, M2, sum f}
@@ -43,30 +44,67 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
     n = nn;
 }
 
-// one wave per row (4 rows per wave, 16 per block); N <= 64 lanes per pass, looping
-// for larger N. Wave 0 then folds the block's rows into one partial record:
-// sums / min for the normalisation decision and, for each candidate return vector
-// (raw, softmax, per-row choice), count, mean, M2 (two-pass inside the block) and
-// the sum of f(ret) (log for the log-return reward).
+// one wave per row (4 rows per wave, 16 per block). EPL > 0 (N <= 64*EPL): the wave
+// loads all four rows' elements into registers up front (lane l holds elements
+// l + 64k: coalesced 256-B rows, every load in flight before the first reduction) and
+// reads memory once; EPL = 0: any N, looping over the row in passes. Wave 0 then
+// folds the block's rows into one partial record: sums / min for the normalisation
+// decision and, for each candidate return vector (raw, softmax, per-row choice),
+// count, mean, M2 (two-pass inside the block) and the sum of f(ret) (log for the
+// log-return reward).
+template <int EPL>
 __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const float* a, const float* v_prev,
                                                                         const float* p, int B, int N, int kind,
                                                                         double* work) {
     __shared__ double sh[4][kRowsPerBlock];       // row sum, row min, raw, softmax
+    constexpr int RPW = kRowsPerBlock / 4;        // rows per wave
+    constexpr int E = EPL > 0 ? EPL : 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int j = 0; j < kRowsPerBlock / 4; ++j) {
-        const int rl = wave * (kRowsPerBlock / 4) + j;
+    float ra[RPW][E], rp[RPW][E];
+    if (EPL > 0) {
+        const uint32_t bytes = (uint32_t)B * (uint32_t)N * 4u;
+        const auto rsa = make_rsrc(a, bytes), rsp = make_rsrc(p, bytes);
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int b = blockIdx.x * kRowsPerBlock + wave * RPW + j;
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                const int n = lane + 64 * k;
+                // lanes past the row (or rows past B) read out of range: 0, no traffic
+                const uint32_t off = (n < N && b < B) ? ((uint32_t)b * (uint32_t)N + (uint32_t)n) * 4u : 0xFFFFFFF0u;
+                ra[j][k] = buf_load1(rsa, off);
+                rp[j][k] = buf_load1(rsp, off);
+            }
+        }
+    }
+    for (int j = 0; j < RPW; ++j) {
+        const int rl = wave * RPW + j;
         const int b = blockIdx.x * kRowsPerBlock + rl;
         if (b >= B) break;
         const double v = (double)v_prev[b];
         double s = 0.0, mn = INFINITY, mx = -INFINITY, raw = 0.0;
         int nan_seen = 0;
-        for (int n = lane; n < N; n += 64) {
-            const double x = (double)a[(size_t)b * N + n];
-            s += x;
-            mn = fmin(mn, x);
-            mx = fmax(mx, x);
-            nan_seen |= isnan(x);
-            raw += v * (x * (double)p[(size_t)b * N + n]);
+        if (EPL > 0) {
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                if (lane + 64 * k < N) {
+                    const double x = (double)ra[j][k];
+                    s += x;
+                    mn = fmin(mn, x);
+                    mx = fmax(mx, x);
+                    nan_seen |= isnan(x);
+                    raw += v * (x * (double)rp[j][k]);
+                }
+            }
+        } else {
+            for (int n = lane; n < N; n += 64) {
+                const double x = (double)a[(size_t)b * N + n];
+                s += x;
+                mn = fmin(mn, x);
+                mx = fmax(mx, x);
+                nan_seen |= isnan(x);
+                raw += v * (x * (double)p[(size_t)b * N + n]);
+            }
         }
         s = wave_sum(s);
         mn = wave_min(mn);
@@ -74,11 +112,24 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
         raw = wave_sum(raw);
         if (__any(nan_seen)) mn = NAN;
         double z = 0.0, sm = 0.0;
-        for (int n = lane; n < N; n += 64) z += exp((double)a[(size_t)b * N + n] - mx);
-        z = wave_sum(z);
-        for (int n = lane; n < N; n += 64) {
-            const double w = exp((double)a[(size_t)b * N + n] - mx) / z;     // torch.softmax(a, dim=1)
-            sm += v * (w * (double)p[(size_t)b * N + n]);
+        if (EPL > 0) {
+            double e[E];
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                e[k] = lane + 64 * k < N ? exp((double)ra[j][k] - mx) : 0.0;
+                z += e[k];
+            }
+            z = wave_sum(z);
+            const double rz = 1.0 / z;
+#pragma unroll
+            for (int k = 0; k < E; ++k) sm += v * ((e[k] * rz) * (double)rp[j][k]);   // torch.softmax(a, dim=1)
+        } else {
+            for (int n = lane; n < N; n += 64) z += exp((double)a[(size_t)b * N + n] - mx);
+            z = wave_sum(z);
+            for (int n = lane; n < N; n += 64) {
+                const double w = exp((double)a[(size_t)b * N + n] - mx) / z;     // torch.softmax(a, dim=1)
+                sm += v * (w * (double)p[(size_t)b * N + n]);
+            }
         }
         sm = wave_sum(sm);
         if (lane == 0) {
@@ -97,7 +148,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
     const int b = blockIdx.x * kRowsPerBlock + lane;
     const bool ok = lane < kRowsPerBlock && b < B;
     const double cnt = (double)min(kRowsPerBlock, B - (int)blockIdx.x * kRowsPerBlock);
-    double* part = work + (size_t)6 * B + 8 + (size_t)blockIdx.x * kPartStride;
+    double* part = work + (size_t)6 * B + 8 + blockIdx.x;
     const int li = ok ? lane : 0;
     const double rs = ok ? sh[0][li] : 0.0, rm = ok ? sh[1][li] : INFINITY;
     const double s_all = wave_sum(rs);
@@ -127,18 +178,219 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
         double val = rec[0];
 #pragma unroll
         for (int i = 1; i < kPartStride; ++i) val = lane == i ? rec[i] : val;
-        part[lane] = val;
+        part[(size_t)lane * gridDim.x] = val;                      // field-major: coalesced final fold
     }
 }
 
-// single workgroup over the block partials: the normalisation decision, the reward
+// ---------------------------------------------------------------- N <= 64: a quad per row
+// Four lanes per row (64 rows per 256-thread workgroup, B/64 workgroups: four waves
+// per SIMD at B = 65,536), lane g of a row holding elements [g*EPL, g*EPL + EPL) in
+// registers from dword-aligned 16-B loads of the contiguous row (range-checked: the
+// batch's last row never reads past the tensor). The row's sums, min, max and
+// softmax go through DPP quad reductions; each wave then folds its 16 rows and
+// thread 0 merges the four wave records in wave order (Chan): deterministic, one
+// partial per 64 rows for the final fold.
+constexpr int kQuadRows = 64;
+constexpr int kQuadMaxN = 64;
+
+template <int EPL>
+struct RowQuad {
+    float a[EPL], p[EPL];
+};
+
+template <int EPL>
+__device__ __forceinline__ RowQuad<EPL> load_row_quad(const float* a, const float* p, int B, int N, int b, int g) {
+    RowQuad<EPL> q;
+    const uint32_t bytes = (uint32_t)B * (uint32_t)N * 4u;
+    const auto ra = make_rsrc(a, bytes), rp = make_rsrc(p, bytes);
+    const uint32_t base = ((uint32_t)b * (uint32_t)N + (uint32_t)(g * EPL)) * 4u;
+#pragma unroll
+    for (int c = 0; c < EPL / 4; ++c) {
+        const f4 va = buf_load4(ra, base + 16u * c), vp = buf_load4(rp, base + 16u * c);
+        q.a[4 * c] = va.x; q.a[4 * c + 1] = va.y; q.a[4 * c + 2] = va.z; q.a[4 * c + 3] = va.w;
+        q.p[4 * c] = vp.x; q.p[4 * c + 1] = vp.y; q.p[4 * c + 2] = vp.z; q.p[4 * c + 3] = vp.w;
+    }
+    return q;
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_quad_kernel(const float* a, const float* v_prev,
+                                                                             const float* p, int B, int N, int kind,
+                                                                             double* work) {
+    __shared__ double rec_w[4][kPartStride];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid & 3;
+    const int r0 = blockIdx.x * kQuadRows;
+    const int nrows = min(kQuadRows, B - r0);
+    const bool ok = (tid >> 2) < nrows;
+    const int b = r0 + (ok ? tid >> 2 : 0);
+    const RowQuad<EPL> q = load_row_quad<EPL>(a, p, B, N, b, g);
+    const double v = (double)v_prev[b];
+    double s = 0.0, mn = INFINITY, mx = -INFINITY, raw = 0.0;
+    bool nan_seen = false;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+        if (g * EPL + i < N) {
+            const double x = (double)q.a[i];
+            s += x;
+            mn = fmin(mn, x);
+            mx = fmax(mx, x);
+            nan_seen |= isnan(x);
+            raw += v * (x * (double)q.p[i]);
+        }
+    }
+    s = quad_sum(s);
+    mn = quad_min(mn);
+    mx = quad_max(mx);
+    raw = quad_sum(raw);
+    if (quad_sum(nan_seen ? 1.0 : 0.0) > 0.0) mn = NAN;            // torch.min propagates NaN
+    double e[EPL];
+    double z = 0.0;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+        e[i] = g * EPL + i < N ? exp((double)q.a[i] - mx) : 0.0;
+        z += e[i];
+    }
+    z = quad_sum(z);
+    const double rz = 1.0 / z;
+    double sm = 0.0;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i)
+        if (g * EPL + i < N) sm += v * ((e[i] * rz) * (double)q.p[i]);   // torch.softmax(a, dim=1)
+    sm = quad_sum(sm);
+    const double x_raw = raw / v, x_sm = sm / v;
+    if (ok && g == 0) {
+        work[(size_t)B + b] = s;
+        work[2 * (size_t)B + b] = mn;
+        work[3 * (size_t)B + b] = x_raw;
+        work[4 * (size_t)B + b] = x_sm;
+    }
+    // this wave's record over its 16 rows (lane g == 0 of each quad contributes)
+    const bool own = ok && g == 0;
+    const double cnt = (double)max(0, min(16, nrows - 16 * wave));
+    double x[3];
+    x[kCandRaw] = own ? x_raw : 0.0;
+    x[kCandSoftmax] = own ? x_sm : 0.0;
+    x[kCandRow] = row_normalises(s, mn) ? x[kCandSoftmax] : x[kCandRaw];
+    double rec[kPartStride];
+    rec[0] = wave_sum(own ? s : 0.0);
+    rec[1] = wave_min(own && !isnan(mn) ? mn : INFINITY);
+    rec[2] = __any(own && isnan(mn)) ? 1.0 : 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double mean = cnt > 0.0 ? wave_sum(x[c]) / cnt : 0.0;
+        const double d = own ? x[c] - mean : 0.0;
+        rec[3 + 4 * c + 0] = cnt;
+        rec[3 + 4 * c + 1] = mean;
+        rec[3 + 4 * c + 2] = wave_sum(d * d);
+        rec[3 + 4 * c + 3] = wave_sum(own ? (kind == PMENV_REWARD_LOG_RETURN ? log(x[c]) : x[c]) : 0.0);
+    }
+    rec[15] = 0.0;
+    if (lane < kPartStride) {
+        double val = rec[0];
+#pragma unroll
+        for (int i = 1; i < kPartStride; ++i) val = lane == i ? rec[i] : val;
+        rec_w[wave][lane] = val;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    double acc[kPartStride];
+    for (int i = 0; i < kPartStride; ++i) acc[i] = rec_w[0][i];
+    for (int w = 1; w < 4; ++w) {
+        const double* r = rec_w[w];
+        acc[0] += r[0];
+        acc[1] = fmin(acc[1], r[1]);
+        acc[2] += r[2];
+        for (int c = 0; c < 3; ++c) {
+            chan_merge(acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], r[3 + 4 * c], r[4 + 4 * c], r[5 + 4 * c]);
+            acc[6 + 4 * c] += r[6 + 4 * c];
+        }
+    }
+    double* part = work + (size_t)6 * B + 8 + blockIdx.x;        // field-major: coalesced final fold
+    for (int i = 0; i < kPartStride; ++i) part[(size_t)i * gridDim.x] = acc[i];
+}
+
+// backward, N <= 64, a quad per row: dR/da through the (optional) softmax. The
+// per-row choice (softmax or raw) is taken here from the forward's workspace (its
+// norm mode at work[6B+4]), so the backward needs no select pass. Whole 16-B chunks
+// of the row are stored as such, the row's tail element by element.
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_grad_quad_kernel(const float* a, const float* v_prev,
+                                                                             const float* p, int B, int N, int kind,
+                                                                             double scale, const double* work,
+                                                                             const float* grad_out, float* grad_a) {
+    const int tid = threadIdx.x, g = tid & 3;
+    const int r0 = blockIdx.x * kQuadRows;
+    const int nrows = min(kQuadRows, B - r0);
+    const bool ok = (tid >> 2) < nrows;
+    const int b = r0 + (ok ? tid >> 2 : 0);
+    const RowQuad<EPL> q = load_row_quad<EPL>(a, p, B, N, b, g);
+    const int norm = (int)work[6 * (size_t)B + 4];                // the forward's mode
+    bool nb;
+    if (norm == PMENV_BNORM_GLOBAL_OR) nb = work[6 * (size_t)B] != 0.0;
+    else if (norm == PMENV_BNORM_ROW_OR) nb = row_normalises(work[(size_t)B + b], work[2 * (size_t)B + b]);
+    else nb = false;
+    const double r = nb ? work[4 * (size_t)B + b] : work[3 * (size_t)B + b];
+    double dr;
+    if (kind == PMENV_REWARD_LOG_RETURN) dr = scale / ((double)B * r);
+    else if (kind == PMENV_REWARD_RETURN) dr = scale / (double)B;
+    else {
+        const double m = work[6 * (size_t)B + 1], sd = work[6 * (size_t)B + 2];
+        dr = scale * (1.0 / ((double)B * sd) - m * (r - m) / ((double)(B - 1) * sd * sd * sd));
+    }
+    dr *= (double)*grad_out;
+    const double v = (double)v_prev[b];
+    float out[EPL];
+    // nb is uniform per quad (a row's lanes agree), so the quad reductions below see
+    // every lane of the quad on the same branch
+    if (!nb) {
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) out[i] = (float)(dr * (v * (double)q.p[i]) / v);
+    } else {
+        double mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < EPL; ++i)
+            if (g * EPL + i < N) mx = fmax(mx, (double)q.a[i]);
+        mx = quad_max(mx);
+        double e[EPL], z = 0.0;
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) {
+            e[i] = g * EPL + i < N ? exp((double)q.a[i] - mx) : 0.0;
+            z += e[i];
+        }
+        z = quad_sum(z);
+        const double rz = 1.0 / z;
+        double wg = 0.0;                                          // sum_m w_m g_m
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) wg += (e[i] * rz) * (dr * (v * (double)q.p[i]) / v);
+        wg = quad_sum(wg);
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) out[i] = (float)((e[i] * rz) * (dr * (v * (double)q.p[i]) / v - wg));
+    }
+    if (!ok) return;
+    const auto rg = make_rsrc(grad_a, (uint32_t)B * (uint32_t)N * 4u);
+    const int n0 = g * EPL;
+    const uint32_t base = ((uint32_t)b * (uint32_t)N + (uint32_t)n0) * 4u;
+#pragma unroll
+    for (int c = 0; c < EPL / 4; ++c) {
+        if (n0 + 4 * c + 4 <= N) {
+            buf_store4(rg, base + 16u * c, f4{out[4 * c], out[4 * c + 1], out[4 * c + 2], out[4 * c + 3]});
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (n0 + 4 * c + k < N) grad_a[(size_t)b * N + n0 + 4 * c + k] = out[4 * c + k];
+        }
+    }
+}
+
+// single workgroup over the `nparts` block partials: the normalisation decision, the reward
 // and the chosen candidate's mean / std. Thread t folds partials t, t + 256, ... in
 // order, then a fixed-shape LDS tree folds the 256 threads: deterministic.
 __global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, int kind, int norm, double scale,
-                                                                         double* work, float* reward_out) {
-    __shared__ double sh[kTrainBlock][kPartStride];
-    const int tid = threadIdx.x;
-    const size_t nblk = batch_reward_blocks(B);
+                                                                         double* work, float* reward_out,
+                                                                         int nparts) {
+    __shared__ double sh[4][kPartStride];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t nblk = (size_t)nparts;
     const double* parts = work + (size_t)6 * B + 8;
     double acc[kPartStride];
     acc[0] = 0.0; acc[1] = INFINITY; acc[2] = 0.0;
@@ -148,38 +400,59 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, 
         acc[0] += q[0];
         acc[1] = fmin(acc[1], q[1]);
         acc[2] += q[2];
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
             chan_merge(acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], q[3 + 4 * c], q[4 + 4 * c], q[5 + 4 * c]);
             acc[6 + 4 * c] += q[6 + 4 * c];
         }
     };
-    for (size_t k = tid; k < nblk; k += kTrainBlock) fold(parts + k * kPartStride);
-    for (int i = 0; i < kPartStride; ++i) sh[tid][i] = acc[i];
-    __syncthreads();
-    for (int o = kTrainBlock / 2; o > 0; o >>= 1) {
-        if (tid < o) {
-            for (int i = 0; i < kPartStride; ++i) acc[i] = sh[tid][i];
-            fold(sh[tid + o]);
-            for (int i = 0; i < kPartStride; ++i) sh[tid][i] = acc[i];
+    // thread t folds partials t, t + 256, ... in order; then a shift-down tree inside
+    // each wave (lane i takes lane i + o) and the four wave records in wave order
+    // partials are field-major (field i of block k at parts[i * nparts + k]): every
+    // load below is a coalesced row, and a thread's four partials are all in flight
+    // before the first fold
+    for (size_t k0 = tid; k0 < nblk; k0 += 4 * kTrainBlock) {
+        double q[4][kPartStride];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const size_t k = k0 + (size_t)j * kTrainBlock;
+#pragma unroll
+            for (int i = 0; i < kPartStride; ++i) q[j][i] = k < nblk ? parts[(size_t)i * nblk + k] : 0.0;
         }
-        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k0 + (size_t)j * kTrainBlock < nblk) fold(q[j]);
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        double q[kPartStride];
+#pragma unroll
+        for (int i = 0; i < kPartStride; ++i)
+            q[i] = __hiloint2double(__shfl_down(__double2hiint(acc[i]), o, 64), __shfl_down(__double2loint(acc[i]), o, 64));
+        if (lane < o) fold(q);
+    }
+    if (lane == 0)
+        for (int i = 0; i < kPartStride; ++i) sh[wave][i] = acc[i];
+    __syncthreads();
     if (tid != 0) return;
-    for (int i = 0; i < kPartStride; ++i) acc[i] = sh[0][i];
+    for (int w = 1; w < 4; ++w) fold(sh[w]);
     // pg.py:52 sums / mins the WHOLE [B, N, 1] tensor; torch.min propagates NaN
     const double mn_all = acc[2] > 0.0 ? NAN : acc[1];
     const bool glob = !(fabs(acc[0] - 1.0) <= 1e-6 + 1e-5) || mn_all < 0.0;
     const int c = norm == PMENV_BNORM_GLOBAL_OR ? (glob ? kCandSoftmax : kCandRaw)
                 : norm == PMENV_BNORM_ROW_OR ? kCandRow : kCandRaw;
-    const double mean = acc[4 + 4 * c];
-    const double sd = B > 1 ? sqrt(acc[5 + 4 * c] / (B - 1)) : NAN;     // torch.std: unbiased
+    // constant indices only (a runtime index into acc would put it in scratch memory)
+    const double mean = c == kCandRaw ? acc[4] : c == kCandSoftmax ? acc[8] : acc[12];
+    const double m2 = c == kCandRaw ? acc[5] : c == kCandSoftmax ? acc[9] : acc[13];
+    const double fsum = c == kCandRaw ? acc[6] : c == kCandSoftmax ? acc[10] : acc[14];
+    const double sd = B > 1 ? sqrt(m2 / (B - 1)) : NAN;                  // torch.std: unbiased
     double R;
     if (kind == PMENV_REWARD_SHARPE) R = mean / sd * scale;               // pg.py:80
-    else R = acc[6 + 4 * c] / B * scale;                                  // pg.py:76, :78
+    else R = fsum / B * scale;                                            // pg.py:76, :78
     work[6 * (size_t)B + 0] = glob ? 1.0 : 0.0;
     work[6 * (size_t)B + 1] = mean;
     work[6 * (size_t)B + 2] = sd;
     work[6 * (size_t)B + 3] = R;
+    work[6 * (size_t)B + 4] = (double)norm;
     *reward_out = (float)R;
 }
 
@@ -197,14 +470,30 @@ __global__ __launch_bounds__(256) void batch_reward_select_kernel(int B, int nor
     if (ret_out) ret_out[b] = (float)r;
 }
 
-// one wave per row: dR/da through the (optional) softmax
+// one wave per row: dR/da through the (optional) softmax. EPL > 0 (N <= 64*EPL):
+// the row is loaded once into registers (lane l: elements l + 64k) and every pass
+// runs from them; EPL = 0: any N, re-reading the row per pass.
+template <int EPL>
 __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, const float* v_prev, const float* p,
                                                                 int B, int N, int kind, double scale,
                                                                 const double* work, const float* grad_out,
                                                                 float* grad_a) {
+    constexpr int E = EPL > 0 ? EPL : 1;
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= B) return;
+    float ra[E], rp[E];
+    if (EPL > 0) {
+        const uint32_t bytes = (uint32_t)B * (uint32_t)N * 4u;
+        const auto rsa = make_rsrc(a, bytes), rsp = make_rsrc(p, bytes);
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            const int n = lane + 64 * k;
+            const uint32_t off = n < N ? ((uint32_t)b * (uint32_t)N + (uint32_t)n) * 4u : 0xFFFFFFF0u;
+            ra[k] = buf_load1(rsa, off);
+            rp[k] = buf_load1(rsp, off);
+        }
+    }
     const double go = (double)*grad_out;
     const double r = work[b];
     double dr;
@@ -217,6 +506,37 @@ __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, 
     dr *= go;
     const double v = (double)v_prev[b];
     const bool nb = work[5 * (size_t)B + b] != 0.0;
+    if (EPL > 0) {
+        float out[E];
+        if (!nb) {
+#pragma unroll
+            for (int k = 0; k < E; ++k) out[k] = (float)(dr * (v * (double)rp[k]) / v);
+        } else {
+            double mx = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < E; ++k)
+                if (lane + 64 * k < N) mx = fmax(mx, (double)ra[k]);
+            mx = wave_max(mx);
+            double e[E], z = 0.0;
+#pragma unroll
+            for (int k = 0; k < E; ++k) {
+                e[k] = lane + 64 * k < N ? exp((double)ra[k] - mx) : 0.0;
+                z += e[k];
+            }
+            z = wave_sum(z);
+            const double rz = 1.0 / z;
+            double wg = 0.0;                           // sum_m w_m g_m
+#pragma unroll
+            for (int k = 0; k < E; ++k) wg += (e[k] * rz) * (dr * (v * (double)rp[k]) / v);
+            wg = wave_sum(wg);
+#pragma unroll
+            for (int k = 0; k < E; ++k) out[k] = (float)((e[k] * rz) * (dr * (v * (double)rp[k]) / v - wg));
+        }
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+            if (lane + 64 * k < N) grad_a[(size_t)b * N + lane + 64 * k] = out[k];
+        return;
+    }
     if (!nb) {
         for (int n = lane; n < N; n += 64)
             grad_a[(size_t)b * N + n] = (float)(dr * (v * (double)p[(size_t)b * N + n]) / v);

@@ -78,6 +78,8 @@ SIGNATURES = [
     ("pmenv_window_init", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P]),
     ("pmenv_window_init_days", ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _I32, _P]),
     ("pmenv_gae", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _P]),
+    ("pmenv_gae_workspace", _SZ, [_I32, _I32]),
+    ("pmenv_gae_ex", ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _P, _SZ, _P]),
     ("pmenv_moments_workspace", ctypes.c_size_t, []),
     ("pmenv_moments", ctypes.c_int, [_P, _I64, _P, _P, _P]),
     ("pmenv_replay_gather", ctypes.c_int,

@@ -2,8 +2,9 @@
 
 The reference's replay/rollout_buffer.py stores (s, a, v, r) per day (:43-57) and
 computes no returns; the north star asks for its GAE / discounted-return pass as
-a device kernel. pmenv_gae walks each env's column of a time-major [T, B] rollout
-backwards (one thread per env, coalesced across envs).
+a device kernel. pmenv_gae_ex scans each env's column of a time-major [T, B]
+rollout backwards (lanes = envs, coalesced rows; the horizon split over waves and,
+for few envs, over workgroups).
 """
 import ctypes
 
@@ -29,7 +30,10 @@ def gae(rewards, values, dones=None, gamma=0.99, lam=0.95):
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
     s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
-    _abi.check(lib.pmenv_gae(_p(r), _p(v), _p(d), _p(adv), _p(ret), T, B, gamma, lam, s), None, "pmenv_gae")
+    nbytes = lib.pmenv_gae_workspace(T, B)         # horizon split for few envs x long rollouts
+    work = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=r.device) if nbytes else None
+    _abi.check(lib.pmenv_gae_ex(_p(r), _p(v), _p(d), _p(adv), _p(ret), T, B, gamma, lam, _p(work), nbytes, s),
+               None, "pmenv_gae_ex")
     return adv, ret
 
 

@@ -26,7 +26,7 @@ def _p(t):
 
 class _BatchReward(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, v_prev, p, kind, norm, scale):
+    def forward(ctx, a, v_prev, p, kind, norm, scale, want_ret):
         lib = _abi.load()
         B = a.shape[0]
         a2 = a.detach().reshape(B, -1).to(torch.float32).contiguous()
@@ -35,18 +35,21 @@ class _BatchReward(torch.autograd.Function):
         p2 = p.detach().reshape(B, N).to(device=a.device, dtype=torch.float32).contiguous()
         work = torch.empty(lib.pmenv_batch_reward_workspace(B) // 8, dtype=torch.float64, device=a.device)
         out = torch.empty((), dtype=torch.float32, device=a.device)
-        ret = torch.empty(B, dtype=torch.float32, device=a.device)
+        ret = torch.empty(B, dtype=torch.float32, device=a.device) if want_ret else None
         s = ctypes.c_void_p(torch.cuda.current_stream(a.device).cuda_stream)
         _abi.check(lib.pmenv_batch_reward_forward(_p(a2), _p(v2), _p(p2), B, N, _KINDS[kind],
                                                   _abi.BATCH_NORM_MODES[norm], float(scale), _p(work),
-                                                  _p(out), _p(ret), s), None, "pmenv_batch_reward_forward")
+                                                  _p(out), _p(ret) if ret is not None else None, s),
+                   None, "pmenv_batch_reward_forward")
         ctx.save_for_backward(a2, v2, p2, work)
         ctx.kind, ctx.scale, ctx.shape = kind, scale, a.shape
+        if ret is None:
+            return out.to(a.dtype)
         ctx.mark_non_differentiable(ret)
         return out.to(a.dtype), ret
 
     @staticmethod
-    def backward(ctx, grad_out, _grad_ret):
+    def backward(ctx, grad_out, _grad_ret=None):
         lib = _abi.load()
         a2, v2, p2, work = ctx.saved_tensors
         B, N = a2.shape
@@ -56,7 +59,7 @@ class _BatchReward(torch.autograd.Function):
         _abi.check(lib.pmenv_batch_reward_backward(_p(a2), _p(v2), _p(p2), B, N, _KINDS[ctx.kind],
                                                    float(ctx.scale), _p(work), _p(g), _p(grad_a), s),
                    None, "pmenv_batch_reward_backward")
-        return grad_a.reshape(ctx.shape), None, None, None, None, None
+        return grad_a.reshape(ctx.shape), None, None, None, None, None, None
 
 
 def batch_reward(a, v_prev, p, reward=REWARD, scale=REWARD_SCALE, norm="global_or", return_ret=False):
@@ -66,8 +69,9 @@ def batch_reward(a, v_prev, p, reward=REWARD, scale=REWARD_SCALE, norm="global_o
         raise ValueError(f"norm must be one of {sorted(_abi.BATCH_NORM_MODES)}")
     if not a.is_cuda:
         raise ValueError("pmenv batched reward runs on the GPU only (no CPU fallback)")
-    r, ret = _BatchReward.apply(a, v_prev, p, reward, norm, scale)
-    return (r, ret) if return_ret else r
+    if return_ret:
+        return _BatchReward.apply(a, v_prev, p, reward, norm, scale, True)
+    return _BatchReward.apply(a, v_prev, p, reward, norm, scale, False)
 
 
 def pg_reward(a, _v, _a, p, reward=REWARD, scale=REWARD_SCALE, norm="global_or"):

@@ -176,6 +176,17 @@ def test_gpu_flat_obs_out_vs_oracle_modes(monkeypatch, kw, kind):
               double_buffer=True)
 
 
+@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+@pytest.mark.parametrize("kind", ["simplex", "mixed"])
+def test_gpu_flat_inplace_vs_oracle_modes(monkeypatch, kw, kind):
+    """The in-place flat stream (advance_flat_inplace_kernel + the halo the scalar
+    step copies), the default in-place path above B = 1024, against the oracle."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    from pmenv import TradingEnv
+    assert "advance_flat_inplace_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
+    _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flatip{kw}{kind}".encode()))
+
+
 @pytest.mark.parametrize("N,W,B", [
     (30, 50, 37),     # env = 1875 chunks: waves straddle envs and rows
     (5, 4, 13),       # rows of 20 floats: several rows per wave, chunks straddle rows
@@ -193,6 +204,19 @@ def test_gpu_flat_obs_out_shapes(monkeypatch, N, W, B, knobs):
         monkeypatch.setenv(*kv.split("="))
     _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 7 + W, double_buffer=True)
     _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + W, double_buffer=True)
+
+
+@pytest.mark.parametrize("N,W,B", [(30, 50, 37), (5, 4, 13), (4, 2, 7), (1, 4, 9), (64, 16, 3), (129, 50, 2),
+                                   (12, 10, 1), (30, 50, 600)])
+@pytest.mark.parametrize("knobs", ["", "PMENV_FLAT_IP_BLOCK=256", "PMENV_FLAT_IP_BLOCK=1024+PMENV_STREAM_POL=0"])
+def test_gpu_flat_inplace_shapes(monkeypatch, N, W, B, knobs):
+    """Workgroup seams (the halo) at every alignment against rows, envs and the
+    tensor's end; (30, 50, 600): hundreds of workgroups, each seam's halo exercised."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    for kv in filter(None, knobs.split("+")):
+        monkeypatch.setenv(*kv.split("="))
+    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 5 + W)
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 3 * W)
 
 
 def test_gpu_flat_resident_series_obs_out(monkeypatch):
@@ -378,6 +402,28 @@ def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
     np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 8192), (700, 4099),
+                                 (16384, 64)])
+def test_gpu_gae_horizon_split_matches_oracle(T, B):
+    """The default wrapper path (pmenv_gae_ex): few envs x long horizons split the
+    horizon across workgroups (maps pass + apply pass) — vs the oracle's recursion,
+    with episode ends inside and across the chunk boundaries."""
+    from pmenv import _abi, rollout
+    lib = _abi.load()
+    assert lib.pmenv_gae_workspace(T, B) > 0
+    rng = np.random.default_rng(T * 7 + B)
+    r = rng.standard_normal((T, B)).astype(np.float32)
+    v = rng.standard_normal((T + 1, B)).astype(np.float32)
+    d = rng.random((T, B)) < 0.003
+    adv, ret = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
+    oadv, oret = or_gae(r, v, d, 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
+    adv2, _ = rollout.gae(_t(r), _t(v), None, 0.99, 1.0)          # no dones, lambda = 1: long carries
+    oadv2, _ = or_gae(r, v, np.zeros_like(d), 0.99, 1.0)
+    np.testing.assert_allclose(adv2.cpu().numpy(), oadv2, rtol=1e-5, atol=1e-4)
+
+
 def test_gpu_gae_and_moments_match_oracle():
     from pmenv import rollout
     rng = np.random.default_rng(1)
@@ -464,7 +510,15 @@ def test_gpu_step_is_graph_capturable():
     assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)
 
 
-def test_gpu_resident_series_equals_bar_batch():
+@pytest.fixture(params=["fused", "flat"])
+def step_kernels(request, monkeypatch):
+    """B = 97 takes the one-launch step by default; "flat" forces the two-launch flat path."""
+    if request.param == "flat":
+        monkeypatch.setenv("PMENV_FUSED", "0")
+    return request.param
+
+
+def test_gpu_resident_series_equals_bar_batch(step_kernels):
     """Resident-series data path (env b reads series[day[b]]) == stepping with the
     gathered bar batch, bit for bit; windows initialised from per-env start days."""
     from pmenv import TradingEnv, MarketSeries

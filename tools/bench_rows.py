@@ -1,13 +1,16 @@
-"""Measure the SURVEY.md §8f kernels (f1 GAE, f2 batched reward, f3 resident-series
-advance, f4 replay gather + metrics) against their algorithmic bytes.
+"""Measure the SURVEY.md §8f kernels (f1 GAE + moments, f2 batched reward, f3
+resident-series advance, f4 replay gather + metrics) against their algorithmic bytes.
 
-Each case is timed with HIP events on torch's current stream (the stream the
-wrappers launch on), median of `--reps` calls after warmup. Wrapper overhead
-(allocations, ctypes) is inside the timed calls; run under
-`rocprofv3 --kernel-trace --stats` for kernel-only durations.
+Every case calls the C ABI directly on preallocated device buffers (what a training
+loop does), timed with HIP events on torch's current stream — the stream the calls
+enqueue on — per call, as the median over `--reps` groups of 10 back-to-back calls
+after warmup. A case is one ABI call (its kernels and the boundaries between them,
+no allocation). Run under
+`rocprofv3 --kernel-trace --stats` for per-kernel durations.
 Prints one JSON object; `--out` writes it too.
 """
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -17,13 +20,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
 import torch  # noqa: E402
 
-from pmenv import MarketSeries, TradingEnv, rollout, synth, trainer  # noqa: E402
-from pmenv.replay import DeviceReplay, trajectory_metrics  # noqa: E402
+from pmenv import MarketSeries, TradingEnv, synth, _abi  # noqa: E402
+from pmenv.replay import DeviceReplay  # noqa: E402
 
 PEAK_GBS = 8000.0
 
 
-def timeit(fn, reps, warmup=3):
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def timeit(fn, reps, warmup=3, inner=10):
+    """Median over `reps` groups of `inner` back-to-back calls (per call): launch
+    latency overlaps the previous call, as in a training loop."""
     st = torch.cuda.current_stream()
     for _ in range(warmup):
         fn()
@@ -31,10 +40,11 @@ def timeit(fn, reps, warmup=3):
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
-        fn()
+        for _ in range(inner):
+            fn()
         b.record(st)
         b.synchronize()
-        ts.append(a.elapsed_time(b) * 1e3)
+        ts.append(a.elapsed_time(b) * 1e3 / inner)
     return statistics.median(ts)
 
 
@@ -49,82 +59,140 @@ def row(name, us, alg_bytes, **kw):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="")
+    ap.add_argument("--only", default="", help="comma list of f1,f2,f3,f4 (default: all)")
     a = ap.parse_args()
+    only = set(a.only.split(",")) if a.only else {"f1", "f2", "f3", "f4"}
     dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lib = _abi.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device=dev).manual_seed(0)
     res = []
 
-    # f1: GAE over a time-major rollout, loop (thread per env) vs wave scan
-    for T, B, dn in ((256, 65536, True), (2048, 8192, True), (4096, 512, True), (16384, 64, False)):
-        r = torch.randn(T, B, device=dev, generator=g)
-        v = torch.randn(T + 1, B, device=dev, generator=g)
-        d = (torch.rand(T, B, device=dev, generator=g) < 0.01) if dn else None
-        alg = T * B * (4 + 4 + 4 + 4 + (1 if dn else 0)) + B * 4
-        for mode in ("loop", "scan", "tile", "tile16"):
-            os.environ["PMENV_GAE"] = mode.rstrip("16")
-            os.environ["PMENV_GAE_U"] = "16" if mode.endswith("16") else "8"
-            us = timeit(lambda: rollout.gae(r, v, d, 0.99, 0.95), a.reps)
-            res.append(row(f"gae_{mode}", us, alg, T=T, B=B, dones=dn))
-        os.environ.pop("PMENV_GAE", None)
-        os.environ.pop("PMENV_GAE_U", None)
+    def ck(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed: {rc}")
 
-    # f1: advantage moments (the 24-byte all-reduce's input)
-    x = torch.randn(256 * 65536, device=dev, generator=g)
-    res.append(row("moments", timeit(lambda: rollout.moments(x), a.reps), x.numel() * 4, n=x.numel()))
+    if "f1" in only:
+        # GAE over a time-major rollout: per-env loop, wave scan, tiled scan (U = 8, 16)
+        for T, B, dn in ((256, 65536, True), (256, 16384, True), (256, 4096, True), (2048, 8192, True),
+                         (4096, 512, True), (16384, 64, False)):
+            r = torch.randn(T, B, device=dev, generator=g)
+            v = torch.randn(T + 1, B, device=dev, generator=g)
+            d = (torch.rand(T, B, device=dev, generator=g) < 0.01).to(torch.uint8) if dn else None
+            adv, ret = torch.empty_like(r), torch.empty_like(r)
+            alg = T * B * (4 + 4 + 4 + 4 + (1 if dn else 0)) + B * 4
+            modes = ("loop", "scan", "tile", "tile16", "auto") if T * B <= (1 << 24) else ("tile", "tile16", "auto")
+            nbytes = lib.pmenv_gae_workspace(T, B)
+            work = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=dev)
+            for mode in modes:
+                for k in ("PMENV_GAE", "PMENV_GAE_U"):
+                    os.environ.pop(k, None)
+                if mode != "auto":
+                    os.environ["PMENV_GAE"] = mode.rstrip("16")
+                    os.environ["PMENV_GAE_U"] = "16" if mode.endswith("16") else "8"
+                # auto = what rollout.gae runs: pmenv_gae_ex with its workspace (horizon split)
+                us = timeit(lambda: ck(lib.pmenv_gae_ex(P(r), P(v), P(d), P(adv), P(ret), T, B, 0.99, 0.95, P(work),
+                                                        nbytes, st), "gae"), a.reps)
+                res.append(row(f"gae_{mode}", us, alg, T=T, B=B, dones=dn, split=bool(nbytes) and mode == "auto"))
+            for k in ("PMENV_GAE", "PMENV_GAE_U"):
+                os.environ.pop(k, None)
+            del r, v, d, adv, ret
+        # advantage moments (the 24-byte all-reduce's input)
+        for n in (256 * 65536, 256 * 4096):
+            x = torch.randn(n, device=dev, generator=g)
+            out = torch.empty(3, dtype=torch.float64, device=dev)
+            work = torch.empty(lib.pmenv_moments_workspace() // 8, dtype=torch.float64, device=dev)
+            us = timeit(lambda: ck(lib.pmenv_moments(P(x), n, P(out), P(work), st), "moments"), a.reps)
+            res.append(row("moments", us, n * 4, n=n))
 
-    # f2: differentiable batched PG reward, forward + backward
-    for B, N in ((65536, 30), (8192, 500)):
-        act = torch.randn(B, N, 1, device=dev, generator=g, requires_grad=True)
-        vp = torch.rand(B, 1, 1, device=dev, generator=g) + 1.0
-        p = 1.0 + 0.01 * torch.randn(B, N, 1, device=dev, generator=g)
+    if "f2" in only:
+        # differentiable batched PG reward: forward (reward only) and backward
+        for B, N in ((65536, 30), (16384, 30), (4096, 30), (8192, 500)):
+            act = torch.randn(B, N, device=dev, generator=g)
+            vp = torch.rand(B, device=dev, generator=g) + 1.0
+            p = 1.0 + 0.01 * torch.randn(B, N, device=dev, generator=g)
+            work = torch.empty(lib.pmenv_batch_reward_workspace(B) // 8, dtype=torch.float64, device=dev)
+            rout = torch.empty((), device=dev)
+            go = torch.ones((), device=dev)
+            ga = torch.empty_like(act)
+            fwd = lambda: ck(lib.pmenv_batch_reward_forward(P(act), P(vp), P(p), B, N, 0, 0, 1.0, P(work),  # noqa: E731
+                                                            P(rout), None, st), "fwd")
+            bwd = lambda: ck(lib.pmenv_batch_reward_backward(P(act), P(vp), P(p), B, N, 0, 1.0, P(work), P(go),  # noqa: E731
+                                                             P(ga), st), "bwd")
+            fwd()
+            f_bytes = B * N * 4 * 2 + B * 4
+            res.append(row("batch_reward_fwd", timeit(fwd, a.reps), f_bytes, B=B, N=N))
+            res.append(row("batch_reward_bwd", timeit(bwd, a.reps), f_bytes + B * N * 4, B=B, N=N))
 
-        def fwd_bwd():
-            act.grad = None
-            trainer.pg_reward(act, vp, None, p).backward()
-        alg = B * N * 4 * 2 + B * 4 + (B * N * 4 * 2 + B * 4 + B * N * 4)   # fwd reads a, p, v; bwd + grad
-        res.append(row("batch_reward_fwd_bwd", timeit(fwd_bwd, a.reps), alg, B=B, N=N))
+    if "f3" in only or "f4" in only:
+        B, N, W, T = 65536, 30, 50, 512
+        bars = synth.series(T, 1, N, device=dev)[:, 0].contiguous()
+        ms = MarketSeries(bars, device=dev)
+    if "f3" in only:
+        # resident series: the env step with a per-env day index into one [T, N, 4] series
+        starts = ms.random_starts(B, W, 64, generator=torch.Generator().manual_seed(1)).to(dev)
+        obs = ms.initial_window(starts, W)
+        out = torch.empty_like(obs)
+        env = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
+        env.reset(obs)
+        actn = synth.actions(1, B, N, device=dev)[0]
+        day = starts.to(torch.int32) + W
+        rew = torch.empty(B, device=dev)
+        bufs = [obs, out]
+        state = {"i": 0}
+        args = _abi.PmenvStepArgs()
+        args.action, args.bar, args.reward = actn.data_ptr(), ms.bars.data_ptr(), rew.data_ptr()
+        args.day, args.series_days = day.data_ptr(), T
 
-    # f3: resident series: advance from a per-env day index into one [T, N, 4] series
-    B, N, W, T = 65536, 30, 50, 512
-    bars = synth.series(T, 1, N, device=dev)[:, 0].contiguous()
-    ms = MarketSeries(bars, device=dev)
-    starts = ms.random_starts(B, W, 64, generator=torch.Generator().manual_seed(1)).to(dev)
-    obs = ms.initial_window(starts, W)
-    out = torch.empty_like(obs)
-    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
-    env.reset(obs)
-    actn = synth.actions(1, B, N, device=dev)[0]
-    day = starts.to(torch.int32) + W
-    bufs = [obs, out]
-    state = {"i": 0}
+        def step_series(db):
+            i = state["i"]
+            args.obs = bufs[i % 2].data_ptr()
+            args.obs_out = bufs[(i + 1) % 2].data_ptr() if db else None
+            ck(lib.pmenv_step_ex(env._h, ctypes.byref(args), st), "step")
+            if db:
+                state["i"] = i + 1
+        for db in (True, False):
+            us = timeit(lambda: step_series(db), a.reps)
+            res.append(row("step_resident_series", us, B * (8 * N * W * 5 + 20), B=B, N=N, W=W,
+                           windows="double" if db else "inplace"))
+        del obs, out, bufs, env
+    if "f4" in only:
+        # replay gather (S samples of s, s' windows) and trajectory metrics
+        B, N, W, H, S = 4096, 30, 50, 256, 8192
+        rb = DeviceReplay(B, N, W, H, ms)
+        for h in range(H):
+            rb.add(torch.full((B,), W + h, dtype=torch.int32, device=dev), torch.rand(B, N, device=dev),
+                   torch.randn(B, device=dev))
+        h0, e = rb.indices(S, generator=torch.Generator().manual_seed(2))
+        s_ = torch.empty(S, N, W, 5, device=dev)
+        s2 = torch.empty_like(s_)
+        ao = torch.empty(S, N, device=dev)
+        ro = torch.empty(S, device=dev)
+        sb = ms.bars
 
-    def step_series():
-        i = state["i"]
-        env.step(actn, bufs[i % 2], series=ms, day=day, out=bufs[(i + 1) % 2])
-        day.add_(1)
-        state["i"] = i + 1
-    res.append(row("step_resident_series", timeit(step_series, a.reps), B * (8 * N * W * 5 + 20),
-                   B=B, N=N, W=W))
-    del obs, out, bufs, env
-
-    # f4: replay gather (S samples of s, s' windows) and trajectory metrics
-    B, N, W, H, S = 4096, 30, 50, 256, 8192
-    rb = DeviceReplay(B, N, W, H, ms)
-    for h in range(H):
-        rb.add(torch.full((B,), W + h, dtype=torch.int32, device=dev), torch.rand(B, N, device=dev),
-               torch.randn(B, device=dev))
-    h0, e = rb.indices(S, generator=torch.Generator().manual_seed(2))
-    alg = S * (2 * N * W * 5 * 4 + N * 4 + 4)          # written windows dominate; reads hit L2
-    res.append(row("replay_gather", timeit(lambda: rb.gather(h0, e), a.reps), alg, S=S, N=N, W=W))
-    T, B = 252, 65536
-    rets = 0.001 * torch.randn(T, B, device=dev, dtype=torch.float64, generator=g)
-    vals = torch.cumprod(torch.cat([torch.ones(1, B, device=dev, dtype=torch.float64), 1 + rets]), 0)
-    wts = torch.softmax(torch.randn(T + 1, B, 30, device=dev, generator=g), -1)
-    alg = T * B * 8 + (T + 1) * B * 8 + (T + 1) * B * 30 * 4 + B * 5 * 8
-    res.append(row("trajectory_metrics", timeit(lambda: trajectory_metrics(rets, vals, wts), a.reps), alg,
-                   T=T, B=B, N=30))
+        def gather():
+            ck(lib.pmenv_replay_gather(P(sb), sb.shape[0], N, 5, W, P(rb.days), P(rb.actions), P(rb.rewards), H, B,
+                                       P(h0), P(e), S, P(s_), P(s2), P(ao), P(ro), st), "gather")
+        alg = S * (2 * N * W * 5 * 4 + N * 4 + 4)          # written windows dominate; reads hit L2
+        res.append(row("replay_gather", timeit(gather, a.reps), alg, S=S, N=N, W=W))
+        del rb, s_, s2
+        for T, B in ((252, 65536), (252, 4096)):
+            rets = 0.001 * torch.randn(T, B, device=dev, dtype=torch.float64, generator=g)
+            vals = torch.cumprod(torch.cat([torch.ones(1, B, device=dev, dtype=torch.float64), 1 + rets]), 0)
+            wts = torch.softmax(torch.randn(T + 1, B, 30, device=dev, generator=g), -1)
+            out = torch.empty(B, 5, dtype=torch.float64, device=dev)
+            alg = T * B * 8 + (T + 1) * B * 8 + (T + 1) * B * 30 * 4 + B * 5 * 8
+            for mode in ("seg", "walk"):
+                os.environ.pop("PMENV_METRICS_WALK", None)
+                if mode == "walk":
+                    os.environ["PMENV_METRICS_WALK"] = "1"
+                us = timeit(lambda: ck(lib.pmenv_metrics(P(rets), P(vals), P(wts), T, B, 30, 0.04, 252.0, P(out), st),
+                                       "metrics"), a.reps)
+                res.append(row(f"trajectory_metrics_{mode}", us, alg, T=T, B=B, N=30))
+            os.environ.pop("PMENV_METRICS_WALK", None)
 
     doc = {"device": torch.cuda.get_device_name(0), "peak_GBs": PEAK_GBS, "cases": res}
     print(json.dumps(doc, indent=1))
