@@ -1,0 +1,78 @@
+"""An on-policy training loop over B lockstep envs — the shape of train/on_policy.py
+(`Train._rollout` :59-67 and `Train._update` :69-74) with the env step, the rollout
+storage, the return pass and the trainer reward all on device.
+
+    reference (one env)                         here (B envs, one launch per step each)
+    s = env.reset(data)                 :62     env.reset(buf.obs(0))
+    a = agent.act(s)                    :64     a = policy(buf.obs(t-1))            (torch, no grad)
+    r, s_ = env.step(a, data, prices)   :65     env.step(a, buf.obs(t-1), bar=..., out=buf.obs(t))
+    buffer.add(s, a, env.value, r)      :66     buf.add(a, env.value, r)
+    for ... in buffer.sample_random():  :71     for s, a, r, _v, _a, p in buf.sample_random(bs):
+        agent.update(i, s, a, r, _v, _a, p)         loss = a2c_loss(policy(s), _v, _a, p); step
+
+The policy is any torch module mapping [S, N, W, F] windows to [S, N, 1] scores
+(the reference's LSRE-CANN is out of scope; `WindowPolicy` below is a small stand-in).
+"""
+import torch
+
+from .rollout_buffer import DeviceRolloutBuffer
+from .trainer import a2c_loss
+
+
+class WindowPolicy(torch.nn.Module):
+    """Per-asset MLP over the log-price window (a stand-in for net/lsre_cann.py):
+    [S, N, W, F] -> [S, N, 1] scores; the batched reward normalises them."""
+
+    def __init__(self, window, features=5, hidden=32):
+        super().__init__()
+        self.net = torch.nn.Sequential(torch.nn.Linear(window * features, hidden), torch.nn.Tanh(),
+                                       torch.nn.Linear(hidden, 1))
+
+    def forward(self, s):
+        S, N, W, F = s.shape
+        x = s.clone()
+        last = x[..., W - 1:W, :F - 1].clamp(min=1e-12)
+        x[..., :F - 1] = torch.log(x[..., :F - 1].clamp(min=1e-12) / last)   # prices relative to the last close
+        return self.net(x.reshape(S, N, W * F))
+
+
+class OnPolicy:
+    def __init__(self, env, policy, horizon, series=None, lr=1e-3, batch_size=256, generator=None):
+        cfg = env.cfg
+        self.env, self.policy = env, policy
+        self.buf = DeviceRolloutBuffer(cfg.num_envs, cfg.num_assets, cfg.window, horizon, cfg.features,
+                                       device=env.device, init_cash=cfg.init_cash, close_channel=cfg.close_channel)
+        self.optim = torch.optim.Adam(policy.parameters(), lr=lr)
+        self.batch_size = batch_size
+        self.generator = generator
+        self.series = series
+
+    def act(self, s):
+        """agent.act (pg.py:29-38): the policy's scores, softmaxed over assets."""
+        with torch.no_grad():
+            return torch.softmax(self.policy(s).squeeze(-1), dim=-1)
+
+    def rollout(self, obs0, bars):
+        """train/on_policy.py:59-67 for every env at once. obs0 [B, N, W, F] is the
+        reset window; bars[t] the day's [B, N, F-1] bars (t = 0 .. horizon-1)."""
+        buf, env = self.buf, self.env
+        buf.reset(obs0)
+        env.reset(buf.obs(0))
+        rewards = []
+        for t in range(1, buf.T + 1):
+            a = self.act(buf.obs(t - 1))
+            r, _ = env.step(a, buf.obs(t - 1), bar=bars[t - 1], out=buf.obs(t))
+            buf.add(a, env.value, r)
+            rewards.append(r)
+        return torch.stack(rewards)
+
+    def update(self):
+        """train/on_policy.py:69-74 with A2C._loss (a2c.py:40-82) as the fused HIP op."""
+        losses = []
+        for s, a, r, v_prev, a_prev, p in self.buf.sample_random(self.batch_size, self.generator):
+            self.optim.zero_grad(set_to_none=True)
+            loss = a2c_loss(self.policy(s), v_prev, a_prev, p)
+            loss.backward()
+            self.optim.step()
+            losses.append(loss.detach())
+        return torch.stack(losses) if losses else torch.empty(0)

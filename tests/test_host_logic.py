@@ -62,3 +62,37 @@ def test_device_replay_ring_indices_cpu():
     assert set(env.tolist()) == set(range(B))
     with pytest.raises(ValueError):
         DeviceReplay(B, N, W, W + 1, None)
+
+
+def test_rollout_buffer_sampling_host_logic():
+    """DeviceRolloutBuffer's indexing (no GPU needed: the buffer is plain torch storage):
+    every (step, env) pair of a rollout is sampled exactly once per pass, and a sample
+    carries the window the action was taken on, the previous value / action and the
+    close relative of its step (replay/rollout_buffer.py:103-142)."""
+    import torch
+    from pmenv.rollout_buffer import DeviceRolloutBuffer
+    B, N, W, T = 5, 3, 4, 6
+    buf = DeviceRolloutBuffer(B, N, W, T, device="cpu")
+    g = torch.Generator().manual_seed(0)
+    obs0 = torch.rand(B, N, W, 5, generator=g) + 0.5
+    buf.reset(obs0)
+    assert torch.equal(buf.obs(0), obs0) and bool((buf.a[0, :, 0] == 1).all()) and bool((buf.v[0] == 25000).all())
+    for t in range(1, T + 1):
+        buf.obs(t).copy_(torch.rand(B, N, W, 5, generator=g) + 0.5)
+        buf.add(torch.full((B, N), float(t)), torch.full((B,), 1000.0 + t, dtype=torch.float64), torch.full((B,), -t))
+    assert len(buf) == T
+    with pytest.raises(IndexError):
+        buf.add(torch.zeros(B, N), torch.zeros(B), torch.zeros(B))
+    seen = []
+    for s, a, r, v_prev, a_prev, p in buf.sample_random(10, generator=torch.Generator().manual_seed(1)):
+        assert s.shape == (10, N, W, 5) and a.shape == (10, N, 1) and r.shape == (10, 1, 1)
+        assert v_prev.shape == (10, 1, 1) and a_prev.shape == (10, N, 1) and p.shape == (10, N, 1)
+        t = a[:, 0, 0].long()                                  # step index, as filled above
+        assert torch.equal(r[:, 0, 0], -t.float())
+        assert torch.equal(v_prev[:, 0, 0], torch.where(t == 1, 25000.0, 1000.0 + t - 1).float())
+        env = torch.tensor([next(e for e in range(B) if torch.equal(s[i], buf.s[t[i] - 1, e])) for i in range(10)])
+        assert torch.equal(p[..., 0], buf.s[t, env][..., W - 1, 3] / buf.s[t - 1, env][..., W - 1, 3])
+        seen += list(zip(t.tolist(), env.tolist()))
+    assert len(seen) == len(set(seen)) == T * B              # a permutation of all pairs
+    ordered = [tuple(x) for s, a, *_ in buf.sample(B) for x in zip(a[:, 0, 0].long().tolist(), range(B))]
+    assert ordered == [(t, e) for t in range(1, T + 1) for e in range(B)]
