@@ -9,10 +9,12 @@ price relatives from the close channel, action normalisation, portfolio value
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
 assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
 Philox OHLC series and softmax actions already resident in HBM. The step runs as
-two launches (scalar_step_kernel, then the streaming advance_flat_kernel); the
-window is double-buffered by default (each day's window is a fresh buffer, as the
-reference's data path hands the env a new window every day — instrument.py:339-356),
-and the in-place advance is timed as well and reported under "inplace".
+two launches (scalar_step_kernel, then the streaming window advance). By default
+the window is advanced in place — the reference's contract: step() mutates the
+caller's features and returns them (trading_env.py:102-105) — by
+advance_flat_inplace_kernel; the double-buffered advance (obs -> a fresh buffer,
+advance_flat_kernel, the form the device rollout buffer uses) is timed as well and
+reported under "alt".
 Multi-GPU runs are weak-scaled (65,536 envs per rank, envs sharded by global id,
 no collective in the step) and launched one process per GPU:
 
@@ -60,11 +62,12 @@ def parse():
     ap.add_argument("--mae-envs", type=int, default=4096)
     ap.add_argument("--mae-steps", type=int, default=64)
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--windows", choices=["double", "inplace"], default="double")
+    ap.add_argument("--windows", choices=["double", "inplace"], default="inplace")
     ap.add_argument("--reward", default="log_returns",
                     choices=["log_returns", "returns", "sharpe_ratio", "diff_sharpe"])
     ap.add_argument("--commission", type=float, default=0.0)
-    ap.add_argument("--inplace-steps", type=int, default=50, help="extra timed in-place steps (0: skip)")
+    ap.add_argument("--alt-steps", type=int, default=50,
+                    help="extra timed steps of the other window mode (0: skip)")
     return ap.parse_args()
 
 
@@ -177,7 +180,7 @@ def main():
     env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev,
                      reward=args.reward, commission=args.commission)
     env.reset(obs)
-    obs_b = torch.empty_like(obs) if args.windows == "double" else None
+    obs_b = torch.empty_like(obs) if (args.windows == "double" or args.alt_steps > 0) else None
     reward = torch.empty(B, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
@@ -233,14 +236,15 @@ def main():
 
     double = args.windows == "double"
     elapsed, kern_avg_s = timed(args.steps, args.warmup, double)
-    inplace = None
-    if double and args.inplace_steps > 0:
-        # continue from the latest window, advancing it in place
-        if (args.warmup + args.steps) % 2:
+    alt = None
+    if args.alt_steps > 0:
+        # the other window mode, continuing from the latest window
+        if double and (args.warmup + args.steps) % 2:
             obs.copy_(obs_b)
-        ip_el, ip_k = timed(args.inplace_steps, 2, False)
-        inplace = {"env_steps_per_s_per_gpu": B * args.inplace_steps / ip_el,
-                   "ms_per_step": ip_el / args.inplace_steps * 1e3, "advance_kernel_avg_us": ip_k * 1e6}
+        a_el, a_k = timed(args.alt_steps, 2, not double)
+        alt = {"windows": "inplace" if double else "double",
+               "env_steps_per_s_per_gpu": B * args.alt_steps / a_el,
+               "ms_per_step": a_el / args.alt_steps * 1e3, "advance_kernel_avg_us": a_k * 1e6}
 
     if world > 1:
         t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64,
@@ -250,10 +254,12 @@ def main():
     nonfinite = env.nonfinite_count()
 
     path = env.step_path
-    if double and "advance_flat_kernel" in path:
-        advance_kernel = "advance_flat_kernel"
-    elif "step_advance_lds_kernel" in path:
+    if "step_advance_lds_kernel" in path:
         advance_kernel = "step_advance_lds_kernel"
+    elif double and "advance_flat_kernel" in path:
+        advance_kernel = "advance_flat_kernel"
+    elif not double and "advance_flat_inplace_kernel" in path:
+        advance_kernel = "advance_flat_inplace_kernel"
     else:
         advance_kernel = "advance_rows_kernel"
     total_env_steps = world * B * args.steps
@@ -263,7 +269,8 @@ def main():
     traffic = None
     try:
         pmc = json.load(open(args.pmc_file))
-        if pmc.get("workload") == [B, N, W, F]:
+        # PMC passes of the same kernel at the same workload only
+        if pmc.get("workload") == [B, N, W, F] and f"::{advance_kernel}<" in pmc.get("dominant_kernel", ""):
             traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -304,7 +311,7 @@ def main():
             "parity_sample": mae,
             "nonfinite_envs": nonfinite,
             "step_path": env.step_path,
-            "inplace": inplace,
+            "alt": alt,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
