@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+EVENT_EVERY = 4        # steps per sampled advance-kernel timing inside the timed region
 
 
 def step_bytes(N, W, F):
@@ -222,10 +223,13 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        # the advance kernel is bracketed by HIP events on every EVENT_EVERY-th step of
+        # the timed region (each event pair costs the stream a few microseconds)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(0, steps, EVENT_EVERY)]
         t0 = time.perf_counter()
         for i in range(steps):
-            one_step(warmup + i, double, ev[i])
+            one_step(warmup + i, double, ev[i // EVENT_EVERY] if i % EVENT_EVERY == 0 else None)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
