@@ -802,10 +802,40 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     if (!series || !days || !actions || !rewards || !h0 || !env || !s || !s_next || !a_out || !r_out || T < 1 ||
         N < 1 || F < 2 || W < 1 || H < W + 1 || B < 1 || S < 1)
         return PMENV_ERR_ARG;
-    // one workgroup per sample with the W+1 staged days in LDS when they fit in 64 KiB
-    // (N = 30, W = 50: 30.6 KiB), else one thread per output float
+    // F = 5: vector staging per asset group (replay_gather_f5_kernel); otherwise one
+    // workgroup per sample with the W+1 staged days in LDS when they fit in 64 KiB, else
+    // one thread per output float. Measured at S = 8,192, N = 30, W = 50: 131 us for the
+    // whole-sample f5 form against 204 us for the per-element staging (bench_rows.py)
     const size_t lds = (size_t)N * (W + 1) * F * sizeof(float);
-    if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
+    const bool al16 = ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0 && ((uintptr_t)series & 15u) == 0;
+    // F = 5 vector staging over asset groups of R rows: R divides N, R*W*F is a multiple
+    // of 4 (16-B aligned groups), R*(W+1) <= 512 pairs (two per thread) when possible
+    int R = 0;
+    if (F == 5 && al16 && !getenv("PMENV_REPLAY_LDS")) {   // A/B knob: the per-element staging kernel
+        // the largest group within 2,048 pairs: whole samples measured faster than
+        // 10-asset groups (131 vs 148 us at N = 30, W = 50) — every workgroup pays the
+        // sample's dependent index loads once
+        for (int r = N; r >= 1; --r)
+            if (N % r == 0 && ((int64_t)r * W * F) % 4 == 0 && (int64_t)r * (W + 1) <= 2048 && r <= 256) {
+                R = r;
+                break;
+            }
+    }
+    if (R > 0) {
+        const FastDiv dr = make_fastdiv((uint32_t)R), dwf = make_fastdiv((uint32_t)(W * F));
+        const size_t glds = (size_t)R * (W + 1) * F * sizeof(float);
+        const dim3 grid((unsigned)S, (unsigned)(N / R));
+        const int pairs = R * (W + 1);
+        if (pairs <= 2 * 256)
+            replay_gather_f5_kernel<2><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
+                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
+        else if (pairs <= 4 * 256)
+            replay_gather_f5_kernel<4><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
+                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
+        else
+            replay_gather_f5_kernel<8><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
+                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
+    } else if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
         replay_gather_lds_kernel<<<(unsigned)S, 256, lds, stream>>>(series, T, N, F, W, days, actions, rewards, H, B,
                                                                    h0, env, s, s_next, a_out, r_out);
     } else {

@@ -258,4 +258,85 @@ __global__ __launch_bounds__(256) void replay_gather_lds_kernel(const float* ser
     }
 }
 
+// F = 5 form of the LDS gather with every load in flight before the first LDS
+// write. Workgroup (j, g) stages sample j's assets [g*R, (g+1)*R) — a few asset
+// rows, so the LDS image is ~10 KiB and many workgroups share a CU — thread i
+// taking the (day, asset) pairs i, i + 256, ... (PPT at most): the pair's four
+// market floats as ONE 16-B load from the [T, N, 4] series and its action as one
+// dword; then the image [R][W+1][5] in LDS; then its rows of s and s' as whole
+// 16-B chunks (R*W*5 is a multiple of 4, so every group starts 16-B aligned).
+// Index divisions by R and W*F are multiply-high.
+template <int PPT>
+__global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* series, int T, int N, int W,
+                                                               const int32_t* days, const float* actions,
+                                                               const float* rewards, int H, int B,
+                                                               const int32_t* h0, const int32_t* env, float* s,
+                                                               float* s_next, float* a_out, float* r_out, int R,
+                                                               FastDiv div_r, FastDiv div_wf) {
+    constexpr int F = 5;
+    extern __shared__ __attribute__((aligned(16))) float ext[];
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const int n0 = blockIdx.y * R;
+    const int b = env[j], hj = h0[j];
+    const int W1 = W + 1;
+    // the day index goes out first, the actions (which need only b and hj) behind it,
+    // so the wait for the day leaves the action loads in flight
+    const int dlast = days[(size_t)((hj + W - 1) % H) * B + b];
+    const int P = R * W1;
+    f4 mk[PPT];
+    float ac[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int it = min(tid + k * 256, P - 1);
+        const int t = (int)fdiv((uint32_t)it, div_r), n = n0 + it - t * R;
+        int h = hj + t;
+        h = h >= H ? h - H : h;
+        ac[k] = actions[((size_t)h * B + b) * N + n];
+    }
+    const int d0 = dlast - (W - 1);
+    const auto rs_ser = make_rsrc(series, (uint32_t)T * (uint32_t)N * 16u);
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int it = min(tid + k * 256, P - 1);
+        const int t = (int)fdiv((uint32_t)it, div_r), n = n0 + it - t * R;
+        const int d = d0 + t;
+        const bool in = tid + k * 256 < P && d >= 0 && d < T;   // days off the series read NaN below
+        mk[k] = buf_load4(rs_ser, in ? ((uint32_t)d * (uint32_t)N + (uint32_t)n) * 16u : 0xFFFFFFF0u);
+    }
+    if (tid < R) a_out[(size_t)j * N + n0 + tid] = actions[((size_t)((hj + W) % H) * B + b) * N + n0 + tid];
+    if (tid == 0 && blockIdx.y == 0) r_out[j] = rewards[(size_t)((hj + W - 1) % H) * B + b];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int it = tid + k * 256;
+        if (it < P) {
+            const int t = (int)fdiv((uint32_t)it, div_r), nl = it - t * R;
+            const int d = d0 + t;
+            const bool in = d >= 0 && d < T;
+            float* dst = ext + ((size_t)nl * W1 + t) * F;
+            dst[0] = in ? mk[k].x : NAN;
+            dst[1] = in ? mk[k].y : NAN;
+            dst[2] = in ? mk[k].z : NAN;
+            dst[3] = in ? mk[k].w : NAN;
+            dst[4] = ac[k];
+        }
+    }
+    __syncthreads();
+    const int WF = W * F, per = R * WF;
+    float* so = s + (size_t)j * N * WF + (size_t)n0 * WF;
+    float* sn = s_next + (size_t)j * N * WF + (size_t)n0 * WF;
+    for (int q = tid; q < per / 4; q += 256) {
+        float v0[4], v1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = 4 * q + k;
+            const int n = (int)fdiv((uint32_t)e, div_wf);
+            const float* x = ext + (size_t)n * F + e;       // LDS row n starts n*F floats later than in s
+            v0[k] = x[0];
+            v1[k] = x[F];
+        }
+        reinterpret_cast<f4*>(so)[q] = f4{v0[0], v0[1], v0[2], v0[3]};
+        reinterpret_cast<f4*>(sn)[q] = f4{v1[0], v1[1], v1[2], v1[3]};
+    }
+}
+
 }  // namespace pmenv_dev

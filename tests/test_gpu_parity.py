@@ -550,15 +550,20 @@ def test_gpu_resident_series_equals_bar_batch(step_kernels):
     assert ea.nonfinite_count() == 1
 
 
-@pytest.mark.parametrize("T,N,W,B,H", [(200, 30, 12, 33, 40),    # LDS-staged, 16-B stores
-                                       (60, 3, 5, 4, 9),          # LDS-staged, sample block not 16-B granular
-                                       (120, 300, 50, 3, 60)])    # staged days > 64 KiB: per-float kernel
-def test_gpu_replay_gather_matches_restatement(T, N, W, B, H):
+@pytest.mark.parametrize("T,N,W,B,H,knob", [
+    (200, 30, 12, 33, 40, ""),                   # F = 5 vector staging (4 pairs per thread)
+    (200, 30, 12, 33, 40, "PMENV_REPLAY_LDS"),   # per-element LDS staging, 16-B stores
+    (300, 30, 50, 17, 80, ""),                   # F = 5 vector staging, 8 pairs per thread (BASELINE shape)
+    (60, 3, 5, 4, 9, ""),                        # LDS-staged, sample block not 16-B granular
+    (120, 300, 50, 3, 60, "")])                  # staged days > 64 KiB: per-float kernel
+def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch):
     """replay/buffer.py:39-79 sample on device vs the numpy restatement
     (the reference module is not importable: parity restated from its text)."""
     from pmenv import MarketSeries
     from pmenv.replay import DeviceReplay
     from oracle import replay_gather
+    if knob:
+        monkeypatch.setenv(knob, "1")
     rng = np.random.default_rng(4)
     bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
     m = MarketSeries(bars, device=DEV)

@@ -177,7 +177,12 @@ def main():
             ck(lib.pmenv_replay_gather(P(sb), sb.shape[0], N, 5, W, P(rb.days), P(rb.actions), P(rb.rewards), H, B,
                                        P(h0), P(e), S, P(s_), P(s2), P(ao), P(ro), st), "gather")
         alg = S * (2 * N * W * 5 * 4 + N * 4 + 4)          # written windows dominate; reads hit L2
-        res.append(row("replay_gather", timeit(gather, a.reps), alg, S=S, N=N, W=W))
+        for mode in ("f5", "lds"):
+            os.environ.pop("PMENV_REPLAY_LDS", None)
+            if mode == "lds":
+                os.environ["PMENV_REPLAY_LDS"] = "1"
+            res.append(row(f"replay_gather_{mode}", timeit(gather, a.reps), alg, S=S, N=N, W=W))
+        os.environ.pop("PMENV_REPLAY_LDS", None)
         del rb, s_, s2
         for T, B in ((252, 65536), (252, 4096)):
             rets = 0.001 * torch.randn(T, B, device=dev, dtype=torch.float64, generator=g)
