@@ -260,6 +260,8 @@ def main():
     path = env.step_path
     if "step_advance_lds_kernel" in path:
         advance_kernel = "step_advance_lds_kernel"
+    elif double and "advance_flat_wg_kernel" in path:
+        advance_kernel = "advance_flat_wg_kernel"
     elif double and "advance_flat_kernel" in path:
         advance_kernel = "advance_flat_kernel"
     elif not double and "advance_flat_inplace_kernel" in path:

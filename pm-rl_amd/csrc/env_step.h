@@ -646,6 +646,8 @@ struct FlatSide {
     int32_t k;
 };
 
+// SKIP (timing-only ablation bits, 0 in the product): 1 bar, 2 w', 4 counter, 8 day
+template <int SKIP = 0>
 __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t q) {
     constexpr int F = 5;
     const int N = p.N, WF = p.W * F;
@@ -658,16 +660,100 @@ __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t
     const bool touch_last = sd.kk + 3 >= WF - F;
     // branch-free: without a day index the day descriptor has no records (reads 0), so
     // no control flow can hold the streaming loads behind the day's latency
+    // the day index only in resident-series mode: a wave-uniform branch on the kernel
+    // argument, taken after the caller has issued its streaming loads, so the bar
+    // load of the bar-batch mode depends on no other load
     const bool by_day = p.day != nullptr;
-    const int32_t d = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
-        make_rsrc(by_day ? (const void*)p.day : (const void*)p.obs, by_day ? (uint32_t)p.B * 4u : 0u), b * 4u, 0, 0);
+    int32_t d = 0;
+    if (!(SKIP & 8) && by_day) d = p.day[b];
     sd.bar_nan = by_day && (d < 0 || d >= p.series_days);
     const uint32_t bar_bytes = (uint32_t)(by_day ? p.series_days : p.B) * (uint32_t)N * 16u;
     const uint32_t bar_row = by_day ? (uint32_t)d : b;
     const uint32_t bar_off = touch_last && !sd.bar_nan ? (bar_row * (uint32_t)N + row) * 16u : 0xFFFFFFF0u;
-    sd.xb = buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
-    sd.xwp = p.w_new[(size_t)b * N + row];
-    sd.k = p.k[b] - 1;                                                    // scalar_step_kernel counted this step
+    sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f} : buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
+    sd.xwp = (SKIP & 2) ? 0.5f : p.w_new[(size_t)b * N + row];
+    sd.k = (SKIP & 4) ? 0 : p.k[b] - 1;                                   // scalar_step_kernel counted this step
+    return sd;
+}
+
+// flat_side_load for a whole wave through the scalar cache. The wave's 64 chunks
+// touch at most a few consecutive global rows (b*N + row); when they span <= 4 rows
+// (WF >= ~86 floats, N >= 4, bar-batch mode), ONE s_load_dwordx16 fetches those rows'
+// bars, one s_load_dwordx4 their w' and one s_load_dwordx2 the counters of the (at
+// most two) envs, and each lane selects its row's values from SGPRs: no vector
+// memory instruction, no texture-address work, for the side data of the stream.
+// Other waves fall back to the per-lane loads. The 4-row window is clamped inside
+// the arrays (rows g0 .. g0+3 with g0 <= rows - 4), so no load runs past them; the
+// counter pair may read the state blob's next word (the ring follows the counters).
+typedef int i16v_t __attribute__((ext_vector_type(16)));
+typedef int i4v_t __attribute__((ext_vector_type(4)));
+typedef int i2v_t __attribute__((ext_vector_type(2)));
+
+struct WaveSide {
+    bool ok;           // the wave's rows fit one 4-row scalar window
+    uint32_t g0, b0;   // first row of the window, first env of the wave
+    i16v_t bar16;
+    i4v_t w4;
+    i2v_t k2;
+};
+
+// qa_in: the wave's first chunk, nq: chunks the wave covers (both wave-uniform)
+__device__ __forceinline__ WaveSide wave_side_load(const StepParams& p, uint32_t qa_in, uint32_t nq, uint32_t qtot) {
+    constexpr int F = 5;
+    const int N = p.N, WF = p.W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    const uint32_t qa = min(qa_in, qtot - 1u), qb = min(qa_in + nq - 1u, qtot - 1u);
+    const uint32_t ba = fdiv(qa, p.div_units), bb = fdiv(qb, p.div_units);
+    const uint32_t ga = ba * (uint32_t)N + fdiv(4u * (qa - ba * per4), p.div_wf);
+    const uint32_t gb = bb * (uint32_t)N + fdiv(4u * (qb - bb * per4), p.div_wf);
+    const uint32_t rows = (uint32_t)p.B * (uint32_t)N;
+    WaveSide ws;
+    ws.ok = !p.day && gb - ga <= 3u && N >= 4 && rows >= 4u;
+    if (!ws.ok) return ws;
+    ws.g0 = __builtin_amdgcn_readfirstlane(min(ga, rows - 4u));
+    ws.b0 = __builtin_amdgcn_readfirstlane(ba);
+    const float* bar_p = p.bar + (size_t)ws.g0 * 4;
+    const float* w_p = p.w_new + ws.g0;
+    const int32_t* k_p = p.k + ws.b0;
+    asm volatile(
+        "s_load_dwordx16 %0, %3, 0x0\n\t"
+        "s_load_dwordx4 %1, %4, 0x0\n\t"
+        "s_load_dwordx2 %2, %5, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(ws.bar16), "=&s"(ws.w4), "=&s"(ws.k2)       // early clobber: no output may reuse an address SGPR
+        : "s"(bar_p), "s"(w_p), "s"(k_p)
+        : "memory");
+    return ws;
+}
+
+template <int SKIP = 0>
+__device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, const WaveSide& ws, uint32_t q) {
+    if (!ws.ok) return flat_side_load<SKIP>(p, q);
+    constexpr int F = 5;
+    const int N = p.N, WF = p.W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    FlatSide sd;
+    const uint32_t b = fdiv(q, p.div_units);
+    const uint32_t j0 = 4u * (q - b * per4);
+    const uint32_t row = fdiv(j0, p.div_wf);
+    sd.kk = (int)(j0 - row * (uint32_t)WF);
+    const int i = (int)(b * (uint32_t)N + row - ws.g0);               // 0 .. 3
+    // two-level selects on the bits of i with constant SGPR indices (a runtime index
+    // into the SGPR tuple lowers to a 16-way compare chain per value)
+    const int m1 = -(i & 1), m2 = -((i >> 1) & 1);
+    auto sel = [&](int r0, int r1, int r2, int r3) {
+        const int lo = (r1 & m1) | (r0 & ~m1), hi = (r3 & m1) | (r2 & ~m1);
+        return (hi & m2) | (lo & ~m2);
+    };
+    sd.bar_nan = false;
+    sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f}
+                       : f4{__int_as_float(sel(ws.bar16[0], ws.bar16[4], ws.bar16[8], ws.bar16[12])),
+                            __int_as_float(sel(ws.bar16[1], ws.bar16[5], ws.bar16[9], ws.bar16[13])),
+                            __int_as_float(sel(ws.bar16[2], ws.bar16[6], ws.bar16[10], ws.bar16[14])),
+                            __int_as_float(sel(ws.bar16[3], ws.bar16[7], ws.bar16[11], ws.bar16[15]))};
+    sd.xwp = (SKIP & 2) ? 0.5f : __int_as_float(sel(ws.w4[0], ws.w4[1], ws.w4[2], ws.w4[3]));
+    const int mk = -(int)(b != ws.b0);
+    sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - 1;   // scalar_step_kernel counted this step
     return sd;
 }
 
@@ -752,27 +838,66 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint3
 // workgroup, which may already have advanced them: they come from `halo`, a copy of
 // every workgroup's first two chunks taken by the scalar step kernel of the same step
 // (copy_halo below), before any advance store.
-template <int BLOCK, int POL>
-__global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams p, uint32_t qtot) {
+// V chunks per thread: wave w covers the contiguous chunks [c0 + 64V*w, +64V), lane
+// l its chunks 64v + l, so each load and store instruction is a coalesced 1 KiB and
+// the wave's side data is one scalar window.
+// ABL (timing-only ablation, PMENV_ABLATE = 64 + ABL with the flat path; 0 in the
+// product): flat_side_load's SKIP bits (1 bar, 2 w', 4 counter, 8 day), 16 = no halo,
+// 32 = per-lane side loads instead of the wave's scalar loads
+// OUT = true: the same workgroup body double-buffered (obs -> obs_out); the two
+// chunks past the workgroup are then read straight from obs (no halo copy).
+template <int BLOCK, int V, int POL, bool OUT, int ABL>
+__device__ __forceinline__ void flat_wg_body(StepParams& p, uint32_t qtot, f4* sh4) {
     constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
-    __shared__ f4 sh4[BLOCK + 2];
-    const int tid = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * BLOCK;
-    const uint32_t nblk = min((uint32_t)BLOCK, qtot - c0);
+    constexpr int CPW = BLOCK * V;                  // chunks per workgroup
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = blockIdx.x * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
     const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
-    const f4 own = buf_load4<kAux>(rs, (uint32_t)tid * 16u);
+    f4 own[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
     // halo of this workgroup = first two chunks of the next one (none for the last)
-    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? 2u : 0u;
-    const f4 hal = buf_load4<0>(make_rsrc(p.halo + (size_t)blockIdx.x * 8, nh * 16u),
-                                tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
-    const FlatSide sd = flat_side_load(p, min(c0 + (uint32_t)tid, qtot - 1u));
-    sh4[tid] = own;
-    if (tid < 2) sh4[BLOCK + tid] = hal;
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : p.halo + (size_t)blockIdx.x * 8;
+    const f4 hal = (ABL & 16) ? own[0] : buf_load4<0>(make_rsrc(hsrc, nh * 16u),
+                                                      tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    // the window and halo loads go out before anything else (a halo issued after the
+    // own chunk's wait costs every workgroup a second memory round trip)
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t qw = __builtin_amdgcn_readfirstlane(c0 + (uint32_t)(64 * V * wave));
+    WaveSide ws;
+    ws.ok = false;
+    if (!(ABL & 32)) ws = wave_side_load(p, qw, 64u * V, qtot);
+    FlatSide sd[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) sd[v] = flat_side_from_wave<ABL & 15>(p, ws, min(qw + 64u * v + lane, qtot - 1u));
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
     __syncthreads();
-    const f4 n1 = sh4[tid + 1], n2 = sh4[tid + 2];
-    const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
-    const float un[4] = {own.x, own.y, own.z, own.w};
-    buf_store4<kAux>(rs, (uint32_t)tid * 16u, flat_compose(p, sd, un, sh));
+    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, flat_compose(p, sd[v], un, sh));
+    }
+}
+
+template <int BLOCK, int V, int POL, int ABL = 0>
+__global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, false, ABL>(p, qtot, sh4);
+}
+
+// the double-buffered twin of advance_flat_inplace_kernel (same body, OUT = true)
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_wg_kernel(StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, true, 0>(p, qtot, sh4);
 }
 
 // Taken by the scalar step kernels before the in-place flat advance of the same step:

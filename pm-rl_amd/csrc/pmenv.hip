@@ -50,7 +50,8 @@ struct pmenv {
     bool flat;            // double-buffered advance as the flat 16-B stream (advance_flat_kernel)
     int flat_block, flat_pol;
     bool flat_inplace;    // in-place advance as the flat stream + halo (advance_flat_inplace_kernel)
-    int flat_ip_block;
+    int flat_ip_block, flat_ip_vec;   // threads per workgroup, chunks per thread
+    bool flat_db_wg;      // double-buffered advance in the workgroup form (advance_flat_wg_kernel)
     float* halo;          // [halo_wgs][2] float4: first two chunks of every in-place flat workgroup
     uint32_t halo_wgs, flat_qtot;
     int scalar_scratch_floats;
@@ -181,6 +182,13 @@ void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
     const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
     const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
     p.div_units = make_fastdiv(per4);
+    if (h->flat_db_wg) {          // workgroup (LDS) form, 512 threads x 2 chunks
+        const unsigned g = (unsigned)((qtot + 1023) / 1024);
+        if (h->flat_pol == 2) advance_flat_wg_kernel<512, 2, 2><<<g, 512, 0, stream>>>(p, qtot);
+        else if (h->flat_pol == 0) advance_flat_wg_kernel<512, 2, 0><<<g, 512, 0, stream>>>(p, qtot);
+        else advance_flat_wg_kernel<512, 2, 1><<<g, 512, 0, stream>>>(p, qtot);
+        return;
+    }
     const int bk = h->flat_block;
     const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
     if (bk == 128) launch_flat_b<128>(h->flat_pol, p, grid, qtot, stream);
@@ -188,11 +196,11 @@ void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
     else launch_flat_b<256>(h->flat_pol, p, grid, qtot, stream);
 }
 
-template <int BLOCK>
+template <int BLOCK, int V>
 void launch_flat_ip_b(int pol, const StepParams& p, unsigned grid, uint32_t qtot, hipStream_t stream) {
-    if (pol == 1) advance_flat_inplace_kernel<BLOCK, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else if (pol == 2) advance_flat_inplace_kernel<BLOCK, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else advance_flat_inplace_kernel<BLOCK, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    if (pol == 1) advance_flat_inplace_kernel<BLOCK, V, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else if (pol == 2) advance_flat_inplace_kernel<BLOCK, V, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
+    else advance_flat_inplace_kernel<BLOCK, V, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
 }
 
 void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
@@ -200,11 +208,17 @@ void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
     const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
     p.div_units = make_fastdiv(per4);
     p.halo = h->halo;
-    const int bk = h->flat_ip_block;
-    const unsigned grid = (unsigned)((h->flat_qtot + bk - 1) / bk);
-    if (bk == 256) launch_flat_ip_b<256>(h->flat_pol, p, grid, h->flat_qtot, stream);
-    else if (bk == 1024) launch_flat_ip_b<1024>(h->flat_pol, p, grid, h->flat_qtot, stream);
-    else launch_flat_ip_b<512>(h->flat_pol, p, grid, h->flat_qtot, stream);
+    const int cpw = h->flat_ip_block * h->flat_ip_vec;
+    const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
+    const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
+    switch (key) {
+    case 2561: launch_flat_ip_b<256, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    case 2562: launch_flat_ip_b<256, 2>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    case 2564: launch_flat_ip_b<256, 4>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    case 5121: launch_flat_ip_b<512, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    case 10241: launch_flat_ip_b<1024, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    default: launch_flat_ip_b<512, 2>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    }
 }
 
 template <int POL>
@@ -258,6 +272,20 @@ void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
     }
     if (!db && h->flat_inplace && !h->ablate) {
         launch_flat_inplace(h, p, stream);
+        return;
+    }
+    if (!db && h->flat_inplace && h->ablate >= 64) {   // timing-only ablations (PMENV_ABLATE = 64 + bits)
+        const pmenv_cfg& c = h->cfg;
+        p.div_units = make_fastdiv((uint32_t)((int64_t)c.num_assets * c.window * c.features / 4));
+        p.halo = h->halo;
+        const unsigned grid = (unsigned)((h->flat_qtot + 511) / 512);
+#define PMENV_ABL(X) case 64 + X: advance_flat_inplace_kernel<512, 1, 1, X><<<grid, 512, 0, stream>>>(p, h->flat_qtot); break;
+        switch (h->ablate) {
+            PMENV_ABL(1) PMENV_ABL(2) PMENV_ABL(4) PMENV_ABL(6) PMENV_ABL(15) PMENV_ABL(31) PMENV_ABL(32)
+            PMENV_ABL(33)
+            default: break;
+        }
+#undef PMENV_ABL
         return;
     }
     p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
@@ -412,10 +440,13 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
                             plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
                             fused_rows == c.num_assets;
     // flat stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31): the default
-    // for obs_out and, with the halo, in place. Measured on MI355X at the BASELINE shape (tools/gpu_ab_pol.sh,
-    // interleaved rounds, profiles/ab_r01/flat_*.log): 512-thread workgroups with nt loads
-    // and stores 665 us per step against 685 us for whole-env units; 256 threads and the
-    // sc0 nt policy within 1 %; the default cache policy 2 % slower.
+    // in place (with the halo) and double-buffered. Measured on MI355X at the BASELINE
+    // shape in interleaved A/B rounds (tools/gpu_ab_pol.sh, profiles/ab_r01/): a step
+    // (scalar + advance) of 647 us in place with 512 threads x 2 chunks and the wave's
+    // side data through scalar loads, against 683 us at 1 chunk per thread, 689 us with
+    // per-lane side loads and 802 us for whole-row units; double-buffered 647 us in the
+    // workgroup (LDS) form against 664 us for the ds_bpermute form; the nt cache policy
+    // 2-5 % ahead of the default.
     h->flat = false;
     h->flat_block = 512;
     {
@@ -423,17 +454,30 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
                              (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
         h->flat = flat_ok;
-        // in place: 711 us per step against 802 us for the whole-row units (same A/B);
-        // 256 / 1024-thread workgroups 8-9 % slower, the default cache policy 5 %
         h->flat_inplace = flat_ok;
+        h->flat_db_wg = true;
         h->flat_ip_block = 512;
+        h->flat_ip_vec = 2;
         h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         if (getenv("PMENV_STREAM_POL") == nullptr) h->flat_pol = 1;
-        if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;   // A/B knob
+        // A/B knobs
+        if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
         if (const char* knob = getenv("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
+        if (const char* knob = getenv("PMENV_FLAT_DB_WG")) h->flat_db_wg = atoi(knob) != 0;
         if (const char* knob = getenv("PMENV_FLAT_IP_BLOCK")) {
             const int bk = atoi(knob);
             if (bk == 256 || bk == 512 || bk == 1024) h->flat_ip_block = bk;
+        }
+        if (const char* knob = getenv("PMENV_FLAT_IP_VEC")) {   // chunks per thread
+            const int v = atoi(knob);
+            if (v == 1 || v == 2 || v == 4) h->flat_ip_vec = v;
+        }
+        {   // the launcher's (block, vec) table: anything else takes the default 512 x 2
+            const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
+            if (key != 2561 && key != 2562 && key != 2564 && key != 5121 && key != 5122 && key != 10241) {
+                h->flat_ip_block = 512;
+                h->flat_ip_vec = 2;
+            }
         }
         if (const char* knob = getenv("PMENV_FLAT_BLOCK")) {
             const int bk = atoi(knob);
@@ -498,7 +542,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->owns_state = true;
     }
     if (h->flat_inplace) {
-        const uint32_t wgs = (h->flat_qtot + h->flat_ip_block - 1) / h->flat_ip_block;
+        const uint32_t cpw = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
+        const uint32_t wgs = (h->flat_qtot + cpw - 1) / cpw;
         h->halo_wgs = wgs > 0 ? wgs - 1 : 0;
         hipError_t ae = hipMalloc(&h->halo, (size_t)(h->halo_wgs + 1) * 32);
         if (ae != hipSuccess) {
@@ -606,7 +651,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
             if (p.obs_out == p.obs && h->flat_inplace && !h->ablate) {   // the in-place advance's halo
                 p.halo = h->halo;
                 p.halo_wgs = h->halo_wgs;
-                p.halo_block = (uint32_t)h->flat_ip_block;
+                p.halo_block = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
                 p.halo_qtot = h->flat_qtot;
             }
             const int N = h->cfg.num_assets;
@@ -651,6 +696,8 @@ const char* pmenv_step_path(const pmenv* h) {
     if (!h->streaming) return "step_advance_lds_kernel";
     if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
     if (h->fused) return "advance_rows_kernel<fused> (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
+    if (h->flat && h->flat_inplace && h->flat_db_wg)
+        return "scalar_step_kernel+advance_flat_wg_kernel (obs_out) | scalar_step_kernel+advance_flat_inplace_kernel (in place)";
     if (h->flat && h->flat_inplace) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_flat_inplace_kernel (in place)";
     if (h->flat) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
     return "scalar_step_kernel+advance_rows_kernel";

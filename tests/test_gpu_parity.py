@@ -171,7 +171,7 @@ def test_gpu_flat_obs_out_vs_oracle_modes(monkeypatch, kw, kind):
     the oracle in every reward / ring / norm / commission mode, through the ring wrap."""
     monkeypatch.setenv("PMENV_FUSED", "0")
     from pmenv import TradingEnv
-    assert "advance_flat_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
+    assert "advance_flat_wg_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
     _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flat{kw}{kind}".encode()),
               double_buffer=True)
 
@@ -197,7 +197,7 @@ def test_gpu_flat_inplace_vs_oracle_modes(monkeypatch, kw, kind):
     (12, 10, 1),      # single env
 ])
 @pytest.mark.parametrize("knobs", ["", "PMENV_STREAM_POL=0", "PMENV_STREAM_POL=2+PMENV_FLAT_BLOCK=128",
-                                   "PMENV_FLAT_BLOCK=256"])
+                                   "PMENV_FLAT_BLOCK=256", "PMENV_FLAT_DB_WG=1", "PMENV_FLAT_DB_WG=0"])
 def test_gpu_flat_obs_out_shapes(monkeypatch, N, W, B, knobs):
     monkeypatch.setenv("PMENV_FUSED", "0")
     for kv in filter(None, knobs.split("+")):
@@ -208,7 +208,8 @@ def test_gpu_flat_obs_out_shapes(monkeypatch, N, W, B, knobs):
 
 @pytest.mark.parametrize("N,W,B", [(30, 50, 37), (5, 4, 13), (4, 2, 7), (1, 4, 9), (64, 16, 3), (129, 50, 2),
                                    (12, 10, 1), (30, 50, 600)])
-@pytest.mark.parametrize("knobs", ["", "PMENV_FLAT_IP_BLOCK=256", "PMENV_FLAT_IP_BLOCK=1024+PMENV_STREAM_POL=0"])
+@pytest.mark.parametrize("knobs", ["", "PMENV_FLAT_IP_BLOCK=256", "PMENV_FLAT_IP_BLOCK=1024+PMENV_STREAM_POL=0",
+                                   "PMENV_FLAT_IP_VEC=1", "PMENV_FLAT_IP_BLOCK=256+PMENV_FLAT_IP_VEC=4"])
 def test_gpu_flat_inplace_shapes(monkeypatch, N, W, B, knobs):
     """Workgroup seams (the halo) at every alignment against rows, envs and the
     tensor's end; (30, 50, 600): hundreds of workgroups, each seam's halo exercised."""

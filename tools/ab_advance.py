@@ -30,7 +30,7 @@ act = synth.actions(a.H, B, N, device=dev)
 envs = {}
 KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED", "PMENV_K1_GROUPS",
          "PMENV_STREAM_BLOCK", "PMENV_STREAM_POL", "PMENV_FLAT", "PMENV_FLAT_BLOCK",
-         "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK")
+         "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK", "PMENV_FLAT_IP_VEC", "PMENV_FLAT_DB_WG")
 for v in a.variants.split(","):
     # "base+KNOB=val+...": extra env knobs at creation (e.g. "o+PMENV_FUSED=0")
     base, *extra = v.split("+")

@@ -43,6 +43,7 @@ for k in sorted(set(fetch) | set(write)):
     res["kernels"][k] = {"fetch_size_kib_raw": fetch.get(k), "write_size_kib": write.get(k),
                          "hbm_read_bytes_corrected": fb, "hbm_write_bytes": wb, "hbm_bytes": fb + wb}
 main = [k for k in res["kernels"] if "advance_flat_inplace_kernel" in k] or \
+       [k for k in res["kernels"] if "advance_flat_wg_kernel" in k] or \
        [k for k in res["kernels"] if "advance_flat_kernel" in k] or \
        [k for k in res["kernels"] if "advance_rows_kernel" in k and "false" in k] or \
        [k for k in res["kernels"] if "advance_rows_kernel" in k]
