@@ -691,6 +691,7 @@ typedef int i2v_t __attribute__((ext_vector_type(2)));
 
 struct WaveSide {
     bool ok;           // the wave's rows fit one 4-row scalar window
+    bool bar_nan;      // resident series: the env's day is outside the series
     uint32_t g0, b0;   // first row of the window, first env of the wave
     i16v_t bar16;
     i4v_t w4;
@@ -708,11 +709,24 @@ __device__ __forceinline__ WaveSide wave_side_load(const StepParams& p, uint32_t
     const uint32_t gb = bb * (uint32_t)N + fdiv(4u * (qb - bb * per4), p.div_wf);
     const uint32_t rows = (uint32_t)p.B * (uint32_t)N;
     WaveSide ws;
-    ws.ok = !p.day && gb - ga <= 3u && N >= 4 && rows >= 4u;
+    // resident-series mode: the wave must sit in one env (its bar rows are that env's
+    // rows of the day's series block); the day index is one more scalar round trip
+    ws.ok = gb - ga <= 3u && N >= 4 && rows >= 4u && (!p.day || ba == bb);
+    ws.bar_nan = false;
     if (!ws.ok) return ws;
     ws.g0 = __builtin_amdgcn_readfirstlane(min(ga, rows - 4u));
     ws.b0 = __builtin_amdgcn_readfirstlane(ba);
     const float* bar_p = p.bar + (size_t)ws.g0 * 4;
+    if (p.day) {
+        ws.g0 = __builtin_amdgcn_readfirstlane(ws.b0 * (uint32_t)N + min(ga - ws.b0 * (uint32_t)N, (uint32_t)N - 4u));
+        int32_t d;
+        const int32_t* d_p = p.day + ws.b0;
+        asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(d) : "s"(d_p) : "memory");
+        ws.bar_nan = d < 0 || d >= p.series_days;
+        // an out-of-range day loads the series' first rows instead (never used: NaN bar)
+        const uint32_t drow = ws.bar_nan ? 0u : (uint32_t)d * (uint32_t)N + (ws.g0 - ws.b0 * (uint32_t)N);
+        bar_p = p.bar + (size_t)__builtin_amdgcn_readfirstlane(drow) * 4;
+    }
     const float* w_p = p.w_new + ws.g0;
     const int32_t* k_p = p.k + ws.b0;
     asm volatile(
@@ -745,7 +759,7 @@ __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, con
         const int lo = (r1 & m1) | (r0 & ~m1), hi = (r3 & m1) | (r2 & ~m1);
         return (hi & m2) | (lo & ~m2);
     };
-    sd.bar_nan = false;
+    sd.bar_nan = ws.bar_nan;
     sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f}
                        : f4{__int_as_float(sel(ws.bar16[0], ws.bar16[4], ws.bar16[8], ws.bar16[12])),
                             __int_as_float(sel(ws.bar16[1], ws.bar16[5], ws.bar16[9], ws.bar16[13])),

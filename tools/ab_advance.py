@@ -21,6 +21,7 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--H", type=int, default=64)
 ap.add_argument("--phases", type=int, default=0, help="pmenv_step_args.phases (1: scalar step only)")
+ap.add_argument("--series-days", type=int, default=512, help="resident series length for '+DAY' variants")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 B, N, W = a.envs, a.assets, a.window
@@ -28,6 +29,10 @@ lib = _abi.load()
 ser = synth.series(a.H + W, B, N, device=dev)
 act = synth.actions(a.H, B, N, device=dev)
 envs = {}
+# '+DAY' variants: resident-series mode, one shared [T, N, 4] series and a per-env day index
+res_ser = synth.series(a.series_days, 1, N, device=dev)[:, 0].contiguous()
+day0 = torch.randint(W, a.series_days - a.H, (B,), generator=torch.Generator().manual_seed(3)).to(dev, torch.int32)
+days = [day0 + t for t in range(a.H)]
 KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED", "PMENV_K1_GROUPS",
          "PMENV_STREAM_BLOCK", "PMENV_STREAM_POL", "PMENV_FLAT", "PMENV_FLAT_BLOCK",
          "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK", "PMENV_FLAT_IP_VEC", "PMENV_FLAT_DB_WG")
@@ -39,7 +44,8 @@ for v in a.variants.split(","):
     for knob in KNOBS:
         os.environ.pop(knob, None)
     for kv in extra:
-        os.environ[kv.split("=")[0]] = kv.split("=")[1]
+        if "=" in kv:
+            os.environ[kv.split("=")[0]] = kv.split("=")[1]
     import re
     m = re.fullmatch(r"(?:u(\d+))?(?:a(\d+))?o?", base)
     if base in ("stream", "o", "so"):
@@ -73,6 +79,8 @@ for r in range(a.rounds):
             args = _abi.PmenvStepArgs()
             args.action = act[t].data_ptr()
             args.bar = ser[W + t].data_ptr()
+            if "DAY" in v.split("+"):
+                args.bar, args.day, args.series_days = res_ser.data_ptr(), days[t].data_ptr(), a.series_days
             src, dst = (obs, obs2) if (obs2 is not None and t_global[v] % 2) else (obs2, obs) if obs2 is not None else (obs, None)
             args.obs = src.data_ptr()
             args.obs_out = dst.data_ptr() if dst is not None else None
@@ -89,8 +97,8 @@ ref = None
 for v, (e, obs, rew, obs2) in envs.items():
     if obs2 is not None and t_global[v] % 2:
         obs = obs2                    # latest window of a double-buffered run
-    if "a" in v.split("+")[0] and v != "lds":
-        continue                      # ablation builds compute wrong windows by design
+    if ("a" in v.split("+")[0] and v != "lds") or "DAY" in v.split("+"):
+        continue                      # ablation builds compute wrong windows by design; DAY reads other bars
     if ref is None:
         ref = (obs, rew, e.value)
     else:
