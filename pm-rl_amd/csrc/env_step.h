@@ -691,9 +691,11 @@ typedef int i2v_t __attribute__((ext_vector_type(2)));
 
 struct WaveSide {
     bool ok;           // the wave's rows fit one 4-row scalar window
-    bool bar_nan;      // resident series: the env's day is outside the series
+    bool two;          // resident series: the wave spans two envs (two days, two bar windows)
+    bool nan_a, nan_b; // resident series: the env's day is outside the series
     uint32_t g0, b0;   // first row of the window, first env of the wave
-    i16v_t bar16;
+    uint32_t ca;       // resident series: first asset row of env b0's bar window
+    i16v_t bar16, bar16b;
     i4v_t w4;
     i2v_t k2;
 };
@@ -709,23 +711,51 @@ __device__ __forceinline__ WaveSide wave_side_load(const StepParams& p, uint32_t
     const uint32_t gb = bb * (uint32_t)N + fdiv(4u * (qb - bb * per4), p.div_wf);
     const uint32_t rows = (uint32_t)p.B * (uint32_t)N;
     WaveSide ws;
-    // resident-series mode: the wave must sit in one env (its bar rows are that env's
-    // rows of the day's series block); the day index is one more scalar round trip
-    ws.ok = gb - ga <= 3u && N >= 4 && rows >= 4u && (!p.day || ba == bb);
-    ws.bar_nan = false;
+    ws.ok = gb - ga <= 3u && N >= 4 && rows >= 4u;
+    ws.two = false;
+    ws.nan_a = ws.nan_b = false;
     if (!ws.ok) return ws;
     ws.g0 = __builtin_amdgcn_readfirstlane(min(ga, rows - 4u));
     ws.b0 = __builtin_amdgcn_readfirstlane(ba);
     const float* bar_p = p.bar + (size_t)ws.g0 * 4;
     if (p.day) {
-        ws.g0 = __builtin_amdgcn_readfirstlane(ws.b0 * (uint32_t)N + min(ga - ws.b0 * (uint32_t)N, (uint32_t)N - 4u));
-        int32_t d;
+        // resident series: the bar rows are env b's asset rows of the series block of
+        // day[b]. Env b0's window is asset rows ca .. ca+3; a wave that runs into env
+        // b0+1 (at most 3 rows further: its rows there are 0 .. 2) takes that env's
+        // rows 0 .. 3 of its own day as a second window. Out-of-range days load row 0
+        // (never used: NaN bar).
+        ws.two = bb != ba;
+        ws.ca = __builtin_amdgcn_readfirstlane(min(ga - ws.b0 * (uint32_t)N, (uint32_t)N - 4u));
         const int32_t* d_p = p.day + ws.b0;
-        asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(d) : "s"(d_p) : "memory");
-        ws.bar_nan = d < 0 || d >= p.series_days;
-        // an out-of-range day loads the series' first rows instead (never used: NaN bar)
-        const uint32_t drow = ws.bar_nan ? 0u : (uint32_t)d * (uint32_t)N + (ws.g0 - ws.b0 * (uint32_t)N);
-        bar_p = p.bar + (size_t)__builtin_amdgcn_readfirstlane(drow) * 4;
+        int32_t d0, d1 = 0;
+        if (ws.two) {
+            i2v_t dd;
+            asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(dd) : "s"(d_p) : "memory");
+            d0 = dd[0];
+            d1 = dd[1];
+        } else {
+            asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(d0) : "s"(d_p) : "memory");
+        }
+        ws.nan_a = d0 < 0 || d0 >= p.series_days;
+        ws.nan_b = d1 < 0 || d1 >= p.series_days;
+        const uint32_t ra = ws.nan_a ? 0u : (uint32_t)d0 * (uint32_t)N + ws.ca;
+        bar_p = p.bar + (size_t)__builtin_amdgcn_readfirstlane(ra) * 4;
+        // the second window is fetched in the same scalar batch (env b0's again when
+        // the wave stays in one env)
+        const uint32_t rb = ws.two && !ws.nan_b ? (uint32_t)d1 * (uint32_t)N : ra;
+        const float* bar_b = p.bar + (size_t)__builtin_amdgcn_readfirstlane(rb) * 4;
+        const float* w_p = p.w_new + ws.g0;
+        const int32_t* k_p = p.k + ws.b0;
+        asm volatile(
+            "s_load_dwordx16 %0, %4, 0x0\n\t"
+            "s_load_dwordx16 %1, %5, 0x0\n\t"
+            "s_load_dwordx4 %2, %6, 0x0\n\t"
+            "s_load_dwordx2 %3, %7, 0x0\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(ws.bar16), "=&s"(ws.bar16b), "=&s"(ws.w4), "=&s"(ws.k2)
+            : "s"(bar_p), "s"(bar_b), "s"(w_p), "s"(k_p)
+            : "memory");
+        return ws;
     }
     const float* w_p = p.w_new + ws.g0;
     const int32_t* k_p = p.k + ws.b0;
@@ -740,6 +770,19 @@ __device__ __forceinline__ WaveSide wave_side_load(const StepParams& p, uint32_t
     return ws;
 }
 
+// two-level selects on the bits of i (0..3) with constant SGPR indices (a runtime index
+// into the SGPR tuple lowers to a 16-way compare chain per value)
+__device__ __forceinline__ int sel4(int i, int r0, int r1, int r2, int r3) {
+    const int m1 = -(i & 1), m2 = -((i >> 1) & 1);
+    const int lo = (r1 & m1) | (r0 & ~m1), hi = (r3 & m1) | (r2 & ~m1);
+    return (hi & m2) | (lo & ~m2);
+}
+
+__device__ __forceinline__ f4 sel_bar(int i, const i16v_t& r) {
+    return f4{__int_as_float(sel4(i, r[0], r[4], r[8], r[12])), __int_as_float(sel4(i, r[1], r[5], r[9], r[13])),
+              __int_as_float(sel4(i, r[2], r[6], r[10], r[14])), __int_as_float(sel4(i, r[3], r[7], r[11], r[15]))};
+}
+
 template <int SKIP = 0>
 __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, const WaveSide& ws, uint32_t q) {
     if (!ws.ok) return flat_side_load<SKIP>(p, q);
@@ -752,21 +795,27 @@ __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, con
     const uint32_t row = fdiv(j0, p.div_wf);
     sd.kk = (int)(j0 - row * (uint32_t)WF);
     const int i = (int)(b * (uint32_t)N + row - ws.g0);               // 0 .. 3
-    // two-level selects on the bits of i with constant SGPR indices (a runtime index
-    // into the SGPR tuple lowers to a 16-way compare chain per value)
-    const int m1 = -(i & 1), m2 = -((i >> 1) & 1);
-    auto sel = [&](int r0, int r1, int r2, int r3) {
-        const int lo = (r1 & m1) | (r0 & ~m1), hi = (r3 & m1) | (r2 & ~m1);
-        return (hi & m2) | (lo & ~m2);
-    };
-    sd.bar_nan = ws.bar_nan;
-    sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f}
-                       : f4{__int_as_float(sel(ws.bar16[0], ws.bar16[4], ws.bar16[8], ws.bar16[12])),
-                            __int_as_float(sel(ws.bar16[1], ws.bar16[5], ws.bar16[9], ws.bar16[13])),
-                            __int_as_float(sel(ws.bar16[2], ws.bar16[6], ws.bar16[10], ws.bar16[14])),
-                            __int_as_float(sel(ws.bar16[3], ws.bar16[7], ws.bar16[11], ws.bar16[15]))};
-    sd.xwp = (SKIP & 2) ? 0.5f : __int_as_float(sel(ws.w4[0], ws.w4[1], ws.w4[2], ws.w4[3]));
-    const int mk = -(int)(b != ws.b0);
+    const bool in_b = b != ws.b0;
+    if (p.day) {                                                       // kernel argument: uniform
+        const int ib = in_b ? (int)row : (int)(row - ws.ca);            // 0 .. 3 in the env's window
+        sd.bar_nan = in_b ? ws.nan_b : ws.nan_a;
+        if (!(SKIP & 1)) {
+            const f4 xa = sel_bar(ib, ws.bar16);
+            sd.xb = xa;
+            if (ws.two) {
+                const f4 xb2 = sel_bar(ib, ws.bar16b);
+                sd.xb = f4{pick(in_b, xb2.x, xa.x), pick(in_b, xb2.y, xa.y), pick(in_b, xb2.z, xa.z),
+                           pick(in_b, xb2.w, xa.w)};
+            }
+        } else {
+            sd.xb = f4{1.f, 1.f, 1.f, 1.f};
+        }
+    } else {
+        sd.bar_nan = false;
+        sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f} : sel_bar(i, ws.bar16);
+    }
+    sd.xwp = (SKIP & 2) ? 0.5f : __int_as_float(sel4(i, ws.w4[0], ws.w4[1], ws.w4[2], ws.w4[3]));
+    const int mk = -(int)in_b;
     sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - 1;   // scalar_step_kernel counted this step
     return sd;
 }
