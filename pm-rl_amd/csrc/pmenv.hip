@@ -16,6 +16,7 @@
 #include "common.h"
 #include "data.h"
 #include "env_step.h"
+#include "scalar_vec.h"
 #include "rollout.h"
 #include "replay.h"
 #include "trainer.h"
@@ -56,6 +57,7 @@ struct pmenv {
     uint32_t halo_wgs, flat_qtot;
     int scalar_scratch_floats;
     int k1_groups;        // env groups per wave in scalar_step_reg_kernel
+    int k1_vec;           // scalar_step_vec_kernel shape 100 * L + A (0: register / LDS form)
     int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
     int ablate;           // PMENV_ABLATE timing-only variants of advance_rows_kernel (0 = product)
     size_t lds_scalar, lds_stream;
@@ -244,6 +246,66 @@ void launch_scalar_reg_l(int groups, const StepParams& p, hipStream_t stream) {
 void launch_scalar_reg(const pmenv* h, const StepParams& p, hipStream_t stream) {
     if (p.N <= 32) launch_scalar_reg_l<32>(h->k1_groups, p, stream);
     else launch_scalar_reg_l<64>(h->k1_groups, p, stream);
+}
+
+// K1 packed form (scalar_vec.h): L lanes x A assets per env, consecutive or strided
+// (STR); h->k1_vec = 100 * L + A (+ kK1Str for the strided layout)
+constexpr int kK1Str = 100000;
+
+template <int L, int A, bool STR>
+void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
+    const unsigned waves = (unsigned)((p.B + 64 / L - 1) / (64 / L));
+    scalar_step_vec_kernel<L, A, STR><<<(waves + 3) / 4, 256, 0, stream>>>(p);
+}
+
+constexpr int kK1Vec[] = {801, 802, 804, 1601, 1602, 1604, 1608, 3202, 3204,
+                          kK1Str + 3202, kK1Str + 3204, kK1Str + 6402, kK1Str + 6404, kK1Str + 6408};
+
+bool launch_scalar_vec(int vec, const StepParams& p, hipStream_t stream) {
+    switch (vec) {
+    case 801: launch_scalar_vec_la<8, 1, false>(p, stream); return true;
+    case 802: launch_scalar_vec_la<8, 2, false>(p, stream); return true;
+    case 804: launch_scalar_vec_la<8, 4, false>(p, stream); return true;
+    case 1601: launch_scalar_vec_la<16, 1, false>(p, stream); return true;
+    case 1602: launch_scalar_vec_la<16, 2, false>(p, stream); return true;
+    case 1604: launch_scalar_vec_la<16, 4, false>(p, stream); return true;
+    case 1608: launch_scalar_vec_la<16, 8, false>(p, stream); return true;
+    case 3202: launch_scalar_vec_la<32, 2, false>(p, stream); return true;
+    case 3204: launch_scalar_vec_la<32, 4, false>(p, stream); return true;
+    case kK1Str + 3202: launch_scalar_vec_la<32, 2, true>(p, stream); return true;
+    case kK1Str + 3204: launch_scalar_vec_la<32, 4, true>(p, stream); return true;
+    case kK1Str + 6402: launch_scalar_vec_la<64, 2, true>(p, stream); return true;
+    case kK1Str + 6404: launch_scalar_vec_la<64, 4, true>(p, stream); return true;
+    case kK1Str + 6408: launch_scalar_vec_la<64, 8, true>(p, stream); return true;
+    default: return false;
+    }
+}
+
+// K1 shape per asset count, or the PMENV_K1 knob ("reg" | "LxA" | "LxAs" strided,
+// e.g. "16x2", "64x8s"; an unbuilt or too-small shape keeps the default). 0: the
+// register form (N <= 64) or the LDS form (N > 512).
+int pick_k1_vec(const pmenv_cfg& c) {
+    const int N = c.num_assets;
+    if ((int64_t)c.num_envs * N * 4 >= (1ll << 32)) return 0;     // descriptors span the [B*N] arrays
+    int v = 0;
+    if (N <= 8) v = 801;
+    else if (N <= 16) v = 802;
+    else if (N <= 32) v = 1602;
+    else if (N <= 64) v = 1604;
+    else if (N <= 128) v = kK1Str + 6402;
+    else if (N <= 256) v = kK1Str + 6404;
+    else if (N <= 512) v = kK1Str + 6408;
+    if (const char* knob = getenv("PMENV_K1")) {
+        int L = 0, A = 0;
+        char s = 0;
+        if (!strcmp(knob, "reg")) return 0;
+        if (sscanf(knob, "%dx%d%c", &L, &A, &s) >= 2) {
+            const int want = 100 * L + A + (s == 's' ? kK1Str : 0);
+            for (int k : kK1Vec)
+                if (k == want && L * A >= N) return k;
+        }
+    }
+    return v;
 }
 
 // one launch per step: whole-env units (the double-buffered geometry), scalar step
@@ -490,6 +552,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->k1_groups = 1;
     if (const char* knob = getenv("PMENV_K1_GROUPS")) h->k1_groups = atoi(knob);   // A/B knob: 1 | 2 | 4
     if (h->k1_groups != 2 && h->k1_groups != 4) h->k1_groups = 1;
+    h->k1_vec = pick_k1_vec(c);
     if (h->streaming) {
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
         h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
@@ -655,7 +718,9 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
                 p.halo_qtot = h->flat_qtot;
             }
             const int N = h->cfg.num_assets;
-            if (N <= 64) {
+            if (h->k1_vec && launch_scalar_vec(h->k1_vec, p, stream)) {
+                // packed form
+            } else if (N <= 64) {
                 launch_scalar_reg(h, p, stream);
             } else {
                 scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar,

@@ -1,0 +1,274 @@
+// scalar_vec.h — the per-env scalar step (K1) in packed form, for the two-launch
+// advance path (included by pmenv.hip after env_step.h).
+//
+// L lanes per env and A assets per lane (L*A >= N): 64/L envs per wave, so a wave
+// carries A times the envs of the one-asset-per-lane form. Lane j holds the
+// consecutive assets j*A .. j*A+A-1 (one dwordx{A} per array: small N), or — STR —
+// the strided assets j, j+L, .. (each dword instruction a coalesced run: large N).
+// Reductions: the lane's A values in order, then an all-lane butterfly inside the
+// group — DPP quad_perm xor 1 / xor 2, row_half_mirror (8 lanes), row_mirror (16) —
+// whose every level combines a value with its partner's in commutative pairs, so all
+// L lanes hold bitwise the same total and every branch on it is group-uniform;
+// L = 32 / 64 use the row-shift + readlane form of the register kernel.
+//
+// Reference semantics (zachramsey/pm-rl), as scalar_finish in env_step.h:
+//   env/sim/trading_env.py:54-100 normalisation, commission mu, value, return, reward
+//   env/sim/weight_buffer.py:13-30 ring update / get_last
+//   env/reward.py:20-31 returns / sharpe_ratio;  data/instrument.py:79 price relatives
+#pragma once
+#include "env_step.h"
+
+namespace pmenv_dev {
+
+constexpr int kHalfMirror = 0x141, kRowMirror = 0x140;
+
+// L-lane group reduction, bitwise the same in every lane of the group
+template <int L, int OP>   // OP 0 sum, 1 max, 2 min
+__device__ __forceinline__ double gred(double v, int lane) {
+    if constexpr (L >= 32) {
+        return OP == 0 ? group_sum<L>(v, lane) : OP == 1 ? group_max<L>(v, lane) : group_min<L>(v, lane);
+    } else {
+        auto op = [](double a, double b) { return OP == 0 ? a + b : OP == 1 ? fmax(a, b) : fmin(a, b); };
+        v = op(v, dpp_shift<kQuadXor1>(v, 0.0));
+        v = op(v, dpp_shift<kQuadXor2>(v, 0.0));
+        if (L >= 8) v = op(v, dpp_shift<kHalfMirror>(v, 0.0));
+        if (L >= 16) v = op(v, dpp_shift<kRowMirror>(v, 0.0));
+        return v;
+    }
+}
+
+// A floats of a [B*N] array for lane j of an env row starting at element `row`: the
+// consecutive elements j*A .. j*A+A-1 (one dwordx{A}), or — STR — the strided
+// elements j, j+L, .. (A dword loads, each a coalesced run across the group's lanes).
+// Past the array's end the buffer descriptor reads 0 (never a fault); lanes mask
+// what is not theirs.
+template <int L, int A, bool STR>
+__device__ __forceinline__ void load_packed(const float* base, uint32_t bytes, size_t row, int j, float (&x)[A]) {
+    const auto r = make_rsrc(base, bytes);
+    if constexpr (STR || A == 1) {
+#pragma unroll
+        for (int e = 0; e < A; ++e) x[e] = buf_load1(r, (uint32_t)(row + j + e * L) * 4u);
+    } else if constexpr (A == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(row + j * A) * 4u, 0, 0);
+        x[0] = __uint_as_float(v[0]);
+        x[1] = __uint_as_float(v[1]);
+    } else {
+        const uint32_t off = (uint32_t)(row + j * A) * 4u;
+#pragma unroll
+        for (int h = 0; h < A / 4; ++h) {
+            const f4 v = buf_load4<0>(r, off + 16u * h);
+            x[4 * h] = v.x; x[4 * h + 1] = v.y; x[4 * h + 2] = v.z; x[4 * h + 3] = v.w;
+        }
+    }
+}
+
+// The in-place flat advance's halo (copy_halo in env_step.h) in two halves: the
+// loads go out with the step's own loads, the stores after its compute, so the copy
+// costs the wave no extra memory round trip. Items past two per thread (grids
+// smaller than half the halo) take the plain loop at the end.
+struct HaloRegs {
+    f4 v[4];
+    bool d0, d1;
+};
+
+__device__ __forceinline__ HaloRegs halo_load(const StepParams& p) {
+    HaloRegs h;
+    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
+    h.d0 = p.halo && gid < p.halo_wgs;
+    h.d1 = p.halo && gid + nthr < p.halo_wgs;
+    const f4* src = reinterpret_cast<const f4*>(p.obs);
+    const f4 z = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const bool d = t ? h.d1 : h.d0;
+        const uint32_t q = (gid + t * nthr + 1) * p.halo_block;
+        h.v[2 * t] = d && q < p.halo_qtot ? src[q] : z;
+        h.v[2 * t + 1] = d && q + 1 < p.halo_qtot ? src[q + 1] : z;
+    }
+    return h;
+}
+
+__device__ __forceinline__ void halo_store(const StepParams& p, const HaloRegs& h) {
+    if (!p.halo) return;
+    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
+    f4* dst = reinterpret_cast<f4*>(p.halo);
+    if (h.d0) { dst[2 * gid] = h.v[0]; dst[2 * gid + 1] = h.v[1]; }
+    if (h.d1) { dst[2 * (gid + nthr)] = h.v[2]; dst[2 * (gid + nthr) + 1] = h.v[3]; }
+    const f4* src = reinterpret_cast<const f4*>(p.obs);
+    for (uint32_t i = gid + 2 * nthr; i < p.halo_wgs; i += nthr) {
+        const uint32_t q = (i + 1) * p.halo_block;
+        dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
+        dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+template <int L, int A, bool STR>
+__global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
+    const HaloRegs halo = halo_load(p);
+    constexpr int EPW = 64 / L;
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int b = w * EPW + lane / L;
+    const int j = lane % L;
+    const int N = p.N, W = p.W, Fm = p.F - 1;
+    const bool env_ok = b < p.B;
+    const int bc = env_ok ? b : 0;
+    const size_t row = (size_t)bc * N;
+    const uint32_t nbytes = (uint32_t)p.B * (uint32_t)N * 4u;
+    int nn[A];                                    // the lane's assets
+    bool act[A];
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        nn[e] = STR ? j + e * L : j * A + e;
+        act[e] = env_ok && nn[e] < N;
+    }
+
+    // every load first, none dependent on another (the bar rows of a resident series
+    // follow the env's day index)
+    const int32_t k = p.k[bc];
+    const double v_prev = p.value[bc];
+    const double sa = p.sa[bc], sb = p.sb[bc];
+    float a[A], wl[A], pl[A], cn[A];
+    load_packed<L, A, STR>(p.action, nbytes, row, j, a);
+    load_packed<L, A, STR>(p.w_new, nbytes, row, j, wl);                  // get_last() (weight_buffer.py:28-30)
+    load_packed<L, A, STR>(p.prices ? p.prices : p.last_close, nbytes, row, j, pl);
+    const float* barb = p.bar ? env_bar(p, bc) : nullptr;
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        const int nc = act[e] ? nn[e] : 0;
+        cn[e] = barb ? barb[(size_t)nc * Fm + p.close_ch] : NAN;
+    }
+
+    // instrument.py:79: the relative is the correctly rounded fp32 quotient of today's
+    // close over the window's last close (caller prices when given)
+    double x[A], y[A];
+    double s_loc = 0.0, mn_loc = INFINITY;
+    bool nan_here = false;
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        x[e] = act[e] ? (double)a[e] : 0.0;
+        y[e] = !act[e] ? 1.0 : (p.bar && !p.prices) ? (double)(cn[e] / pl[e]) : (double)pl[e];
+        s_loc += x[e];
+        mn_loc = fmin(mn_loc, act[e] ? x[e] : INFINITY);
+        nan_here |= act[e] && isnan(a[e]);
+    }
+    // trading_env.py:58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min < 0
+    const double sum = gred<L, 0>(s_loc, lane);
+    double mn = gred<L, 2>(mn_loc, lane);
+    const uint64_t gmask = L == 64 ? ~0ull : (((1ull << (L & 63)) - 1ull) << (lane & ~(L - 1)));
+    if (__ballot(nan_here) & gmask) mn = NAN;     // torch.min propagates NaN
+    const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
+    const bool negative = mn < 0.0;
+    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    double wv[A];
+#pragma unroll
+    for (int e = 0; e < A; ++e) wv[e] = x[e];
+    if (__any(norm)) {
+        double shift = 0.0;
+        if (p.norm_mode == PMENV_NORM_OR) {       // torch.softmax is max-shifted
+            double m = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < A; ++e) m = fmax(m, act[e] ? x[e] : -INFINITY);
+            shift = gred<L, 1>(m, lane);
+        }
+        double ex[A], z_loc = 0.0;
+#pragma unroll
+        for (int e = 0; e < A; ++e) {
+            ex[e] = act[e] ? exp(x[e] - shift) : 0.0;   // :59 (no max-shift in AND mode)
+            z_loc += ex[e];
+        }
+        const double z = gred<L, 0>(z_loc, lane);
+        if (norm) {
+#pragma unroll
+            for (int e = 0; e < A; ++e) wv[e] = ex[e] / z;   // :60
+        }
+    }
+
+    // :67-75 commission fixed point (f64, capped), per env group
+    double V = v_prev;
+    if (p.commission > 0.0) {
+        const double c = p.commission;
+        const int g0 = lane & ~(L - 1);
+        const double w0 = __shfl(wv[0], g0, 64);
+        const double wl0 = (double)__shfl(wl[0], g0, 64);
+        double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
+        int it = 0;
+        bool done = !(fabs(mu - mu_last) > p.mu_tol) || p.mu_max_iter <= 0;
+        while (__any(!done)) {
+            double part = 0.0;
+#pragma unroll
+            for (int e = 0; e < A; ++e) {
+                const double d = (act[e] && nn[e] > 0) ? (double)wl[e] - mu * wv[e] : 0.0;
+                part += d > 0.0 ? d : 0.0;        // torch.maximum(x, 0) as intended
+            }
+            const double tot = gred<L, 0>(part, lane);
+            if (!done) {
+                mu_last = mu;
+                mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
+                ++it;
+                done = !(fabs(mu - mu_last) > p.mu_tol) || it >= p.mu_max_iter;
+            }
+        }
+        V = mu * V;
+    }
+
+    // :78-79 portfolio value; :83-84 w' = portfolio / value -> ring slot (1 + k) % W
+    double pv[A], pv_loc = 0.0;
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        pv[e] = act[e] ? V * (wv[e] * y[e]) : 0.0;
+        pv_loc += pv[e];
+    }
+    const double value = gred<L, 0>(pv_loc, lane);
+    const int slot = (int)((1 + (int64_t)k) % W);
+    float* ring_row = p.ring + (size_t)bc * W * N + (size_t)slot * N;
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        if (!act[e]) continue;
+        const int n = nn[e];
+        const float wp = (float)(pv[e] / value);
+        ring_row[n] = wp;
+        p.w_new[(size_t)bc * N + n] = wp;
+        if (p.weights) p.weights[(size_t)bc * N + n] = wp;
+        if (p.bar) p.last_close[(size_t)bc * N + n] = cn[e];
+    }
+    if (env_ok && j == 0) {
+        // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
+        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
+        double r;
+        switch (p.reward_kind) {
+        case PMENV_REWARD_RETURN:
+            r = ret * p.scale;
+            break;
+        case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
+            const double m = (double)(k + 1);
+            double mean = sa, m2 = sb;
+            const double d = ret - mean;
+            mean += d / m;
+            m2 += d * (ret - mean);
+            p.sa[b] = mean;
+            p.sb[b] = m2;
+            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
+            break;
+        }
+        case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
+            const double R = ret - 1.0, Am = sa, Bm = sb;
+            const double dA = R - Am, dB = R * R - Bm, var = Bm - Am * Am;
+            r = var > 1e-12 ? (Bm * dA - 0.5 * Am * dB) / (var * sqrt(var)) * p.scale : 0.0;
+            p.sa[b] = Am + p.eta * dA;
+            p.sb[b] = Bm + p.eta * dB;
+            break;
+        }
+        default:
+            r = log(ret) * p.scale;              // :99
+        }
+        p.value[b] = value;
+        p.k[b] = k + 1;
+        if (p.reward) p.reward[b] = (float)r;
+        if (p.ret) p.ret[b] = ret;
+        if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
+    }
+    halo_store(p, halo);
+}
+
+}  // namespace pmenv_dev

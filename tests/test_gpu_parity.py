@@ -251,6 +251,30 @@ def test_gpu_flat_resident_series_obs_out(monkeypatch):
     assert bool(torch.isnan(nxt[7, :, -1, :4]).all()) and not bool(torch.isnan(nxt[6]).any())
 
 
+@pytest.mark.parametrize("k1", ["reg", "8x4", "16x2", "32x2", "32x2s", "64x2s"])
+@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+def test_gpu_k1_packed_shapes_vs_oracle_modes(monkeypatch, k1, kw):
+    """The scalar step's packed form (scalar_step_vec_kernel: L lanes x A assets per
+    env, DPP butterfly reductions) in every lane/asset split against the oracle, in
+    every reward / ring / norm / commission mode; "reg" is the one-asset-per-lane form."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    monkeypatch.setenv("PMENV_K1", k1)
+    _run_both(kw, B=67, N=30, W=50, T=56, kind="mixed", seed=zlib.crc32(f"k1{k1}{kw}".encode()))
+
+
+@pytest.mark.parametrize("N,W,B", [(1, 4, 9), (4, 6, 13), (8, 10, 21), (9, 4, 5), (16, 8, 33), (17, 4, 7),
+                                   (33, 4, 11), (64, 16, 3), (65, 4, 6), (129, 8, 5), (256, 4, 3), (300, 8, 4),
+                                   (500, 50, 4), (512, 2, 3)])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_k1_packed_asset_counts(monkeypatch, N, W, B, db):
+    """Default packed shape per asset count (partial last lane, group edges at 8 / 16 /
+    32 / 64 lanes, N up to 512) through both window modes, against the oracle."""
+    monkeypatch.setenv("PMENV_FUSED", "0")
+    _run_both({}, B=B, N=N, W=W, T=W + 5, kind="mixed", seed=N * 31 + W, double_buffer=db)
+    _run_both({"commission": 0.0025, "norm": "or"}, B=B, N=N, W=W, T=W + 2, kind="rawpos", seed=N + 7 * W,
+              double_buffer=db)
+
+
 @pytest.mark.parametrize("fused", ["0", "db", "all"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES[:1] + MODES[4:8], ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
