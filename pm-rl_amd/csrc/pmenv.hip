@@ -938,15 +938,53 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
         const size_t glds = (size_t)R * (W + 1) * F * sizeof(float);
         const dim3 grid((unsigned)S, (unsigned)(N / R));
         const int pairs = R * (W + 1);
-        if (pairs <= 2 * 256)
-            replay_gather_f5_kernel<2><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
-                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
-        else if (pairs <= 4 * 256)
-            replay_gather_f5_kernel<4><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
-                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
-        else
-            replay_gather_f5_kernel<8><<<grid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, h0,
-                                                                   env, s, s_next, a_out, r_out, R, dr, dwf);
+        // s / s' are written once per sample: nt stores, 129.6 -> 118.6 us at S = 8,192
+        // (tools/ab_replay.py, profiles/ab_r01/replay_nt_tpb_r01h.log). A/B knobs:
+        // PMENV_REPLAY_NT=0 (default-policy stores), PMENV_REPLAY_TPB=512
+        const bool nt = !(getenv("PMENV_REPLAY_NT") && atoi(getenv("PMENV_REPLAY_NT")) == 0);
+        const bool t512 = getenv("PMENV_REPLAY_TPB") && atoi(getenv("PMENV_REPLAY_TPB")) == 512;
+#define PMENV_RG(PPT, NTV, TPB)                                                                              \
+    replay_gather_f5_kernel<PPT, NTV, TPB><<<grid, TPB, glds, stream>>>(series, T, N, W, days, actions, rewards, \
+                                                                        H, B, h0, env, s, s_next, a_out, r_out, \
+                                                                        R, dr, dwf)
+        // persistent form (replay_gather_f5p_kernel) by default: one workgroup per CU
+        // loops over the samples with the next sample's loads in flight. One per CU is
+        // the measured optimum (S = 8,192: 96 us at 256 workgroups; 114-121 us at 192,
+        // 288, 512, 768, 1,280 and one workgroup per sample, 117 us;
+        // profiles/ab_r01/replay_grid_r01j.log). PMENV_REPLAY_PERSIST=0: one workgroup
+        // per sample; PMENV_REPLAY_GRID: G.
+        const bool persist = !t512 && !(getenv("PMENV_REPLAY_PERSIST") && atoi(getenv("PMENV_REPLAY_PERSIST")) == 0);
+        if (persist) {
+            static int cus = 0;
+            if (!cus) {
+                int dev = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                    cus = 256;
+            }
+            const int gy = N / R;
+            int G = cus / gy > 0 ? cus / gy : 1;
+            if (const char* knob = getenv("PMENV_REPLAY_GRID")) G = atoi(knob) > 0 ? atoi(knob) : G;
+            const dim3 pgrid((unsigned)(S < G ? S : G), (unsigned)(N / R));
+            const int ppt = pairs <= 2 * 256 ? 2 : pairs <= 4 * 256 ? 4 : 8;
+#define PMENV_RGP(PPT, NTV)                                                                                   \
+    replay_gather_f5p_kernel<PPT, NTV><<<pgrid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, \
+                                                                     h0, env, S, s, s_next, a_out, r_out, R, dr, dwf)
+            if (nt) { if (ppt == 2) PMENV_RGP(2, 2); else if (ppt == 4) PMENV_RGP(4, 2); else PMENV_RGP(8, 2); }
+            else { if (ppt == 2) PMENV_RGP(2, 0); else if (ppt == 4) PMENV_RGP(4, 0); else PMENV_RGP(8, 0); }
+#undef PMENV_RGP
+            return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        }
+        const int tpb = t512 ? 512 : 256;
+        const int ppt = pairs <= 2 * tpb ? 2 : pairs <= 4 * tpb ? 4 : 8;
+        if (t512) {
+            if (nt) { if (ppt == 2) PMENV_RG(2, 2, 512); else if (ppt == 4) PMENV_RG(4, 2, 512); else PMENV_RG(8, 2, 512); }
+            else { if (ppt == 2) PMENV_RG(2, 0, 512); else if (ppt == 4) PMENV_RG(4, 0, 512); else PMENV_RG(8, 0, 512); }
+        } else {
+            if (nt) { if (ppt == 2) PMENV_RG(2, 2, 256); else if (ppt == 4) PMENV_RG(4, 2, 256); else PMENV_RG(8, 2, 256); }
+            else { if (ppt == 2) PMENV_RG(2, 0, 256); else if (ppt == 4) PMENV_RG(4, 0, 256); else PMENV_RG(8, 0, 256); }
+        }
+#undef PMENV_RG
     } else if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
         replay_gather_lds_kernel<<<(unsigned)S, 256, lds, stream>>>(series, T, N, F, W, days, actions, rewards, H, B,
                                                                    h0, env, s, s_next, a_out, r_out);

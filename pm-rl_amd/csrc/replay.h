@@ -266,8 +266,10 @@ __global__ __launch_bounds__(256) void replay_gather_lds_kernel(const float* ser
 // dword; then the image [R][W+1][5] in LDS; then its rows of s and s' as whole
 // 16-B chunks (R*W*5 is a multiple of 4, so every group starts 16-B aligned).
 // Index divisions by R and W*F are multiply-high.
-template <int PPT>
-__global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* series, int T, int N, int W,
+// NT: cache policy of the s / s' stores (written once, read by the learner later:
+// 0 default, 2 nt); TPB threads per workgroup.
+template <int PPT, int NT = 0, int TPB = 256>
+__global__ __launch_bounds__(TPB) void replay_gather_f5_kernel(const float* series, int T, int N, int W,
                                                                const int32_t* days, const float* actions,
                                                                const float* rewards, int H, int B,
                                                                const int32_t* h0, const int32_t* env, float* s,
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* seri
     float ac[PPT];
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-        const int it = min(tid + k * 256, P - 1);
+        const int it = min(tid + k * TPB, P - 1);
         const int t = (int)fdiv((uint32_t)it, div_r), n = n0 + it - t * R;
         int h = hj + t;
         h = h >= H ? h - H : h;
@@ -297,17 +299,17 @@ __global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* seri
     const auto rs_ser = make_rsrc(series, (uint32_t)T * (uint32_t)N * 16u);
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-        const int it = min(tid + k * 256, P - 1);
+        const int it = min(tid + k * TPB, P - 1);
         const int t = (int)fdiv((uint32_t)it, div_r), n = n0 + it - t * R;
         const int d = d0 + t;
-        const bool in = tid + k * 256 < P && d >= 0 && d < T;   // days off the series read NaN below
+        const bool in = tid + k * TPB < P && d >= 0 && d < T;   // days off the series read NaN below
         mk[k] = buf_load4(rs_ser, in ? ((uint32_t)d * (uint32_t)N + (uint32_t)n) * 16u : 0xFFFFFFF0u);
     }
     if (tid < R) a_out[(size_t)j * N + n0 + tid] = actions[((size_t)((hj + W) % H) * B + b) * N + n0 + tid];
     if (tid == 0 && blockIdx.y == 0) r_out[j] = rewards[(size_t)((hj + W - 1) % H) * B + b];
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-        const int it = tid + k * 256;
+        const int it = tid + k * TPB;
         if (it < P) {
             const int t = (int)fdiv((uint32_t)it, div_r), nl = it - t * R;
             const int d = d0 + t;
@@ -324,7 +326,8 @@ __global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* seri
     const int WF = W * F, per = R * WF;
     float* so = s + (size_t)j * N * WF + (size_t)n0 * WF;
     float* sn = s_next + (size_t)j * N * WF + (size_t)n0 * WF;
-    for (int q = tid; q < per / 4; q += 256) {
+    const auto rso = make_rsrc(so, (uint32_t)per * 4u), rsn = make_rsrc(sn, (uint32_t)per * 4u);
+    for (int q = tid; q < per / 4; q += TPB) {
         float v0[4], v1[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -334,8 +337,109 @@ __global__ __launch_bounds__(256) void replay_gather_f5_kernel(const float* seri
             v0[k] = x[0];
             v1[k] = x[F];
         }
-        reinterpret_cast<f4*>(so)[q] = f4{v0[0], v0[1], v0[2], v0[3]};
-        reinterpret_cast<f4*>(sn)[q] = f4{v1[0], v1[1], v1[2], v1[3]};
+        buf_store4<NT>(rso, (uint32_t)q * 16u, f4{v0[0], v0[1], v0[2], v0[3]});
+        buf_store4<NT>(rsn, (uint32_t)q * 16u, f4{v1[0], v1[1], v1[2], v1[3]});
+    }
+}
+
+
+// The F = 5 gather as a persistent loop: workgroup g takes samples g, g + G, g + 2G, ..
+// and keeps the pipeline full across them — the next sample's staging loads go out
+// (into the same registers, once the current image is in LDS) before the current
+// sample's write-out, and its index chain (env / h0, then the day) is fetched two and
+// one samples ahead — so a sample costs its write-out, not three dependent memory
+// round trips plus the write-out. Same image and write-out as replay_gather_f5_kernel.
+template <int PPT, int NT>
+__global__ __launch_bounds__(256) void replay_gather_f5p_kernel(const float* series, int T, int N, int W,
+                                                                const int32_t* days, const float* actions,
+                                                                const float* rewards, int H, int B,
+                                                                const int32_t* h0, const int32_t* env, int S, float* s,
+                                                                float* s_next, float* a_out, float* r_out, int R,
+                                                                FastDiv div_r, FastDiv div_wf) {
+    constexpr int F = 5;
+    extern __shared__ __attribute__((aligned(16))) float ext[];
+    const int tid = threadIdx.x;
+    const int n0 = blockIdx.y * R;
+    const int W1 = W + 1, P = R * W1, WF = W * F, per = R * WF;
+    const int G = gridDim.x;
+    int j = blockIdx.x;
+    if (j >= S) return;                                    // uniform per workgroup
+    const auto rs_ser = make_rsrc(series, (uint32_t)T * (uint32_t)N * 16u);
+    auto day_of = [&](int bb, int hh) { return days[(size_t)((hh + W - 1) % H) * B + bb]; };
+    f4 mk[PPT];
+    float ac[PPT];
+    auto issue = [&](int bb, int hh, int dl) {            // the sample's staging loads, nothing waited
+        const int d0 = dl - (W - 1);
+#pragma unroll
+        for (int k = 0; k < PPT; ++k) {
+            const int it = min(tid + k * 256, P - 1);
+            const int t = (int)fdiv((uint32_t)it, div_r), n = n0 + it - t * R;
+            int h = hh + t;
+            h = h >= H ? h - H : h;
+            ac[k] = actions[((size_t)h * B + bb) * N + n];
+            const int d = d0 + t;
+            const bool in = tid + k * 256 < P && d >= 0 && d < T;
+            mk[k] = buf_load4(rs_ser, in ? ((uint32_t)d * (uint32_t)N + (uint32_t)n) * 16u : 0xFFFFFFF0u);
+        }
+    };
+    // index pipeline: (b0, h0, d0) current; (b1, h1, d1) next; (b2, h2) the one after
+    int bc = env[j], hc = h0[j];
+    int dc = day_of(bc, hc);
+    bool m1 = j + G < S, m2 = j + 2 * G < S;
+    int b1 = 0, h1 = 0, d1 = 0, b2 = 0, h2 = 0;
+    if (m1) { b1 = env[j + G]; h1 = h0[j + G]; }
+    if (m2) { b2 = env[j + 2 * G]; h2 = h0[j + 2 * G]; }
+    if (m1) d1 = day_of(b1, h1);
+    issue(bc, hc, dc);
+    while (true) {
+        if (tid < R) a_out[(size_t)j * N + n0 + tid] = actions[((size_t)((hc + W) % H) * B + bc) * N + n0 + tid];
+        if (tid == 0 && blockIdx.y == 0) r_out[j] = rewards[(size_t)((hc + W - 1) % H) * B + bc];
+        const int dfirst = dc - (W - 1);
+#pragma unroll
+        for (int k = 0; k < PPT; ++k) {
+            const int it = tid + k * 256;
+            if (it < P) {
+                const int t = (int)fdiv((uint32_t)it, div_r), nl = it - t * R;
+                const int d = dfirst + t;
+                const bool in = d >= 0 && d < T;
+                float* dst = ext + ((size_t)nl * W1 + t) * F;
+                dst[0] = in ? mk[k].x : NAN;
+                dst[1] = in ? mk[k].y : NAN;
+                dst[2] = in ? mk[k].z : NAN;
+                dst[3] = in ? mk[k].w : NAN;
+                dst[4] = ac[k];
+            }
+        }
+        __syncthreads();
+        if (m1) issue(b1, h1, d1);                          // the next sample's loads fly during the write-out
+        float* so = s + (size_t)j * N * WF + (size_t)n0 * WF;
+        float* sn = s_next + (size_t)j * N * WF + (size_t)n0 * WF;
+        const auto rso = make_rsrc(so, (uint32_t)per * 4u), rsn = make_rsrc(sn, (uint32_t)per * 4u);
+        for (int q = tid; q < per / 4; q += 256) {
+            float v0[4], v1[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int e = 4 * q + k;
+                const int n = (int)fdiv((uint32_t)e, div_wf);
+                const float* x = ext + (size_t)n * F + e;
+                v0[k] = x[0];
+                v1[k] = x[F];
+            }
+            buf_store4<NT>(rso, (uint32_t)q * 16u, f4{v0[0], v0[1], v0[2], v0[3]});
+            buf_store4<NT>(rsn, (uint32_t)q * 16u, f4{v1[0], v1[1], v1[2], v1[3]});
+        }
+        // index chain ahead: the day of the sample after next, env / h0 of the one after that
+        const int j3 = j + 3 * G;
+        const bool m3 = j3 < S;
+        const int d2 = m2 ? day_of(b2, h2) : 0;
+        int b3 = 0, h3 = 0;
+        if (m3) { b3 = env[j3]; h3 = h0[j3]; }
+        __syncthreads();                                   // the image is rewritten next
+        if (!m1) break;
+        j += G;
+        bc = b1; hc = h1; dc = d1;
+        b1 = b2; h1 = h2; d1 = d2; m1 = m2;
+        b2 = b3; h2 = h3; m2 = m3;
     }
 }
 

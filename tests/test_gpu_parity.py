@@ -580,7 +580,12 @@ def test_gpu_resident_series_equals_bar_batch(step_kernels):
     (200, 30, 12, 33, 40, "PMENV_REPLAY_LDS"),   # per-element LDS staging, 16-B stores
     (300, 30, 50, 17, 80, ""),                   # F = 5 vector staging, 8 pairs per thread (BASELINE shape)
     (60, 3, 5, 4, 9, ""),                        # LDS-staged, sample block not 16-B granular
-    (120, 300, 50, 3, 60, "")])                  # staged days > 64 KiB: per-float kernel
+    (120, 300, 50, 3, 60, ""),                   # staged days > 64 KiB: per-float kernel
+    (200, 30, 12, 33, 40, "PMENV_REPLAY_GRID=5"),      # persistent F = 5 loop: 13 samples per workgroup
+    (300, 30, 50, 17, 80, "PMENV_REPLAY_GRID=3"),      # persistent, 8 pairs per thread, ragged tail
+    (300, 30, 50, 17, 80, "PMENV_REPLAY_PERSIST=0"),   # one workgroup per sample, nt stores
+    (300, 30, 50, 17, 80, "PMENV_REPLAY_TPB=512"),     # one workgroup per sample, 512 threads
+    (300, 30, 50, 17, 80, "PMENV_REPLAY_NT=0")])       # persistent, default-policy stores
 def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch):
     """replay/buffer.py:39-79 sample on device vs the numpy restatement
     (the reference module is not importable: parity restated from its text)."""
@@ -588,7 +593,8 @@ def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch)
     from pmenv.replay import DeviceReplay
     from oracle import replay_gather
     if knob:
-        monkeypatch.setenv(knob, "1")
+        k, _, v = knob.partition("=")
+        monkeypatch.setenv(k, v or "1")
     rng = np.random.default_rng(4)
     bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
     m = MarketSeries(bars, device=DEV)
