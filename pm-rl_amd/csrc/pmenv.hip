@@ -18,6 +18,7 @@
 #include "env_step.h"
 #include "scalar_vec.h"
 #include "rollout.h"
+#include "gae_vec.h"
 #include "replay.h"
 #include "trainer.h"
 
@@ -841,7 +842,23 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     const bool tile = fits && (knob ? !strcmp(knob, "tile") : !scan);
     const char* uknob = getenv("PMENV_GAE_U");    // A/B knob: steps per lane and segment (8 | 16)
     const int U = uknob ? atoi(uknob) : (B >= 16384 ? 8 : 16);
-    if (tile && U == 16)
+    // A/B knob PMENV_GAE_E: envs per lane of the pipelined tile (gae_tile_vec_kernel;
+    // 1, 2 or 4, needs B % E == 0); 0 = gae_tile_kernel
+    const char* eknob = getenv("PMENV_GAE_E");
+    int E = eknob ? atoi(eknob) : 0;
+    if (E != 1 && E != 2 && E != 4) E = 0;
+    if (E && B % E) E = 0;
+    if (tile && E) {
+        const unsigned g = (unsigned)((B + 64 * E - 1) / (64 * E));
+#define PMENV_GAEV(U_, E_) \
+    gae_tile_vec_kernel<8, U_, E_><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam)
+        if (E == 1 && U == 16) PMENV_GAEV(16, 1);
+        else if (E == 1) PMENV_GAEV(8, 1);
+        else if (E == 2 && U == 4) PMENV_GAEV(4, 2);
+        else if (E == 2) PMENV_GAEV(8, 2);
+        else PMENV_GAEV(4, 4);                    // E = 4 at U = 8 spills
+#undef PMENV_GAEV
+    } else if (tile && U == 16)
         gae_tile_kernel<8, 16><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
                                                                  lam);
     else if (tile)

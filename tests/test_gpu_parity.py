@@ -427,6 +427,33 @@ def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
     np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("E,U", [(1, 8), (1, 16), (2, 8), (2, 4), (4, 4)])
+@pytest.mark.parametrize("T,B", [(1, 8), (37, 100), (37, 102), (64, 64), (129, 4100), (1000, 200), (256, 65536), (300, 132)])
+def test_gpu_gae_tile_vec_matches_oracle(T, B, E, U, monkeypatch):
+    """The pipelined tile (gae_tile_vec_kernel, E envs per lane): vs the oracle's
+    recursion, and bitwise equal to gae_tile_kernel at the same segment length U
+    (ragged B falls back to E = 1 where B % E != 0)."""
+    from pmenv import rollout
+    rng = np.random.default_rng(T * 3 + B)
+    r = rng.standard_normal((T, B)).astype(np.float32)
+    v = rng.standard_normal((T + 1, B)).astype(np.float32)
+    d = rng.random((T, B)) < 0.02
+    monkeypatch.setenv("PMENV_GAE", "tile")
+    monkeypatch.setenv("PMENV_GAE_U", str(U))
+    monkeypatch.setenv("PMENV_GAE_E", str(E))
+    adv, ret = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
+    oadv, oret = or_gae(r, v, d, 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
+    if U in (8, 16):
+        monkeypatch.delenv("PMENV_GAE_E")
+        adv0, ret0 = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
+        assert torch.equal(adv, adv0) and torch.equal(ret, ret0)
+    adv2, _ = rollout.gae(_t(r), _t(v), None, 0.99, 1.0)            # no dones
+    oadv2, _ = or_gae(r, v, np.zeros_like(d), 0.99, 1.0)
+    np.testing.assert_allclose(adv2.cpu().numpy(), oadv2, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 8192), (700, 4099),
                                  (16384, 64)])
 def test_gpu_gae_horizon_split_matches_oracle(T, B):
