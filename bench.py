@@ -9,12 +9,12 @@ price relatives from the close channel, action normalisation, portfolio value
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
 assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
 Philox OHLC series and softmax actions already resident in HBM. The step runs as
-two launches (scalar_step_kernel, then the streaming window advance). By default
-the window is advanced in place — the reference's contract: step() mutates the
-caller's features and returns them (trading_env.py:102-105) — by
-advance_flat_inplace_kernel; the double-buffered advance (obs -> a fresh buffer,
-advance_flat_kernel, the form the device rollout buffer uses) is timed as well and
-reported under "alt".
+two launches (the per-env scalar step scalar_step_vec_kernel, then the streaming
+window advance). By default the window is advanced in place — the reference's
+contract: step() mutates the caller's features and returns them
+(trading_env.py:102-105) — by advance_flat_inplace_kernel; the double-buffered
+advance (obs -> a fresh buffer, advance_flat_wg_kernel, the form the device rollout
+buffer uses) is timed as well and reported under "alt".
 Multi-GPU runs are weak-scaled (65,536 envs per rank, envs sharded by global id,
 no collective in the step) and launched one process per GPU:
 

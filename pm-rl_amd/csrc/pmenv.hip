@@ -761,12 +761,19 @@ const char* pmenv_step_path(const pmenv* h) {
     if (!h) return "";
     if (!h->streaming) return "step_advance_lds_kernel";
     if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
-    if (h->fused) return "advance_rows_kernel<fused> (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
-    if (h->flat && h->flat_inplace && h->flat_db_wg)
-        return "scalar_step_kernel+advance_flat_wg_kernel (obs_out) | scalar_step_kernel+advance_flat_inplace_kernel (in place)";
-    if (h->flat && h->flat_inplace) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_flat_inplace_kernel (in place)";
-    if (h->flat) return "scalar_step_kernel+advance_flat_kernel (obs_out) | scalar_step_kernel+advance_rows_kernel (in place)";
-    return "scalar_step_kernel+advance_rows_kernel";
+    // the two-launch path: the scalar step (K1) the handle launches, then the stream
+    const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
+                   : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
+    const char* db = h->fused ? nullptr
+                   : h->flat ? (h->flat_db_wg ? "advance_flat_wg_kernel" : "advance_flat_kernel")
+                   : "advance_rows_kernel";
+    const char* ip = h->flat && h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
+    static thread_local char buf[256];
+    if (db)
+        snprintf(buf, sizeof buf, "%s+%s (obs_out) | %s+%s (in place)", k1, db, k1, ip);
+    else
+        snprintf(buf, sizeof buf, "advance_rows_kernel<fused> (obs_out) | %s+%s (in place)", k1, ip);
+    return buf;
 }
 
 int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
