@@ -522,7 +522,13 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->flat_ip_block = 512;
         h->flat_ip_vec = 2;
         h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
-        if (getenv("PMENV_STREAM_POL") == nullptr) h->flat_pol = 1;
+        // nt unless the window fits the Infinity Cache with room for its double buffer
+        // (<= 128 MiB): step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default
+        // policy against 46.5 nt (double-buffered 46.3 / 47.4); 8,192 envs: 84.4 / 85.7
+        // in place but 91.2 / 86.5 double-buffered; 16,384: 199.6 / 164.6
+        // (profiles/ab_r01/pol_small_r01j.log)
+        if (getenv("PMENV_STREAM_POL") == nullptr)
+            h->flat_pol = (int64_t)c.num_envs * per * 4 <= (128ll << 20) ? 0 : 1;
         // A/B knobs
         if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
         if (const char* knob = getenv("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
