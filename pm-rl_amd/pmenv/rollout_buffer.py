@@ -91,7 +91,9 @@ class DeviceRolloutBuffer:
         r = self.r[t, env].reshape(S, 1, 1)                           # :130
         v_prev = self.v[t - 1, env].to(torch.float32).reshape(S, 1, 1)   # :131
         a_prev = self.a[t - 1, env].reshape(S, self.N, 1)             # :132
-        p = (self.s[t, env][..., self.W - 1, c] / s[..., self.W - 1, c]).reshape(S, self.N, 1)   # :133
+        # :133 — only the last day's close of the next window is read (indexing the slab
+        # directly: no [S, N, W, F] copy of the next windows)
+        p = (self.s[t, env, :, self.W - 1, c] / s[..., self.W - 1, c]).reshape(S, self.N, 1)
         return s, a, r, v_prev, a_prev, p
 
     def _pairs(self, order):
