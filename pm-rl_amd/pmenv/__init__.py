@@ -6,9 +6,9 @@ this package is the host-side mirror of the reference's Python interface
 """
 from .config import EnvConfig  # noqa: F401
 from .trading_env import TradingEnv, RingView  # noqa: F401
-from . import synth, rollout, parallel, trainer, data, replay, rollout_buffer, on_policy  # noqa: F401
+from . import synth, rollout, parallel, trainer, data, replay, rollout_buffer, on_policy, off_policy  # noqa: F401
 from .data import MarketSeries  # noqa: F401
 from .rollout_buffer import DeviceRolloutBuffer  # noqa: F401
 
 __all__ = ["EnvConfig", "TradingEnv", "RingView", "synth", "rollout", "parallel", "trainer", "data", "MarketSeries", "replay",
-           "DeviceRolloutBuffer", "rollout_buffer", "on_policy"]
+           "DeviceRolloutBuffer", "rollout_buffer", "on_policy", "off_policy"]

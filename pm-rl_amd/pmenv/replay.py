@@ -50,11 +50,14 @@ class DeviceReplay:
         span = self.count - self.W - 1
         if span < 1:
             raise ValueError("not enough recorded steps to sample a window")
-        st = torch.randint(0, span, (batch_size,), generator=generator)
-        env = torch.randint(0, self.B, (batch_size,), generator=generator)
+        # drawn where the generator lives: a CPU generator (reproducible across devices)
+        # costs a host->device copy per batch; no generator or a device one stays on the GPU
+        dev = self.days.device
+        gdev = generator.device if generator is not None else dev
+        st = torch.randint(0, span, (batch_size,), generator=generator, device=gdev)
+        env = torch.randint(0, self.B, (batch_size,), generator=generator, device=gdev)
         oldest = (self.head - self.count) % self.H
         h0 = (oldest + st) % self.H
-        dev = self.days.device
         return h0.to(dev, torch.int32), env.to(dev, torch.int32)
 
     def gather(self, h0, env):
