@@ -250,11 +250,29 @@ def main():
                "env_steps_per_s_per_gpu": B * args.alt_steps / a_el,
                "ms_per_step": a_el / args.alt_steps * 1e3, "advance_kernel_avg_us": a_k * 1e6}
 
+    collective = None
     if world > 1:
         t = torch.tensor([elapsed, kern_avg_s], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_avg_s = float(t[0]), float(t[1])
+        # the path's one exchange (outside the timed step loop): the advantage-
+        # normalisation moments of the last rewards, {count, sum, sum of squares} f64
+        # from the HIP moments kernel, summed over ranks (pmenv.parallel.normalize)
+        from pmenv import parallel
+        adv = reward                                              # device tensor (gloo stages it)
+        parallel.normalize(adv)                                   # warm
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        c0 = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            normed = parallel.normalize(adv)
+        torch.cuda.synchronize(dev)
+        c_us = (time.perf_counter() - c0) / reps * 1e6
+        n_all, _, _ = parallel.allreduce_moments(parallel.local_moments_cpu(adv).to(adv.device))
+        collective = {"op": "all_reduce(sum) of 24-byte advantage moments + normalise", "backend": dist.get_backend(),
+                      "us_per_update": c_us, "count_all_ranks": n_all, "normalised_finite": bool(torch.isfinite(normed).all())}
     nonfinite = env.nonfinite_count()
 
     path = env.step_path
@@ -318,6 +336,7 @@ def main():
             "nonfinite_envs": nonfinite,
             "step_path": env.step_path,
             "alt": alt,
+            "collective": collective,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

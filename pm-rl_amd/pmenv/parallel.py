@@ -32,7 +32,7 @@ def allreduce_moments(local, group=None):
 
 def local_moments_cpu(x):
     """CPU/host counterpart of rollout.moments (for gloo paths and tests)."""
-    x = x.detach().to(torch.float64).reshape(-1)
+    x = x.detach().to("cpu", torch.float64).reshape(-1)
     return torch.stack([torch.tensor(float(x.numel()), dtype=torch.float64), x.sum(), (x * x).sum()])
 
 
