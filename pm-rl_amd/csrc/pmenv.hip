@@ -944,10 +944,12 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     if (!series || !days || !actions || !rewards || !h0 || !env || !s || !s_next || !a_out || !r_out || T < 1 ||
         N < 1 || F < 2 || W < 1 || H < W + 1 || B < 1 || S < 1)
         return PMENV_ERR_ARG;
-    // F = 5: vector staging per asset group (replay_gather_f5_kernel); otherwise one
-    // workgroup per sample with the W+1 staged days in LDS when they fit in 64 KiB, else
-    // one thread per output float. Measured at S = 8,192, N = 30, W = 50: 131 us for the
-    // whole-sample f5 form against 204 us for the per-element staging (bench_rows.py)
+    // F = 5: vector staging per asset group (replay_gather_f5p_kernel, persistent; or
+    // replay_gather_f5_kernel, one workgroup per sample); otherwise one workgroup per
+    // sample with the W+1 staged days in LDS when they fit in 64 KiB, else one thread per
+    // output float. Measured at S = 8,192, N = 30, W = 50: 96-102 us for the persistent
+    // f5 form, 117 us one workgroup per sample, 204 us for the per-element staging
+    // (tools/ab_replay.py, bench_rows.py)
     const size_t lds = (size_t)N * (W + 1) * F * sizeof(float);
     const bool al16 = ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0 && ((uintptr_t)series & 15u) == 0;
     // F = 5 vector staging over asset groups of R rows: R divides N, R*W*F is a multiple
