@@ -15,8 +15,10 @@ contract: step() mutates the caller's features and returns them
 (trading_env.py:102-105) — by advance_flat_inplace_kernel; the double-buffered
 advance (obs -> a fresh buffer, advance_flat_wg_kernel, the form the device rollout
 buffer uses) is timed as well and reported under "alt".
-Multi-GPU runs are weak-scaled (65,536 envs per rank, envs sharded by global id,
-no collective in the step) and launched one process per GPU:
+Multi-GPU runs are weak-scaled by default (65,536 envs per rank, envs sharded by
+global id, no collective in the step); --global-envs G runs G envs in total sharded
+over the ranks (strong scaling; BASELINE config 4 is 65,536 over 8 GPUs). One
+process per GPU:
 
     python bench.py                                   # N = 1
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -52,6 +54,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--global-envs", type=int, default=0,
+                    help="strong scaling: this many envs in total, sharded over the ranks "
+                         "(BASELINE config 4: 65536 over 8 GPUs); 0 = weak scaling, --envs-per-gpu per rank")
     ap.add_argument("--assets", type=int, default=30)
     ap.add_argument("--window", type=int, default=50)
     ap.add_argument("--features", type=int, default=5)
@@ -172,8 +177,15 @@ def main():
     from pmenv import TradingEnv, synth, _abi
     lib = _abi.load()
 
-    B, N, W, F = args.envs_per_gpu, args.assets, args.window, args.features
-    lo = rank * B                                    # weak scaling: global env ids of this rank
+    N, W, F = args.assets, args.window, args.features
+    if args.global_envs:                             # strong scaling: a shard of a fixed total
+        from pmenv.parallel import shard_range
+        lo, hi = shard_range(args.global_envs, rank, world)
+        B = hi - lo
+        args.envs_per_gpu = B
+    else:                                            # weak scaling: global env ids of this rank
+        B = args.envs_per_gpu
+        lo = rank * B
     H = max(1, min(args.horizon, args.steps + args.warmup))
     series = synth.series(H + W, B, N, env_offset=lo, seed=args.seed, device=dev)      # [H+W, B, N, 4]
     actions = synth.actions(H, B, N, env_offset=lo, seed=args.seed + 1, device=dev)     # [H, B, N]
@@ -286,7 +298,7 @@ def main():
         advance_kernel = "advance_flat_inplace_kernel"
     else:
         advance_kernel = "advance_rows_kernel"
-    total_env_steps = world * B * args.steps
+    total_env_steps = (args.global_envs or world * B) * args.steps
     value = total_env_steps / elapsed
     bstep = step_bytes(N, W, F)
     achieved = bstep * B / kern_avg_s / 1e9
@@ -313,13 +325,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_envs else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Philox OHLC random walk + softmax actions, resident in HBM)",
             "config": {
-                "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels",
-                "envs_per_gpu": B, "global_envs": world * B, "assets": N, "window": W, "features": F,
+                "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels"
+                            + (f" ({args.global_envs} envs in total, sharded)" if args.global_envs else ""),
+                "envs_per_gpu": B, "global_envs": args.global_envs or world * B, "assets": N, "window": W, "features": F,
                 "reward": args.reward, "commission": args.commission, "obs_dtype": "f32", "accumulate": "f64",
                 "windows": args.windows,
                 "parallelism": f"env-sharded x{world} (no collective in the step)",
