@@ -151,6 +151,39 @@ def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
         "sample": f"{S} envs x {T} steps, HIP vs CPU restatement"}
 
 
+def reference_golden_mae(dev, torch, TradingEnv):
+    """Reward MAE / value error of the HIP path against the REFERENCE's own recorded
+    outputs: tests/golden/simplex_n30_w50_t256_{f32,f64}.npz were written by running
+    zachramsey/pm-rl's env/sim/trading_env.py (tests/golden/gen_golden.py) on a
+    256-day, 30-asset, 50-day-window case; here one env replays the same windows and
+    actions through the fused advance step (rank 0, outside the timed region)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import golden_util as gu
+    out = {}
+    for name in ("simplex_n30_w50_t256_f32", "simplex_n30_w50_t256_f64"):
+        g = gu.load(name)
+        m = g["meta"]
+        N, W, F, T = m["N"], m["W"], m["F"], m["T"]
+        env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=dev)
+        obs = None
+        r = np.full(T + 1, np.nan)
+        v = np.zeros(T + 1)
+        for i in range(T + 1):
+            if g["ops"][i]:
+                obs = torch.as_tensor(gu.window(g, i)[0], dtype=torch.float32, device=dev).contiguous()
+                env.reset(obs)
+            else:
+                ri, _ = env.step(torch.as_tensor(g["actions"][i], dtype=torch.float32, device=dev).reshape(N, 1),
+                                 obs, bar=torch.as_tensor(gu.bar(g, i), dtype=torch.float32, device=dev))
+                r[i] = float(ri)
+            v[i] = float(env.value)
+        ok = ~g["ops"].astype(bool) & np.isfinite(g["rewards"])
+        out[m["dtype"]] = {"reward_mae": float(np.mean(np.abs(r[ok] - g["rewards"][ok]))),
+                           "value_max_rel": float(np.max(np.abs(v / g["values"] - 1.0))), "steps": int(ok.sum())}
+    return {"case": "simplex_n30_w50_t256 (reference env outputs recorded in tests/golden)", **out}
+
+
 def main():
     args = parse()
     import torch
@@ -311,9 +344,10 @@ def main():
     except (OSError, ValueError):
         pass
 
-    cpu = mae = None
+    cpu = mae = ref_gold = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu, mae = cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv)
+        ref_gold = reference_golden_mae(dev, torch, TradingEnv)
 
     if rank == 0:
         line = {
@@ -346,6 +380,7 @@ def main():
             "cpu_baseline": cpu,
             "reward_mae": None if mae is None else mae["reward_mae"],
             "parity_sample": mae,
+            "reference_goldens": ref_gold,
             "nonfinite_envs": nonfinite,
             "step_path": env.step_path,
             "alt": alt,
