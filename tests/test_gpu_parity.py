@@ -638,6 +638,40 @@ def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch)
     assert np.array_equal(a.cpu().numpy()[..., 0], ea) and np.array_equal(r.cpu().numpy()[:, 0, 0], er)
 
 
+def test_gpu_replay_gather_full_size_persistent():
+    """The replay at the f4 bench shape (4,096 envs x 256 recorded steps, 8,192 samples
+    of 30 assets x 50 days): the default persistent gather (one workgroup per CU, ~32
+    samples each, the next sample's loads in flight) vs the restatement on 512 of the
+    samples, and bitwise equal to the one-workgroup-per-sample form on all of them."""
+    import os
+    from pmenv import MarketSeries
+    from pmenv.replay import DeviceReplay
+    from oracle import replay_gather
+    B, N, W, H, S, T = 4096, 30, 50, 256, 8192, 700
+    rng = np.random.default_rng(11)
+    bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
+    m = MarketSeries(bars, device=DEV)
+    rb = DeviceReplay(B, N, W, H, m)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    day0 = torch.randint(W, T - H - 2, (B,), device=DEV, generator=g, dtype=torch.int32)
+    for h in range(H + 40):                      # wraps the ring
+        rb.add(day0 + h % H, torch.rand(B, N, device=DEV, generator=g), torch.randn(B, device=DEV, generator=g))
+    h0, env = rb.indices(S, generator=torch.Generator().manual_seed(6))
+    s, a, r, s2 = rb.gather(h0, env)
+    os.environ["PMENV_REPLAY_PERSIST"] = "0"
+    try:
+        s_b, a_b, r_b, s2_b = rb.gather(h0, env)
+    finally:
+        del os.environ["PMENV_REPLAY_PERSIST"]
+    assert torch.equal(s, s_b) and torch.equal(s2, s2_b) and torch.equal(a, a_b) and torch.equal(r, r_b)
+    pick = np.sort(np.random.default_rng(7).choice(S, 512, replace=False))
+    es, ea, er, es2 = replay_gather(bars, rb.days.cpu().numpy(), rb.actions.cpu().numpy(), rb.rewards.cpu().numpy(),
+                                    h0.cpu().numpy()[pick], env.cpu().numpy()[pick], W)
+    assert np.array_equal(s.cpu().numpy()[pick], es, equal_nan=True)
+    assert np.array_equal(s2.cpu().numpy()[pick], es2, equal_nan=True)
+    assert np.array_equal(a.cpu().numpy()[pick, :, 0], ea) and np.array_equal(r.cpu().numpy()[pick, 0, 0], er)
+
+
 @pytest.mark.parametrize("B,N,W,T", [(300, 30, 20, 80), (5, 300, 4, 9), (70, 1, 3, 2), (9, 257, 2, 5)])
 def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
     """util/eval.py:14-37 metrics over an env trajectory vs the numpy restatement
