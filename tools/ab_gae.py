@@ -1,6 +1,6 @@
 """A/B the GAE kernels (env knobs read at each call) in ONE process, interleaved
 rounds. Variants are '+'-joined KEY=VALUE knob sets; variants with the same
-segment length (PMENV_GAE_U) must agree bit for bit, all of them within 1e-5 of
+segment length (PMENV_GAE_NW x PMENV_GAE_U) must agree bit for bit, all of them within 1e-5 of
 the first.
 
     python tools/ab_gae.py --shapes 256x65536,256x16384 \
@@ -32,7 +32,7 @@ dev = torch.device("cuda:0")
 lib = _abi.load()
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-KN = ("PMENV_GAE", "PMENV_GAE_U", "PMENV_GAE_E")
+KN = ("PMENV_GAE", "PMENV_GAE_U", "PMENV_GAE_E", "PMENV_GAE_NW")
 
 
 def knobs(v):
@@ -75,7 +75,8 @@ for shape in a.shapes.split(","):
     first = next(iter(bufs))
     by_u = {}
     for vn, (adv, ret) in bufs.items():
-        u = knobs(vn).get("PMENV_GAE_U", "")
+        kv = knobs(vn)                             # same segment (NW x U): same arithmetic
+        u = int(kv.get("PMENV_GAE_U", "8")) * int(kv.get("PMENV_GAE_NW", "8"))
         if u in by_u:
             assert torch.equal(adv, by_u[u][0]) and torch.equal(ret, by_u[u][1]), (vn, "not bitwise equal at U", u)
         else:
