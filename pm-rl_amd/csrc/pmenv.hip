@@ -953,7 +953,8 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     const size_t lds = (size_t)N * (W + 1) * F * sizeof(float);
     const bool al16 = ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0 && ((uintptr_t)series & 15u) == 0;
     // F = 5 vector staging over asset groups of R rows: R divides N, R*W*F is a multiple
-    // of 4 (16-B aligned groups), R*(W+1) <= 512 pairs (two per thread) when possible
+    // of 4 (16-B aligned groups), R*(W+1) <= 2,048 (day, asset) pairs (at most 8 per
+    // thread); N = 30, W = 50: R = 30, one group per sample
     int R = 0;
     if (F == 5 && al16 && !getenv("PMENV_REPLAY_LDS")) {   // A/B knob: the per-element staging kernel
         // the largest group within 2,048 pairs: whole samples measured faster than
