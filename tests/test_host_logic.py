@@ -96,3 +96,27 @@ def test_rollout_buffer_sampling_host_logic():
     assert len(seen) == len(set(seen)) == T * B              # a permutation of all pairs
     ordered = [tuple(x) for s, a, *_ in buf.sample(B) for x in zip(a[:, 0, 0].long().tolist(), range(B))]
     assert ordered == [(t, e) for t in range(1, T + 1) for e in range(B)]
+
+
+def test_off_policy_host_checks_cpu():
+    """pmenv.off_policy.OffPolicy host logic (train/off_policy.py shape) without a GPU:
+    series/env shape agreement, the replay sized from the env, the series-length check
+    of collect, and the random seeding action being a simplex point."""
+    import types
+    import numpy as np
+    import torch
+    from pmenv.config import EnvConfig
+    from pmenv.data import MarketSeries
+    from pmenv.off_policy import OffPolicy
+    cfg = EnvConfig(num_envs=4, num_assets=3, window=5)
+    env = types.SimpleNamespace(cfg=cfg, device=torch.device("cpu"))
+    bars = np.ones((40, 3, 4), np.float32)
+    m = MarketSeries(bars, device="cpu")
+    with pytest.raises(ValueError):
+        OffPolicy(env, MarketSeries(np.ones((40, 2, 4), np.float32), device="cpu"), capacity=10)
+    loop = OffPolicy(env, m, capacity=10)
+    assert loop.replay.days.shape == (10, 4) and loop.replay.actions.shape == (10, 4, 3)
+    with pytest.raises(ValueError):                      # 30 + 5 + 10 > 40 days
+        loop.collect(torch.full((4,), 30, dtype=torch.int32), 10)
+    a = loop._random_action()
+    assert a.shape == (4, 3) and torch.all(a >= 0) and torch.allclose(a.sum(-1), torch.ones(4))
