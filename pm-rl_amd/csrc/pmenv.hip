@@ -1034,12 +1034,24 @@ int pmenv_metrics(const double* returns, const double* values, const float* weig
     if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;
     // measured on MI355X (tools/bench_rows.py): the horizon split over four waves per
     // 64 envs against the thread-per-env walk — see profiles/rows_r01*/
-    if (getenv("PMENV_METRICS_WALK"))   // A/B knob: the thread-per-env walk
+    const int tpe = N <= 256 ? N : 256, eb = 256 / tpe;
+    const int nseg = (B + 63) / 64, nturn = (B + eb - 1) / eb;
+    // one launch for both passes (metrics_fused_kernel); A/B knobs: PMENV_METRICS_FUSED=0
+    // (two launches), PMENV_METRICS_SEG_FIRST=0 (turnover blocks dispatched first)
+    const bool walk = getenv("PMENV_METRICS_WALK") != nullptr;   // A/B knob: the thread-per-env walk
+    const bool fused = !walk && !(getenv("PMENV_METRICS_FUSED") && atoi(getenv("PMENV_METRICS_FUSED")) == 0);
+    if (fused) {
+        const int seg_first = !(getenv("PMENV_METRICS_SEG_FIRST") && atoi(getenv("PMENV_METRICS_SEG_FIRST")) == 0);
+        metrics_fused_kernel<<<(unsigned)(nseg + nturn), 256, 0, stream>>>(returns, values, weights, T, B, N,
+                                                                           risk_free_rate, periods, tpe, eb, nseg,
+                                                                           nturn, seg_first, out);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+    if (walk)
         metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
     else
-        metrics_seg_kernel<<<(B + 63) / 64, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
-    const int tpe = N <= 256 ? N : 256, eb = 256 / tpe;
-    metrics_turnover_kernel<<<(unsigned)((B + eb - 1) / eb), 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
+        metrics_seg_kernel<<<(unsigned)nseg, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
+    metrics_turnover_kernel<<<(unsigned)nturn, 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

@@ -96,11 +96,11 @@ __global__ void metrics_kernel(const double* returns, const double* values, int 
 //   re-walks its segment (an L2 re-read) with the running peak seeded by the
 //   maximum of every earlier segment.
 // Wave 0 adds the four segments' sums in wave order: deterministic.
-__global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
-                                                          double rf, double periods, double* out) {
+__device__ __forceinline__ void metrics_seg_body(const double* returns, const double* values, int T, int B, double rf,
+                                                 double periods, double* out, int bid) {
     __shared__ double sh[5][4][64];              // S1, S2, down, segment max (of values), mdd
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int b = blockIdx.x * 64 + lane;
+    const int b = bid * 64 + lane;
     const bool ok = b < B;
     const int bb = ok ? b : B - 1;
     const double rfp = rf != 0.0 ? pow(1.0 + rf, 1.0 / periods) - 1.0 : 0.0;
@@ -164,17 +164,22 @@ __global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns,
     out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
 }
 
+__global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
+                                                          double rf, double periods, double* out) {
+    metrics_seg_body(returns, values, T, B, rf, periods, out, (int)blockIdx.x);
+}
+
 // util/eval.py:32-37 average turnover, element-parallel: a workgroup owns `eb` whole
 // envs (N <= 256: one thread per (env, asset), so each day's read is eb*N contiguous
 // floats) and every thread walks the days keeping the previous weight in a
 // register; the env's assets are then summed in a fixed order. N > 256: one env
 // per workgroup, threads stride over the assets.
-__global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
-                                                               int eb, double* out) {
+__device__ __forceinline__ void metrics_turnover_body(const float* weights, int T, int B, int N, int tpe, int eb,
+                                                      double* out, int bid) {
     __shared__ double sh[256];
     const int tid = threadIdx.x;
     const int el = tid % tpe, le = tid / tpe;
-    const int b = blockIdx.x * eb + le;
+    const int b = bid * eb + le;
     double acc = 0.0;
     if (le < eb && b < B) {
         for (int n = el; n < N; n += tpe) {
@@ -203,6 +208,25 @@ __global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weig
         for (int i = 0; i < tpe; ++i) tot += sh[le * tpe + i];
         out[(size_t)b * 5 + 3] = tot / T;
     }
+}
+
+__global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
+                                                               int eb, double* out) {
+    metrics_turnover_body(weights, T, B, N, tpe, eb, out, (int)blockIdx.x);
+}
+
+// Both metric passes in one launch: they read disjoint inputs and write disjoint
+// fields of out, so the latency-bound segment walk (returns, values) runs beside the
+// bandwidth-bound turnover stream (weights) instead of before it. Blocks [0, nseg)
+// take the segment walk when seg_first, else the turnover blocks come first.
+__global__ __launch_bounds__(256) void metrics_fused_kernel(const double* returns, const double* values,
+                                                            const float* weights, int T, int B, int N, double rf,
+                                                            double periods, int tpe, int eb, int nseg, int nturn,
+                                                            int seg_first, double* out) {
+    const int bid = (int)blockIdx.x;
+    const bool seg = seg_first ? bid < nseg : bid >= nturn;
+    if (seg) metrics_seg_body(returns, values, T, B, rf, periods, out, seg_first ? bid : bid - nturn);
+    else metrics_turnover_body(weights, T, B, N, tpe, eb, out, seg_first ? bid - nseg : bid);
 }
 
 // replay/buffer.py:53-79, one workgroup per sample: the W+1 days the pair (s, s')

@@ -672,6 +672,28 @@ def test_gpu_replay_gather_full_size_persistent():
     assert np.array_equal(a.cpu().numpy()[pick, :, 0], ea) and np.array_equal(r.cpu().numpy()[pick, 0, 0], er)
 
 
+@pytest.mark.parametrize("B,N,T", [(300, 30, 80), (4097, 30, 252), (9, 257, 5), (70, 1, 2)])
+def test_gpu_metrics_one_launch_equals_two(B, N, T, monkeypatch):
+    """metrics_fused_kernel (both passes in one launch, either block order) writes
+    bitwise what the two launches write."""
+    from pmenv.replay import trajectory_metrics
+    g = torch.Generator(device=DEV).manual_seed(B + N + T)
+    rets = 0.01 * torch.randn(T, B, device=DEV, dtype=torch.float64, generator=g)
+    vals = torch.cumprod(torch.cat([torch.ones(1, B, device=DEV, dtype=torch.float64), 1 + rets]), 0)
+    wts = torch.softmax(torch.randn(T + 1, B, N, device=DEV, generator=g), -1)
+    outs = []
+    for knobs in ({}, {"PMENV_METRICS_SEG_FIRST": "0"}, {"PMENV_METRICS_FUSED": "0"}):
+        for k in ("PMENV_METRICS_SEG_FIRST", "PMENV_METRICS_FUSED"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        m = trajectory_metrics(rets, vals, wts)
+        outs.append(torch.stack([m[k] for k in ("sharpe", "sortino", "max_drawdown", "average_turnover",
+                                                "final_value")]))
+    for o in outs[1:]:
+        assert torch.equal(o.view(torch.int64), outs[0].view(torch.int64))
+
+
 @pytest.mark.parametrize("B,N,W,T", [(300, 30, 20, 80), (5, 300, 4, 9), (70, 1, 3, 2), (9, 257, 2, 5)])
 def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
     """util/eval.py:14-37 metrics over an env trajectory vs the numpy restatement

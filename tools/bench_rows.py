@@ -190,14 +190,18 @@ def main():
             wts = torch.softmax(torch.randn(T + 1, B, 30, device=dev, generator=g), -1)
             out = torch.empty(B, 5, dtype=torch.float64, device=dev)
             alg = T * B * 8 + (T + 1) * B * 8 + (T + 1) * B * 30 * 4 + B * 5 * 8
-            for mode in ("seg", "walk"):
+            for mode in ("fused", "seg", "walk"):
                 os.environ.pop("PMENV_METRICS_WALK", None)
+                os.environ.pop("PMENV_METRICS_FUSED", None)
                 if mode == "walk":
                     os.environ["PMENV_METRICS_WALK"] = "1"
+                if mode == "seg":                       # the two passes as two launches
+                    os.environ["PMENV_METRICS_FUSED"] = "0"
                 us = timeit(lambda: ck(lib.pmenv_metrics(P(rets), P(vals), P(wts), T, B, 30, 0.04, 252.0, P(out), st),
                                        "metrics"), a.reps)
                 res.append(row(f"trajectory_metrics_{mode}", us, alg, T=T, B=B, N=30))
             os.environ.pop("PMENV_METRICS_WALK", None)
+            os.environ.pop("PMENV_METRICS_FUSED", None)
 
     doc = {"device": torch.cuda.get_device_name(0), "peak_GBs": PEAK_GBS, "cases": res}
     print(json.dumps(doc, indent=1))
