@@ -715,3 +715,29 @@ def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
     exp = ref_metrics(rets.cpu().numpy(), vals.cpu().numpy(), wts.cpu().numpy())
     for i, k in enumerate(("sharpe", "sortino", "max_drawdown", "average_turnover", "final_value")):
         np.testing.assert_allclose(got[k].cpu().numpy(), exp[:, i], rtol=1e-6, atol=1e-9, err_msg=k)
+
+
+def test_gpu_beyond_flat_index_range_in_place():
+    """A window past the flat stream's 32-bit chunk index (1.2 M envs x 30 x 50 x 5 =
+    36 GB, 2.25e9 chunks): the handle falls back to the row kernel, and one in-place
+    step still shifts every sampled env's window by one day, appends its bar and
+    writes a finite reward (start, middle and end of the tensor)."""
+    from pmenv import TradingEnv
+    B, N, W = 1_200_000, 30, 50
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    assert "advance_flat_inplace_kernel" not in env.step_path.split("|")[-1]
+    g = torch.Generator(device=DEV).manual_seed(3)
+    obs = torch.rand(B, N, W, 5, device=DEV, generator=g) + 0.5
+    env.reset(obs)
+    bar = torch.rand(B, N, 4, device=DEV, generator=g) + 0.5
+    act = torch.softmax(torch.randn(B, N, device=DEV, generator=g), -1)
+    pick = torch.tensor([0, 1, B // 2, B - 2, B - 1], device=DEV)
+    before = obs[pick].clone()
+    r, out = env.step(act, obs, bar=bar)
+    assert out is obs
+    after = obs[pick]
+    assert torch.equal(after[:, :, :-1, :], before[:, :, 1:, :])
+    assert torch.equal(after[:, :, -1, :4], bar[pick])
+    assert torch.isfinite(r).all() and env.nonfinite_count() == 0
+    del obs, bar, env
+    torch.cuda.empty_cache()
