@@ -50,7 +50,7 @@ struct pmenv {
     int stream_pol;       // cache policy of the window stream (advance_rows_kernel POL)
     int fused_vec;        // float4 per thread of the fused one-launch step (512 threads, whole env)
     bool flat;            // double-buffered advance as the flat 16-B stream (advance_flat_kernel)
-    int flat_block, flat_pol;
+    int flat_block, flat_pol, flat_ip_pol;   // cache policy: double-buffered / in-place stream
     bool flat_inplace;    // in-place advance as the flat stream + halo (advance_flat_inplace_kernel)
     int flat_ip_block, flat_ip_vec;   // threads per workgroup, chunks per thread
     bool flat_db_wg;      // double-buffered advance in the workgroup form (advance_flat_wg_kernel)
@@ -215,12 +215,12 @@ void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
     const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
     const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
     switch (key) {
-    case 2561: launch_flat_ip_b<256, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
-    case 2562: launch_flat_ip_b<256, 2>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
-    case 2564: launch_flat_ip_b<256, 4>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
-    case 5121: launch_flat_ip_b<512, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
-    case 10241: launch_flat_ip_b<1024, 1>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
-    default: launch_flat_ip_b<512, 2>(h->flat_pol, p, grid, h->flat_qtot, stream); break;
+    case 2561: launch_flat_ip_b<256, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    case 2562: launch_flat_ip_b<256, 2>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    case 2564: launch_flat_ip_b<256, 4>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    case 5121: launch_flat_ip_b<512, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    case 10241: launch_flat_ip_b<1024, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    default: launch_flat_ip_b<512, 2>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
     }
 }
 
@@ -487,14 +487,14 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // streaming geometry
     static const int kInplaceOrder[3] = {2, 4, 1}, kDoubleOrder[3] = {4, 2, 1};
     h->stream_block = h->stream_block_db = kStreamBlock;
-    h->stream_pol = h->flat_pol = 0;
+    h->stream_pol = h->flat_pol = h->flat_ip_pol = 0;
     if (const char* knob = getenv("PMENV_STREAM_BLOCK")) {        // A/B knob: 128 | 256 | 512
         const int bk = atoi(knob);
         if (bk == 128 || bk == 256 || bk == 512) h->stream_block = h->stream_block_db = bk;
     }
     if (const char* knob = getenv("PMENV_STREAM_POL")) {          // A/B knob: 0 | 1 (nt) | 2 (sc0 nt)
         const int pol = atoi(knob);
-        if (pol >= 0 && pol <= 2) h->stream_pol = h->flat_pol = pol;
+        if (pol >= 0 && pol <= 2) h->stream_pol = h->flat_pol = h->flat_ip_pol = pol;
     }
     int fused_rows = 0;
     h->streaming = plan_streaming(c, kInplaceOrder, h->stream_block, &h->unit_rows, &h->stream_vec) &&
@@ -522,13 +522,17 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->flat_ip_block = 512;
         h->flat_ip_vec = 2;
         h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
-        // nt unless the window fits the Infinity Cache with room for its double buffer
-        // (<= 128 MiB): step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default
-        // policy against 46.5 nt (double-buffered 46.3 / 47.4); 8,192 envs: 84.4 / 85.7
-        // in place but 91.2 / 86.5 double-buffered; 16,384: 199.6 / 164.6
-        // (profiles/ab_r01/pol_small_r01j.log)
-        if (getenv("PMENV_STREAM_POL") == nullptr)
-            h->flat_pol = (int64_t)c.num_envs * per * 4 <= (128ll << 20) ? 0 : 1;
+        // nt unless the stream's working set fits the 256 MiB Infinity Cache: the window
+        // in place (<= 256 MiB), the window and its double buffer otherwise (<= 128 MiB).
+        // Step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default policy against
+        // 46.5 nt (double-buffered 46.3 / 47.4); 6,144 envs in place 62.6 / 66.9;
+        // 8,192 envs (246 MB) in place 84.6 / 86.1 but double-buffered 91.2 / 86.5;
+        // 16,384: 199.6 / 164.6 (profiles/ab_r01/pol_small_r01j.log, pol_ip_r01m.log)
+        if (getenv("PMENV_STREAM_POL") == nullptr) {
+            const int64_t win = (int64_t)c.num_envs * per * 4;
+            h->flat_pol = win <= (128ll << 20) ? 0 : 1;
+            h->flat_ip_pol = win <= (256ll << 20) ? 0 : 1;
+        }
         // A/B knobs
         if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
         if (const char* knob = getenv("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
