@@ -8,37 +8,51 @@ price relatives from the close channel, action normalisation, portfolio value
 
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65k envs x 30
 assets"): 65,536 envs x 30 assets x 50-day window x 5 channels per GPU, synthetic
-Philox OHLC series and softmax actions already resident in HBM. The step runs as
-two launches (the per-env scalar step scalar_step_vec_kernel, then the streaming
-window advance). By default the window is advanced in place — the reference's
-contract: step() mutates the caller's features and returns them
-(trading_env.py:102-105) — by advance_flat_inplace_kernel; the double-buffered
-advance (obs -> a fresh buffer, advance_flat_wg_kernel, the form the device rollout
-buffer uses) is timed as well and reported under "alt".
+Philox OHLC series and softmax actions already resident in HBM. By default the
+window is advanced in place — the reference's contract: step() mutates the
+caller's features and returns them (trading_env.py:102-105); the double-buffered
+advance (obs -> a fresh buffer, the form the device rollout buffer uses) is timed
+as well and reported under "alt". `step_path` names the kernels one step launches.
+
+Legs, in order (one process per GPU):
+  1. parity leg, every rank: 64 steps of the bench's own workload through the same
+     handle and buffers that are then timed; the first S envs' rewards and values
+     are kept and, after the timed region, checked against the CPU restatement on
+     the same inputs. It also carries the GPU past its start-up clock transient
+     (profiles/warm_curve_r02a.json: steps 3-25 of a cold process run up to 1.3x
+     slower), so the timed steps start at steady state whatever --warmup is.
+  2. --warmup untimed steps, then exactly --steps timed steps between barriers and
+     device synchronisations; max over ranks.
+  3. the other window mode (alt), the collective (N > 1), then on rank 0 at N = 1
+     the CPU baseline and the replay of the reference's own recorded outputs.
+
 Multi-GPU runs are weak-scaled by default (65,536 envs per rank, envs sharded by
 global id, no collective in the step); --global-envs G runs G envs in total sharded
-over the ranks (strong scaling; BASELINE config 4 is 65,536 over 8 GPUs). One
-process per GPU:
+over the ranks (strong scaling; BASELINE config 4 is 65,536 over 8 GPUs):
 
     python bench.py                                   # N = 1
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0. Refuses to run when any PMENV_* environment
+variable is set (the product library reads none; nothing may alter the timed path).
 """
 import argparse
 import ctypes
 import json
 import os
 import platform
+import statistics
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
-EVENT_EVERY = 4        # steps per sampled advance-kernel timing inside the timed region
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+L3_BYTES = 256 << 20    # Infinity Cache (MI355X_MICROARCH.md, Infinity Cache)
+EVENT_EVERY = 4         # steps per sampled kernel timing inside the timed region
+PARITY_STEPS = 64       # steps of the parity leg
 
 
 def step_bytes(N, W, F):
@@ -63,10 +77,9 @@ def parse():
     ap.add_argument("--horizon", type=int, default=256, help="resident days of synthetic bars/actions (cycled)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-sample-envs", type=int, default=4096)
+    ap.add_argument("--cpu-sample-envs", type=int, default=65536)
     ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="target CPU-seconds of oracle work")
-    ap.add_argument("--mae-envs", type=int, default=4096)
-    ap.add_argument("--mae-steps", type=int, default=64)
+    ap.add_argument("--parity-envs", type=int, default=4096, help="envs of the parity leg checked on the CPU")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--windows", choices=["double", "inplace"], default="inplace")
     ap.add_argument("--reward", default="log_returns",
@@ -74,6 +87,8 @@ def parse():
     ap.add_argument("--commission", type=float, default=0.0)
     ap.add_argument("--alt-steps", type=int, default=50,
                     help="extra timed steps of the other window mode (0: skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI; gloo lets several ranks share one GPU (functional rehearsal)")
     return ap.parse_args()
 
 
@@ -87,68 +102,88 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv):
-    """Bounded sample on rank 0: (1) the CPU restatement (oracle, test infrastructure)
-    timed on the host cores; (2) reward MAE of the HIP path vs that CPU reference on
-    identical inputs (a fresh sample env, outside the timed region)."""
+def host_cpus():
+    """CPUs this process may use and the share the harness grants it (OMP_NUM_THREADS
+    on the GPU box: one GPU's slice of the node)."""
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return affinity, (min(share, affinity) if share > 0 else affinity)
+
+
+def cpu_baseline(args, series, actions, H, torch):
+    """The CPU restatement (oracle/pmenv_oracle.c, OpenMP over envs; test infrastructure
+    used here as the timed baseline only) stepping the SAME workload shape — the full
+    per-GPU env count, the same synthetic bars and actions — on the host cores, in place."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle import OracleEnv
+    from pmenv import synth
+    from pmenv.config import EnvConfig
+
+    N, W, F = args.assets, args.window, args.features
+    B = series.shape[1]
+    S = min(args.cpu_sample_envs, B)
+    Hc = min(16, H)                                            # distinct days cycled (host memory)
+    obs = synth.window_from_series(series[:W, :S].contiguous(), W, F).cpu().numpy()
+    bars = series[W:W + Hc, :S].cpu().numpy()
+    acts = actions[:Hc, :S].cpu().numpy()
+    affinity, threads = host_cpus()
+
+    def run(envs, nthreads, budget_cpu_s):
+        env = OracleEnv(EnvConfig(num_envs=envs, num_assets=N, window=W, features=F, reward=args.reward,
+                                  commission=args.commission))
+        o = np.ascontiguousarray(obs[:envs])
+        b = [np.ascontiguousarray(bars[t, :envs]) for t in range(Hc)]
+        a = [np.ascontiguousarray(acts[t, :envs]) for t in range(Hc)]
+        env.reset(o)
+        env.step(a[0], o, bar=b[0], threads=nthreads)          # first touch of the state
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            env.step(a[steps % Hc], o, bar=b[steps % Hc], threads=nthreads)
+            steps += 1
+            el = time.perf_counter() - t0
+            if el * nthreads >= budget_cpu_s or steps >= 100000:
+                return envs * steps / el, steps, el
+
+    rate, steps, el = run(S, threads, args.cpu_budget_s)
+    s1 = min(S, 4096)
+    rate1, steps1, el1 = run(s1, 1, min(5.0, args.cpu_budget_s / 4))
+    return {
+        "value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+        "sample": f"{S} envs x {steps} steps of the same N={N} W={W} F={F} fused in-place step "
+                  f"(oracle/pmenv_oracle.c, OpenMP over envs, the bench's own synthetic bars and actions) "
+                  f"in {el:.2f} s wall on {threads} threads (~{el * threads:.0f} CPU-s) of {cpu_model()}",
+        "host_cpus": {"affinity": affinity, "nproc": os.cpu_count(), "threads_used": threads,
+                      "note": "threads = the box's CPU share for one GPU (OMP_NUM_THREADS set by the "
+                              "harness) when set, else every CPU in the affinity mask"},
+        "single_thread": {"value": rate1, "sample": f"{s1} envs x {steps1} steps in {el1:.2f} s on 1 thread"},
+    }
+
+
+def parity_check(args, rec, lo, torch):
+    """The parity leg's recorded GPU outputs vs the CPU restatement on the same inputs."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     from oracle import OracleEnv
     from pmenv.config import EnvConfig
 
+    obs, bars, acts, g_r, g_v, g_obs = rec
+    S = obs.shape[0]
     N, W, F = args.assets, args.window, args.features
-    S = min(args.mae_envs, args.envs_per_gpu)
-    T = args.mae_steps
-    ser = synth.series(W + T, S, N, env_offset=0, seed=args.seed, device=dev)
-    act = synth.actions(T, S, N, env_offset=0, seed=args.seed + 1, device=dev)
-    obs = synth.window_from_series(ser, W, F)
-    obs_h = obs.cpu().numpy().copy()
-    ser_h, act_h = ser.cpu().numpy(), act.cpu().numpy()
-    # HIP path on the sample
-    genv = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=dev,
-                      reward=args.reward, commission=args.commission)
-    genv.reset(obs)
-    g_r = []
-    for t in range(T):
-        r, _ = genv.step(act[t], obs, bar=ser[W + t])
-        g_r.append(r)
-    g_r = torch.stack(g_r).cpu().numpy().astype(np.float64)
-    g_v = genv.value.cpu().numpy()
-    # CPU restatement on the same inputs
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F, reward=args.reward,
-                               commission=args.commission))
-    cenv.reset(obs_h)
-    c_r = np.stack([cenv.step(act_h[t], obs_h, bar=ser_h[W + t], threads=threads)[0] for t in range(T)])
+    env = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F, reward=args.reward,
+                              commission=args.commission))
+    env.reset(obs)
+    _, threads = host_cpus()
+    c_r = np.stack([env.step(acts[t], obs, bar=bars[t], threads=threads)[0] for t in range(acts.shape[0])])
+    g_r = g_r.astype(np.float64)
     both_nan = np.isnan(g_r) & np.isnan(c_r)
-    mae = float(np.mean(np.where(both_nan, 0.0, np.abs(g_r - c_r))))
-    max_rel_value = float(np.max(np.abs(g_v / cenv.value - 1.0)))
-    obs_equal = bool(np.array_equal(obs.cpu().numpy(), obs_h))
-
-    # timing: bounded sample of the same workload shape
-    Sc = min(args.cpu_sample_envs, S)
-    tenv = OracleEnv(EnvConfig(num_envs=Sc, num_assets=N, window=W, features=F, reward=args.reward,
-                               commission=args.commission))
-    tobs = np.ascontiguousarray(obs_h[:Sc])
-    tenv.reset(tobs)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        t = steps % T
-        tenv.step(np.ascontiguousarray(act_h[t, :Sc]), tobs, bar=np.ascontiguousarray(ser_h[W + t, :Sc]),
-                  threads=threads)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el * threads >= args.cpu_budget_s or el >= args.cpu_budget_s or steps >= 100000:
-            break
-    rate = Sc * steps / el
-    return {
-        "value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
-        "sample": f"{Sc} envs x {steps} steps of the same N={N} W={W} F={F} fused step "
-                  f"(oracle/pmenv_oracle.c, OpenMP over envs) in {el:.2f} s wall on {threads} threads "
-                  f"(~{el * threads:.0f} CPU-s) of {cpu_model()}",
-    }, {"reward_mae": mae, "value_max_rel": max_rel_value, "obs_bit_exact": obs_equal,
-        "sample": f"{S} envs x {T} steps, HIP vs CPU restatement"}
+    err = np.where(both_nan, 0.0, np.abs(g_r - c_r))
+    return {"reward_mae": float(err.mean()),
+            "reward_max_rel": float(np.max(np.where(both_nan, 0.0, err / (np.abs(c_r) + 1e-9)))),
+            "value_max_rel": float(np.max(np.abs(g_v / env.value - 1.0))),
+            "obs_bit_exact": bool(np.array_equal(g_obs, obs)),
+            "sample": f"global envs {lo}..{lo + S - 1} of the timed handle x {acts.shape[0]} steps, "
+                      f"HIP vs CPU restatement"}
 
 
 def reference_golden_mae(dev, torch, TradingEnv):
@@ -156,7 +191,7 @@ def reference_golden_mae(dev, torch, TradingEnv):
     outputs: tests/golden/simplex_n30_w50_t256_{f32,f64}.npz were written by running
     zachramsey/pm-rl's env/sim/trading_env.py (tests/golden/gen_golden.py) on a
     256-day, 30-asset, 50-day-window case; here one env replays the same windows and
-    actions through the fused advance step (rank 0, outside the timed region)."""
+    actions through the fused advance step (rank 0, after the timed region)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import golden_util as gu
@@ -184,8 +219,16 @@ def reference_golden_mae(dev, torch, TradingEnv):
     return {"case": "simplex_n30_w50_t256 (reference env outputs recorded in tests/golden)", **out}
 
 
+def spread(us):
+    return {"min": min(us), "median": statistics.median(us), "max": max(us), "samples": len(us)}
+
+
 def main():
     args = parse()
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("PMENV_")}
+    if knobs:
+        sys.exit(f"bench.py refuses to time with PMENV_* variables set: {sorted(knobs)} "
+                 "(the product library reads none; A/B variants live in the tools build)")
     import torch
     import torch.distributed as dist
 
@@ -199,13 +242,12 @@ def main():
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
-        # RCCL ("nccl") over xGMI; PMENV_DIST_BACKEND=gloo lets several ranks share
-        # one GPU for functional rehearsal (RCCL refuses two ranks on one device)
-        backend = os.environ.get("PMENV_DIST_BACKEND", "nccl")
-        if backend == "nccl":
+        # RCCL ("nccl") over xGMI; --dist-backend gloo lets several ranks share one GPU for
+        # functional rehearsal (RCCL refuses two ranks on one device)
+        if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group("gloo")
 
     from pmenv import TradingEnv, synth, _abi
     lib = _abi.load()
@@ -219,13 +261,12 @@ def main():
     else:                                            # weak scaling: global env ids of this rank
         B = args.envs_per_gpu
         lo = rank * B
-    H = max(1, min(args.horizon, args.steps + args.warmup))
+    H = max(1, min(args.horizon, max(PARITY_STEPS, args.steps + args.warmup)))
     series = synth.series(H + W, B, N, env_offset=lo, seed=args.seed, device=dev)      # [H+W, B, N, 4]
     actions = synth.actions(H, B, N, env_offset=lo, seed=args.seed + 1, device=dev)     # [H, B, N]
     obs = synth.window_from_series(series, W, F)                                         # [B, N, W, F]
     env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev,
                      reward=args.reward, commission=args.commission)
-    env.reset(obs)
     obs_b = torch.empty_like(obs) if (args.windows == "double" or args.alt_steps > 0) else None
     reward = torch.empty(B, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -239,8 +280,10 @@ def main():
     args_a = _abi.PmenvStepArgs()
     args_a.reward = reward.data_ptr()
     ping = [obs, obs_b]
+    paths = env.step_path.split(" | ")              # "<double-buffered> (obs_out) | <in place> (in place)"
 
     def one_step(i, double, phase_events=None):
+        phased = "+" in paths[0 if double else -1]  # two launches: time the window stream on its own
         t = i % H
         src, dst = (ping[i % 2], ping[(i + 1) % 2]) if double else (obs, None)
         for a in (args_s, args_a):
@@ -250,7 +293,7 @@ def main():
         if phase_events is None:
             args_s.phases = 0
             rc = step_fn(h, ctypes.byref(args_s), sp)
-        else:
+        elif phased:
             # same two launches as phases=0, with an event between them so the
             # streaming kernel is timed on its own stream
             args_s.phases, args_a.phases = _abi.PHASE_SCALAR, _abi.PHASE_ADVANCE
@@ -258,9 +301,35 @@ def main():
             phase_events[0].record(stream)
             rc = rc or step_fn(h, ctypes.byref(args_a), sp)
             phase_events[1].record(stream)
+        else:                                        # one launch per step: time that launch
+            args_s.phases = 0
+            phase_events[0].record(stream)
+            rc = step_fn(h, ctypes.byref(args_s), sp)
+            phase_events[1].record(stream)
         if rc != 0:
             _abi.check(rc, h, "pmenv_step_ex")
 
+    # ---- 1. parity leg on the timed handle (every rank)
+    S = min(args.parity_envs if world == 1 else 256, B)
+    rec_obs0 = obs[:S].cpu().numpy()
+    env.reset(obs)
+    rec_r = torch.empty(PARITY_STEPS, S, dtype=torch.float32, device=dev)
+    for i in range(PARITY_STEPS):
+        one_step(i, False)
+        rec_r[i].copy_(reward[:S])
+    torch.cuda.synchronize(dev)
+    rec = (rec_obs0, series[W:W + PARITY_STEPS, :S].cpu().numpy() if PARITY_STEPS <= H else None,
+           actions[:PARITY_STEPS, :S].cpu().numpy() if PARITY_STEPS <= H else None,
+           rec_r.cpu().numpy(), env.value[:S].cpu().numpy(), obs[:S].cpu().numpy())
+    if PARITY_STEPS > H:                             # the leg cycled through the H resident days
+        idx = [t % H for t in range(PARITY_STEPS)]
+        rec = (rec[0], series[W:W + H, :S].cpu().numpy()[idx], actions[:, :S].cpu().numpy()[idx]) + rec[3:]
+    # back to the initial window and a fresh env state for the timed legs
+    obs.copy_(synth.window_from_series(series, W, F))
+    env.reset(obs)
+    torch.cuda.synchronize(dev)
+
+    # ---- 2. the timed region
     def timed(steps, warmup, double):
         for i in range(warmup):
             one_step(i, double)
@@ -268,8 +337,8 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        # the advance kernel is bracketed by HIP events on every EVENT_EVERY-th step of
-        # the timed region (each event pair costs the stream a few microseconds)
+        # the stream kernel (or the one-launch step) is bracketed by HIP events on every
+        # EVENT_EVERY-th step of the timed region (each event pair costs the stream a few us)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(0, steps, EVENT_EVERY)]
         t0 = time.perf_counter()
@@ -280,11 +349,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
-        k_ms = [a.elapsed_time(b) for a, b in ev]
-        return el, sum(k_ms) / len(k_ms) / 1e3
+        return el, [a.elapsed_time(b) * 1e3 for a, b in ev]
 
     double = args.windows == "double"
-    elapsed, kern_avg_s = timed(args.steps, args.warmup, double)
+    elapsed, k_us = timed(args.steps, args.warmup, double)
+    kern_avg_s = sum(k_us) / len(k_us) / 1e6
     alt = None
     if args.alt_steps > 0:
         # the other window mode, continuing from the latest window
@@ -293,7 +362,8 @@ def main():
         a_el, a_k = timed(args.alt_steps, 2, not double)
         alt = {"windows": "inplace" if double else "double",
                "env_steps_per_s_per_gpu": B * args.alt_steps / a_el,
-               "ms_per_step": a_el / args.alt_steps * 1e3, "advance_kernel_avg_us": a_k * 1e6}
+               "ms_per_step": a_el / args.alt_steps * 1e3, "kernel_avg_us": sum(a_k) / len(a_k),
+               "kernel_us": spread(a_k)}
 
     collective = None
     if world > 1:
@@ -320,36 +390,37 @@ def main():
                       "us_per_update": c_us, "count_all_ranks": n_all, "normalised_finite": bool(torch.isfinite(normed).all())}
     nonfinite = env.nonfinite_count()
 
-    path = env.step_path
-    if "step_advance_lds_kernel" in path:
-        advance_kernel = "step_advance_lds_kernel"
-    elif double and "advance_flat_wg_kernel" in path:
-        advance_kernel = "advance_flat_wg_kernel"
-    elif double and "advance_flat_kernel" in path:
-        advance_kernel = "advance_flat_kernel"
-    elif not double and "advance_flat_inplace_kernel" in path:
-        advance_kernel = "advance_flat_inplace_kernel"
-    else:
-        advance_kernel = "advance_rows_kernel"
+    # ---- 3. checks and baselines (after the timed region)
+    parity = parity_check(args, rec, lo, torch)
+    if world > 1:
+        t = torch.tensor([parity["reward_max_rel"], parity["value_max_rel"], 0.0 if parity["obs_bit_exact"] else 1.0],
+                         dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        parity.update({"reward_max_rel_all_ranks": float(t[0]), "value_max_rel_all_ranks": float(t[1]),
+                       "obs_bit_exact_all_ranks": float(t[2]) == 0.0})
+    cpu = ref_gold = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cpu = cpu_baseline(args, series, actions, H, torch)
+        ref_gold = reference_golden_mae(dev, torch, TradingEnv)
+
+    kernel = paths[0 if double else -1].split(" (")[0].split("+")[-1]
     total_env_steps = (args.global_envs or world * B) * args.steps
     value = total_env_steps / elapsed
     bstep = step_bytes(N, W, F)
     achieved = bstep * B / kern_avg_s / 1e9
+    achieved_step = bstep * B / (elapsed / args.steps) / 1e9
+    window_bytes = B * N * W * F * 4
     traffic = None
     try:
         pmc = json.load(open(args.pmc_file))
         # PMC passes of the same kernel at the same workload only
-        if pmc.get("workload") == [B, N, W, F] and f"::{advance_kernel}<" in pmc.get("dominant_kernel", ""):
+        if pmc.get("workload") == [B, N, W, F] and f"::{kernel}<" in pmc.get("dominant_kernel", ""):
             traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 
-    cpu = mae = ref_gold = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu, mae = cpu_baseline_and_mae(args, dev, torch, synth, TradingEnv)
-        ref_gold = reference_golden_mae(dev, torch, TradingEnv)
-
     if rank == 0:
+        l3 = window_bytes * (2 if double else 1) <= L3_BYTES
         line = {
             "metric": "env-steps/sec (whole node) at 65k envs x 30 assets; reward MAE vs CPU ref",
             "value": value,
@@ -374,15 +445,20 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": advance_kernel, "kernel_avg_us": kern_avg_s * 1e6,
+                "kernel": kernel, "kernel_avg_us": kern_avg_s * 1e6, "kernel_us": spread(k_us),
                 "bytes_per_env_step": bstep,
+                "achieved_step": achieved_step, "frac_step": achieved_step / HBM_PEAK_GBS,
+                "l3_resident": l3,
+                "note": ("the window (x2 double-buffered) fits the 256 MiB Infinity Cache: frac is not an HBM fraction"
+                         if l3 else "window streams through HBM (larger than the 256 MiB Infinity Cache)"),
             },
             "cpu_baseline": cpu,
-            "reward_mae": None if mae is None else mae["reward_mae"],
-            "parity_sample": mae,
+            "reward_mae": parity["reward_mae"],
+            "parity_sample": parity,
             "reference_goldens": ref_gold,
             "nonfinite_envs": nonfinite,
             "step_path": env.step_path,
+            "knobs": knobs,
             "alt": alt,
             "collective": collective,
         }

@@ -70,10 +70,15 @@ typedef enum pmenv_ring_mode {
     PMENV_RING_CHRONO = 1   /* intended: oldest..newest always */
 } pmenv_ring_mode;
 
-/* Which value the return uses (trading_env.py:75,88). */
+/* Which value the return uses (trading_env.py:75,88). The reference has two answers:
+ * step() takes log(value / (mu * V_prev)) (trading_env.py:75,88,99 — the commission is
+ * excluded), while env/reward.py:20-31 forms its returns / sharpe_ratio from
+ * info["values"], i.e. V_t / V_{t-1} (trading_env.py:80 — commission included). AUTO,
+ * the default, follows each: gross for the log-return reward, net for the others. */
 typedef enum pmenv_ret_mode {
-    PMENV_RET_GROSS = 0, /* reference: ret = value / (mu * V_prev), i.e. excludes commission */
-    PMENV_RET_NET = 1    /* ret = value / V_prev, includes commission */
+    PMENV_RET_GROSS = 0, /* ret = value / (mu * V_prev): excludes commission (trading_env.py:88) */
+    PMENV_RET_NET = 1,   /* ret = value / V_prev: includes commission (reward.py:20-31 over info["values"]) */
+    PMENV_RET_AUTO = 2   /* GROSS for PMENV_REWARD_LOG_RETURN, NET for every other kind (resolved at create) */
 } pmenv_ret_mode;
 
 typedef struct pmenv_cfg {
@@ -85,7 +90,7 @@ typedef struct pmenv_cfg {
     int32_t reward_kind;    /* pmenv_reward_kind */
     int32_t norm_mode;      /* pmenv_norm_mode */
     int32_t ring_mode;      /* pmenv_ring_mode */
-    int32_t ret_mode;       /* pmenv_ret_mode */
+    int32_t ret_mode;       /* pmenv_ret_mode (AUTO is resolved at create; pmenv_get_cfg returns the result) */
     int32_t mu_max_iter;    /* cap on the commission fixed point (trading_env.py:70 has none) */
     double init_cash;       /* config/base.py:47 INITIAL_CASH = 25000 */
     double commission;      /* config/base.py:48 COMISSION = 0.0 */
@@ -172,8 +177,24 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
                float* obs, float* reward, hipStream_t stream);
 
 /* Which kernels the advance path launches for this handle's shape (diagnostics):
- * "scalar_step_kernel+advance_rows_kernel" or "step_advance_lds_kernel". */
+ * "<obs_out path> (obs_out) | <in-place path> (in place)", each either
+ * "step_env_kernel" (the whole step in one launch) or "<scalar step>+<window stream>"
+ * (two launches); or "step_advance_lds_kernel" (single-launch fallback, any F). */
 const char* pmenv_step_path(const pmenv* h);
+
+/* Advance-mode step implementation. AUTO (the default) picks per shape and window
+ * mode; ONE_LAUNCH forces step_env_kernel (one workgroup per env: F = 5, W >= 2,
+ * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
+ * kernel followed by the window stream (F = 5, 16-B granular env windows). Returns
+ * PMENV_ERR_ARG (handle unchanged) when the shape does not fit the requested path.
+ * Results are the same either way up to the last bits of the f64 sums (the two
+ * scalar-step forms reduce in different orders). */
+typedef enum pmenv_step_path_kind {
+    PMENV_STEP_PATH_AUTO = 0,
+    PMENV_STEP_PATH_ONE_LAUNCH = 1,
+    PMENV_STEP_PATH_TWO_LAUNCH = 2
+} pmenv_step_path_kind;
+int pmenv_set_step_path(pmenv* h, int32_t path);
 
 /* Device pointer to the env-owned portfolio values [B] f64 (TradingEnv.value). */
 double* pmenv_value(pmenv* h);

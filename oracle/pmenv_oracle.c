@@ -24,6 +24,10 @@
 or_env* or_create(const pmenv_cfg* cfg) {
     or_env* e = (or_env*)calloc(1, sizeof(or_env));
     e->cfg = *cfg;
+    /* PMENV_RET_AUTO: trading_env.py:88 (gross) for the log-return reward,
+     * env/reward.py:20-31 over info["values"] (net) for the others */
+    if (e->cfg.ret_mode == PMENV_RET_AUTO)
+        e->cfg.ret_mode = cfg->reward_kind == PMENV_REWARD_LOG_RETURN ? PMENV_RET_GROSS : PMENV_RET_NET;
     size_t B = (size_t)cfg->num_envs, W = (size_t)cfg->window, N = (size_t)cfg->num_assets;
     e->value = (double*)calloc(B, sizeof(double));
     e->k = (int32_t*)calloc(B, sizeof(int32_t));

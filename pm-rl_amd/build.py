@@ -1,6 +1,6 @@
 """Build the in-tree native libraries.
 
-    python pm-rl_amd/build.py            # libpmenv.so (HIP, gfx950) + oracle/liboracle.so
+    python pm-rl_amd/build.py            # libpmenv.so (HIP, gfx950), tools/libpmenv_ab.so, oracle/liboracle.so
 
 libpmenv.so is the product (the C ABI of include/pmenv.h). oracle/liboracle.so is
 the CPU parity checker (test infrastructure). Both are built in place so they
@@ -13,6 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "pmenv", "libpmenv.so")
+AB_LIB = os.path.join(ROOT, "tools", "libpmenv_ab.so")
 SRC = os.path.join(HERE, "csrc", "pmenv.hip")
 ORACLE_SRC = os.path.join(ROOT, "oracle", "pmenv_oracle.c")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
@@ -32,15 +33,19 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
-def build_pmenv(force=False):
+def build_pmenv(force=False, ab=False):
+    """The product library; ab=True: the tools build (-DPMENV_AB -> tools/libpmenv_ab.so),
+    which alone reads the PMENV_* A/B knobs and carries the measured alternatives and the
+    timing-only ablations."""
+    out = AB_LIB if ab else LIB
     deps = [os.path.join(ROOT, "include", "pmenv.h")] + [
         os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
-    if not force and not _stale(LIB, SRC, *deps, __file__):
-        return LIB
+    if not force and not _stale(out, SRC, *deps, __file__):
+        return out
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-          "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
-          "-o", LIB, SRC])
-    return LIB
+          "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
+         + (["-DPMENV_AB"] if ab else []) + ["-o", out, SRC])
+    return out
 
 
 def build_oracle(force=False):
@@ -54,6 +59,7 @@ def build_oracle(force=False):
 
 def build_all(force=False):
     build_pmenv(force)
+    build_pmenv(force, ab=True)
     build_oracle(force)
 
 

@@ -956,6 +956,14 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams 
     flat_wg_body<BLOCK, V, POL, false, ABL>(p, qtot, sh4);
 }
 
+// the same kernel held to 80 SGPRs (8 waves per SIMD instead of 7; tools A/B)
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void advance_flat_inplace_s80_kernel(
+    StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, false, 0>(p, qtot, sh4);
+}
+
 // the double-buffered twin of advance_flat_inplace_kernel (same body, OUT = true)
 template <int BLOCK, int V, int POL>
 __global__ __launch_bounds__(BLOCK) void advance_flat_wg_kernel(StepParams p, uint32_t qtot) {

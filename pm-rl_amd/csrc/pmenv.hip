@@ -1,10 +1,17 @@
 // pmenv.hip — host side and C ABI (include/pmenv.h) of the MI355X-native
-// vectorised portfolio environment. Device code lives in env_step.h (step / reset),
-// data.h (synthetic market data) and rollout.h (GAE, moments).
+// vectorised portfolio environment. Device code lives in step_env.h (the one-launch
+// step), env_step.h (scalar step, window streams, reset, fallbacks), scalar_vec.h
+// (packed scalar step), data.h (synthetic market data), rollout.h / gae_vec.h (GAE,
+// moments), replay.h (replay gather, metrics) and trainer.h (batched reward).
 //
 // Every entry point enqueues on the caller's stream and never synchronises,
 // allocates or frees (graph-capturable), except create / destroy / the explicit
 // synchronous queries documented in the header.
+//
+// Kernel choice is a function of the shape only (and of pmenv_set_step_path). The
+// A/B variants measured while choosing — other geometries, cache policies, the
+// timing-only ablations that skip work — exist only in the tools build
+// (-DPMENV_AB -> tools/libpmenv_ab.so), which alone reads the PMENV_* knobs.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -17,12 +24,24 @@
 #include "data.h"
 #include "env_step.h"
 #include "scalar_vec.h"
+#include "step_env.h"
 #include "rollout.h"
 #include "gae_vec.h"
 #include "replay.h"
 #include "trainer.h"
 
 using namespace pmenv_dev;
+
+#ifdef PMENV_AB
+static const char* ab_knob(const char* name) { return getenv(name); }
+static int ab_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+#else
+static inline const char* ab_knob(const char*) { return nullptr; }
+static inline int ab_int(const char*, int dflt) { return dflt; }
+#endif
 
 struct pmenv {
     pmenv_cfg cfg;
@@ -43,24 +62,33 @@ struct pmenv {
     bool vec;
     size_t lds_tile, lds_surface;
     // two-launch streaming path geometry
-    bool streaming;       // scalar_step_kernel + advance_rows_kernel
-    int unit_rows, units_per_env, stream_vec;          // in-place advance
-    int unit_rows_db, units_per_env_db, stream_vec_db; // double-buffered advance (obs_out)
-    int stream_block, stream_block_db;                 // threads per advance workgroup (128 | 256 | 512)
-    int stream_pol;       // cache policy of the window stream (advance_rows_kernel POL)
-    int fused_vec;        // float4 per thread of the fused one-launch step (512 threads, whole env)
-    bool flat;            // double-buffered advance as the flat 16-B stream (advance_flat_kernel)
+    bool streaming;       // scalar step kernel + window stream
+    int unit_rows, units_per_env, stream_vec;          // row-kernel advance in place
+    int unit_rows_db, units_per_env_db, stream_vec_db; // row-kernel advance double-buffered (obs_out)
+    int stream_block, stream_block_db;                 // threads per row-kernel workgroup (tools: 128 | 256)
+    int stream_pol;       // cache policy of the row kernel
+    bool flat;            // double-buffered advance as the flat 16-B stream
     int flat_block, flat_pol, flat_ip_pol;   // cache policy: double-buffered / in-place stream
     bool flat_inplace;    // in-place advance as the flat stream + halo (advance_flat_inplace_kernel)
     int flat_ip_block, flat_ip_vec;   // threads per workgroup, chunks per thread
-    bool flat_db_wg;      // double-buffered advance in the workgroup form (advance_flat_wg_kernel)
+    bool flat_db_wg;      // double-buffered flat stream in the workgroup form (tools: ds_bpermute form)
     float* halo;          // [halo_wgs][2] float4: first two chunks of every in-place flat workgroup
     uint32_t halo_wgs, flat_qtot;
     int scalar_scratch_floats;
     int k1_groups;        // env groups per wave in scalar_step_reg_kernel
     int k1_vec;           // scalar_step_vec_kernel shape 100 * L + A (0: register / LDS form)
-    int fused;            // PMENV_FUSE_* bits: which windows take the one-launch fused step
-    int ablate;           // PMENV_ABLATE timing-only variants of advance_rows_kernel (0 = product)
+    // one launch per step
+    bool one_ok;          // the shape fits step_env_kernel
+    int one_auto;         // PMENV_FUSE_* bits the automatic choice gives step_env_kernel
+    int one;              // PMENV_FUSE_* bits: which windows take step_env_kernel now
+    int one_v, one_waves; // step_env_kernel: chunks per lane, waves per workgroup
+    uint32_t per4;        // 16-B chunks per env window
+    int path;             // pmenv_step_path_kind
+    // tools build only
+    int fused;            // PMENV_FUSE_* bits: advance_rows_kernel<fused> (PMENV_FUSED)
+    int fused_vec;
+    int ablate;           // PMENV_ABLATE timing-only variants
+    bool one_s80, flat_s80;
     size_t lds_scalar, lds_stream;
     char err[512];
 };
@@ -124,19 +152,18 @@ int check_launch(pmenv* h, const char* what) {
     return PMENV_OK;
 }
 
-// Geometry of the streaming path: units of R whole asset rows per `block`-thread
-// workgroup, R*W*F floats <= 4*block*V (V float4 per thread) and R*W*F % 4 == 0 so
-// every unit starts 16-B aligned. `v_order` lists V in preference order. Returns
-// false when the shape needs the LDS fallback. Measured on MI355X at the BASELINE
-// shape (tools/ab_advance.py, interleaved rounds in one process): see the defaults
-// chosen in pmenv_create.
+constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
+
+// Geometry of the row-kernel stream (the fallback of the flat stream): units of R
+// whole asset rows per `block`-thread workgroup, R*W*F floats <= 4*block*V (V float4
+// per thread) and R*W*F % 4 == 0 so every unit starts 16-B aligned. `v_order` lists V
+// in preference order. Returns false when the shape needs the LDS fallback.
 bool plan_streaming(const pmenv_cfg& c, const int* v_order, int block, int* unit_rows, int* vec_per_thread) {
     const int64_t WF = (int64_t)c.window * c.features;
     if (c.features != 5 || ((int64_t)c.num_assets * WF) % 4 != 0) return false;
     int align = 1;                       // rows per unit must be a multiple of this
     while ((align * WF) % 4 != 0) ++align;
-    int want = 0;
-    if (const char* knob = getenv("PMENV_UNIT_ROWS")) want = atoi(knob);   // tuning knob
+    const int want = ab_int("PMENV_UNIT_ROWS", 0);
     static const int kAscending[3] = {1, 2, 4};
     if (want > 0) v_order = kAscending;   // a forced unit takes the fewest float4 per thread that hold it
     for (int vi = 0; vi < 3; ++vi) {
@@ -158,6 +185,8 @@ bool plan_streaming(const pmenv_cfg& c, const int* v_order, int block, int* unit
     return false;
 }
 
+// ---------------------------------------------------------------- launchers
+// the row-kernel stream (fallback of the flat stream: W = 1, or windows past 2^31 chunks)
 template <int BLOCK, int V, int ABL, int POL>
 void launch_advance_bv(const StepParams& p, unsigned grid, hipStream_t stream) {
     if (p.obs_out == p.obs)
@@ -173,39 +202,47 @@ void launch_advance_b(int vec, const StepParams& p, unsigned grid, hipStream_t s
     else launch_advance_bv<BLOCK, 4, ABL, POL>(p, grid, stream);
 }
 
-template <int BLOCK>
-void launch_flat_b(int pol, const StepParams& p, unsigned grid, uint32_t qtot, hipStream_t stream) {
-    if (pol == 1) advance_flat_kernel<BLOCK, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else if (pol == 2) advance_flat_kernel<BLOCK, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else advance_flat_kernel<BLOCK, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
+template <int POL>
+void launch_advance_p(int block, int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
+#ifdef PMENV_AB
+    if (block == 128) { launch_advance_b<128, 0, POL>(vec, p, grid, stream); return; }
+    if (block == 256) { launch_advance_b<256, 0, POL>(vec, p, grid, stream); return; }
+#endif
+    (void)block;
+    launch_advance_b<kStreamBlock, 0, POL>(vec, p, grid, stream);
 }
 
+// the double-buffered flat stream: the workgroup (LDS) form, 512 threads x 2 chunks
 void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
     const pmenv_cfg& c = h->cfg;
     const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
     const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
     p.div_units = make_fastdiv(per4);
-    if (h->flat_db_wg) {          // workgroup (LDS) form, 512 threads x 2 chunks
-        const unsigned g = (unsigned)((qtot + 1023) / 1024);
-        if (h->flat_pol == 2) advance_flat_wg_kernel<512, 2, 2><<<g, 512, 0, stream>>>(p, qtot);
-        else if (h->flat_pol == 0) advance_flat_wg_kernel<512, 2, 0><<<g, 512, 0, stream>>>(p, qtot);
-        else advance_flat_wg_kernel<512, 2, 1><<<g, 512, 0, stream>>>(p, qtot);
+#ifdef PMENV_AB
+    if (!h->flat_db_wg) {        // the ds_bpermute form, one chunk per thread
+        const int bk = h->flat_block;
+        const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
+#define PMENV_FLATB(BK)                                                                             \
+        if (bk == BK) {                                                                             \
+            if (h->flat_pol == 1) advance_flat_kernel<BK, 1><<<grid, BK, 0, stream>>>(p, qtot);      \
+            else if (h->flat_pol == 2) advance_flat_kernel<BK, 2><<<grid, BK, 0, stream>>>(p, qtot); \
+            else advance_flat_kernel<BK, 0><<<grid, BK, 0, stream>>>(p, qtot);                       \
+            return;                                                                                 \
+        }
+        PMENV_FLATB(128) PMENV_FLATB(512) PMENV_FLATB(256)
+#undef PMENV_FLATB
+    }
+    if (h->flat_pol == 2) {
+        advance_flat_wg_kernel<512, 2, 2><<<(unsigned)((qtot + 1023) / 1024), 512, 0, stream>>>(p, qtot);
         return;
     }
-    const int bk = h->flat_block;
-    const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
-    if (bk == 128) launch_flat_b<128>(h->flat_pol, p, grid, qtot, stream);
-    else if (bk == 512) launch_flat_b<512>(h->flat_pol, p, grid, qtot, stream);
-    else launch_flat_b<256>(h->flat_pol, p, grid, qtot, stream);
+#endif
+    const unsigned g = (unsigned)((qtot + 1023) / 1024);
+    if (h->flat_pol == 0) advance_flat_wg_kernel<512, 2, 0><<<g, 512, 0, stream>>>(p, qtot);
+    else advance_flat_wg_kernel<512, 2, 1><<<g, 512, 0, stream>>>(p, qtot);
 }
 
-template <int BLOCK, int V>
-void launch_flat_ip_b(int pol, const StepParams& p, unsigned grid, uint32_t qtot, hipStream_t stream) {
-    if (pol == 1) advance_flat_inplace_kernel<BLOCK, V, 1><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else if (pol == 2) advance_flat_inplace_kernel<BLOCK, V, 2><<<grid, BLOCK, 0, stream>>>(p, qtot);
-    else advance_flat_inplace_kernel<BLOCK, V, 0><<<grid, BLOCK, 0, stream>>>(p, qtot);
-}
-
+// the in-place flat stream: 512 threads x 2 chunks, the halo copied by the scalar step
 void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
     const pmenv_cfg& c = h->cfg;
     const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
@@ -213,37 +250,83 @@ void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
     p.halo = h->halo;
     const int cpw = h->flat_ip_block * h->flat_ip_vec;
     const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
+#ifdef PMENV_AB
     const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
-    switch (key) {
-    case 2561: launch_flat_ip_b<256, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
-    case 2562: launch_flat_ip_b<256, 2>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
-    case 2564: launch_flat_ip_b<256, 4>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
-    case 5121: launch_flat_ip_b<512, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
-    case 10241: launch_flat_ip_b<1024, 1>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
-    default: launch_flat_ip_b<512, 2>(h->flat_ip_pol, p, grid, h->flat_qtot, stream); break;
+    const int pol = h->flat_ip_pol;
+    if (h->ablate >= 64 && h->ablate < 128) {     // timing-only ablations (PMENV_ABLATE = 64 + SKIP bits)
+        const unsigned g1 = (unsigned)((h->flat_qtot + 511) / 512);
+#define PMENV_ABL(X) case 64 + X: advance_flat_inplace_kernel<512, 1, 1, X><<<g1, 512, 0, stream>>>(p, h->flat_qtot); break;
+        switch (h->ablate) {
+            PMENV_ABL(1) PMENV_ABL(2) PMENV_ABL(4) PMENV_ABL(6) PMENV_ABL(15) PMENV_ABL(31) PMENV_ABL(32)
+            PMENV_ABL(33)
+            default: break;
+        }
+#undef PMENV_ABL
+        return;
     }
+    if (h->flat_s80 && key == 5122) {
+        if (pol == 1) advance_flat_inplace_s80_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
+        else advance_flat_inplace_s80_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
+        return;
+    }
+#define PMENV_FIP(BK, V)                                                                                      \
+    if (key == BK * 10 + V) {                                                                                 \
+        if (pol == 1) advance_flat_inplace_kernel<BK, V, 1><<<grid, BK, 0, stream>>>(p, h->flat_qtot);         \
+        else if (pol == 2) advance_flat_inplace_kernel<BK, V, 2><<<grid, BK, 0, stream>>>(p, h->flat_qtot);    \
+        else advance_flat_inplace_kernel<BK, V, 0><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                  \
+        return;                                                                                               \
+    }
+    PMENV_FIP(256, 1) PMENV_FIP(256, 2) PMENV_FIP(256, 4) PMENV_FIP(512, 1) PMENV_FIP(1024, 1)
+#undef PMENV_FIP
+#endif
+    if (h->flat_ip_pol == 1) advance_flat_inplace_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
+    else advance_flat_inplace_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
 }
 
-template <int POL>
-void launch_advance_p(int block, int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
-    if (block == 128) launch_advance_b<128, 0, POL>(vec, p, grid, stream);
-    else if (block == 256) launch_advance_b<256, 0, POL>(vec, p, grid, stream);
-    else launch_advance_b<512, 0, POL>(vec, p, grid, stream);
+// the second launch of the two-launch step
+void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
+    const bool db = p.obs_out != p.obs;
+    if (db && h->flat && !h->ablate) {
+        launch_flat(h, p, stream);
+        return;
+    }
+    if (!db && h->flat_inplace && (!h->ablate || (h->ablate >= 64 && h->ablate < 128))) {
+        launch_flat_inplace(h, p, stream);
+        return;
+    }
+    p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
+    p.units_per_env = db ? h->units_per_env_db : h->units_per_env;
+    p.div_units = make_fastdiv((uint32_t)p.units_per_env);
+    const int vec = db ? h->stream_vec_db : h->stream_vec;
+    const int block = db ? h->stream_block_db : h->stream_block;
+    const unsigned grid = (unsigned)(h->cfg.num_envs * p.units_per_env);
+#ifdef PMENV_AB
+    switch (h->ablate) {     // timing-only builds: 512-thread geometry, default policy
+    case 1: launch_advance_b<kStreamBlock, 1, 0>(vec, p, grid, stream); return;
+    case 2: launch_advance_b<kStreamBlock, 2, 0>(vec, p, grid, stream); return;
+    case 3: launch_advance_b<kStreamBlock, 3, 0>(vec, p, grid, stream); return;
+    case 7: launch_advance_b<kStreamBlock, 7, 0>(vec, p, grid, stream); return;
+    default: break;
+    }
+    if (h->stream_pol == 2) { launch_advance_p<2>(block, vec, p, grid, stream); return; }
+#endif
+    if (h->stream_pol == 1) launch_advance_p<1>(block, vec, p, grid, stream);
+    else launch_advance_p<0>(block, vec, p, grid, stream);
 }
 
-constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
-
+// K1, the first launch of the two-launch step: the register form (N <= 64)
 template <int L>
 void launch_scalar_reg_l(int groups, const StepParams& p, hipStream_t stream) {
     const int per_wave = (64 / L) * groups;
     const unsigned waves = (unsigned)((p.B + per_wave - 1) / per_wave);
     const unsigned grid = (waves + 3) / 4;
-    if (groups == 4) scalar_step_reg_kernel<L, 4><<<grid, 256, 0, stream>>>(p);
-    else if (groups == 2) scalar_step_reg_kernel<L, 2><<<grid, 256, 0, stream>>>(p);
-    else scalar_step_reg_kernel<L, 1><<<grid, 256, 0, stream>>>(p);
+#ifdef PMENV_AB
+    if (groups == 4) { scalar_step_reg_kernel<L, 4><<<grid, 256, 0, stream>>>(p); return; }
+    if (groups == 2) { scalar_step_reg_kernel<L, 2><<<grid, 256, 0, stream>>>(p); return; }
+#endif
+    scalar_step_reg_kernel<L, 1><<<grid, 256, 0, stream>>>(p);
 }
 
-// K1 register form (N <= 64): two envs per wave up to 32 assets
 void launch_scalar_reg(const pmenv* h, const StepParams& p, hipStream_t stream) {
     if (p.N <= 32) launch_scalar_reg_l<32>(h->k1_groups, p, stream);
     else launch_scalar_reg_l<64>(h->k1_groups, p, stream);
@@ -259,32 +342,30 @@ void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
     scalar_step_vec_kernel<L, A, STR><<<(waves + 3) / 4, 256, 0, stream>>>(p);
 }
 
-constexpr int kK1Vec[] = {801, 802, 804, 1601, 1602, 1604, 1608, 3202, 3204,
-                          kK1Str + 3202, kK1Str + 3204, kK1Str + 6402, kK1Str + 6404, kK1Str + 6408};
-
 bool launch_scalar_vec(int vec, const StepParams& p, hipStream_t stream) {
-    switch (vec) {
+    switch (vec) {   // the shapes pick_k1_vec chooses per asset count
     case 801: launch_scalar_vec_la<8, 1, false>(p, stream); return true;
     case 802: launch_scalar_vec_la<8, 2, false>(p, stream); return true;
-    case 804: launch_scalar_vec_la<8, 4, false>(p, stream); return true;
-    case 1601: launch_scalar_vec_la<16, 1, false>(p, stream); return true;
     case 1602: launch_scalar_vec_la<16, 2, false>(p, stream); return true;
     case 1604: launch_scalar_vec_la<16, 4, false>(p, stream); return true;
+    case kK1Str + 6402: launch_scalar_vec_la<64, 2, true>(p, stream); return true;
+    case kK1Str + 6404: launch_scalar_vec_la<64, 4, true>(p, stream); return true;
+    case kK1Str + 6408: launch_scalar_vec_la<64, 8, true>(p, stream); return true;
+#ifdef PMENV_AB
+    case 804: launch_scalar_vec_la<8, 4, false>(p, stream); return true;
+    case 1601: launch_scalar_vec_la<16, 1, false>(p, stream); return true;
     case 1608: launch_scalar_vec_la<16, 8, false>(p, stream); return true;
     case 3202: launch_scalar_vec_la<32, 2, false>(p, stream); return true;
     case 3204: launch_scalar_vec_la<32, 4, false>(p, stream); return true;
     case kK1Str + 3202: launch_scalar_vec_la<32, 2, true>(p, stream); return true;
     case kK1Str + 3204: launch_scalar_vec_la<32, 4, true>(p, stream); return true;
-    case kK1Str + 6402: launch_scalar_vec_la<64, 2, true>(p, stream); return true;
-    case kK1Str + 6404: launch_scalar_vec_la<64, 4, true>(p, stream); return true;
-    case kK1Str + 6408: launch_scalar_vec_la<64, 8, true>(p, stream); return true;
+#endif
     default: return false;
     }
 }
 
-// K1 shape per asset count, or the PMENV_K1 knob ("reg" | "LxA" | "LxAs" strided,
-// e.g. "16x2", "64x8s"; an unbuilt or too-small shape keeps the default). 0: the
-// register form (N <= 64) or the LDS form (N > 512).
+// K1 shape per asset count (tools build: the PMENV_K1 knob "reg" | "LxA" | "LxAs"
+// strided, e.g. "16x2", "64x8s"). 0: the register form (N <= 64) or the LDS form (N > 512).
 int pick_k1_vec(const pmenv_cfg& c) {
     const int N = c.num_assets;
     if ((int64_t)c.num_envs * N * 4 >= (1ll << 32)) return 0;     // descriptors span the [B*N] arrays
@@ -296,7 +377,9 @@ int pick_k1_vec(const pmenv_cfg& c) {
     else if (N <= 128) v = kK1Str + 6402;
     else if (N <= 256) v = kK1Str + 6404;
     else if (N <= 512) v = kK1Str + 6408;
-    if (const char* knob = getenv("PMENV_K1")) {
+    if (const char* knob = ab_knob("PMENV_K1")) {
+        static const int kK1Vec[] = {801, 802, 804, 1601, 1602, 1604, 1608, 3202, 3204,
+                                     kK1Str + 3202, kK1Str + 3204, kK1Str + 6402, kK1Str + 6404, kK1Str + 6408};
         int L = 0, A = 0;
         char s = 0;
         if (!strcmp(knob, "reg")) return 0;
@@ -309,8 +392,76 @@ int pick_k1_vec(const pmenv_cfg& c) {
     return v;
 }
 
-// one launch per step: whole-env units (the double-buffered geometry), scalar step
-// inside the workgroup (N <= 64)
+// the first launch of the two-launch step (with the in-place stream's halo copy)
+int launch_scalar(pmenv* h, StepParams p, hipStream_t stream) {
+    if (p.obs_out == p.obs && h->flat_inplace && !h->ablate) {   // the in-place advance's halo
+        p.halo = h->halo;
+        p.halo_wgs = h->halo_wgs;
+        p.halo_block = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
+        p.halo_qtot = h->flat_qtot;
+    }
+    const int N = h->cfg.num_assets;
+    if (h->k1_vec && launch_scalar_vec(h->k1_vec, p, stream)) {
+        // packed form
+    } else if (N <= 64) {
+        launch_scalar_reg(h, p, stream);
+    } else {
+        const int B = h->cfg.num_envs;
+        scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar, stream>>>(
+            p, h->scalar_scratch_floats);
+    }
+    return check_launch(h, "scalar_step_kernel");
+}
+
+// the whole step in one launch, one workgroup per env (step_env.h)
+template <int V>
+void launch_one_v(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const bool out = p.obs_out != p.obs;
+    const int pol = out ? h->flat_pol : h->flat_ip_pol;
+    const unsigned threads = 64u * (unsigned)h->one_waves;
+    const size_t lds = ((size_t)threads * V + 2) * 16;
+    const unsigned grid = (unsigned)h->cfg.num_envs;
+#ifdef PMENV_AB
+    if (h->ablate == 128 || h->ablate == 130) {    // timing-only: no scalar step / unconditional side reads
+        if (h->ablate == 128 && out) step_env_kernel<V, true, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (h->ablate == 128) step_env_kernel<V, false, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (out) step_env_kernel<V, true, 1, 2><<<grid, threads, lds, stream>>>(p, h->per4);
+        else step_env_kernel<V, false, 1, 2><<<grid, threads, lds, stream>>>(p, h->per4);
+        return;
+    }
+    if (h->one_s80) {
+        if (out && pol == 1) step_env_s80_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (out) step_env_s80_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (pol == 1) step_env_s80_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else step_env_s80_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+        return;
+    }
+#endif
+    if (out) {
+        if (pol == 1) step_env_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else step_env_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+    } else {
+        if (pol == 1) step_env_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else step_env_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+    }
+}
+
+void launch_one(const pmenv* h, const StepParams& p, hipStream_t stream) {
+#ifdef PMENV_AB
+    switch (h->one_v) {
+    case 1: launch_one_v<1>(h, p, stream); return;
+    case 2: launch_one_v<2>(h, p, stream); return;
+    case 3: launch_one_v<3>(h, p, stream); return;
+    case 6: launch_one_v<6>(h, p, stream); return;
+    case 8: launch_one_v<8>(h, p, stream); return;
+    default: break;
+    }
+#endif
+    launch_one_v<4>(h, p, stream);
+}
+
+#ifdef PMENV_AB
+// tools build: the previous one-launch form (whole-env row units, scalar step inside)
 void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
     p.unit_rows = h->cfg.num_assets;
     p.units_per_env = 1;
@@ -325,48 +476,13 @@ void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
     else { PMENV_FUSED_LAUNCH(4) }
 #undef PMENV_FUSED_LAUNCH
 }
+#endif
 
-// ablation builds are selected only by the PMENV_ABLATE knob (timing studies)
-void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
-    const bool db = p.obs_out != p.obs;
-    if (db && h->flat && !h->ablate) {
-        launch_flat(h, p, stream);
-        return;
-    }
-    if (!db && h->flat_inplace && !h->ablate) {
-        launch_flat_inplace(h, p, stream);
-        return;
-    }
-    if (!db && h->flat_inplace && h->ablate >= 64) {   // timing-only ablations (PMENV_ABLATE = 64 + bits)
-        const pmenv_cfg& c = h->cfg;
-        p.div_units = make_fastdiv((uint32_t)((int64_t)c.num_assets * c.window * c.features / 4));
-        p.halo = h->halo;
-        const unsigned grid = (unsigned)((h->flat_qtot + 511) / 512);
-#define PMENV_ABL(X) case 64 + X: advance_flat_inplace_kernel<512, 1, 1, X><<<grid, 512, 0, stream>>>(p, h->flat_qtot); break;
-        switch (h->ablate) {
-            PMENV_ABL(1) PMENV_ABL(2) PMENV_ABL(4) PMENV_ABL(6) PMENV_ABL(15) PMENV_ABL(31) PMENV_ABL(32)
-            PMENV_ABL(33)
-            default: break;
-        }
-#undef PMENV_ABL
-        return;
-    }
-    p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
-    p.units_per_env = db ? h->units_per_env_db : h->units_per_env;
-    p.div_units = make_fastdiv((uint32_t)p.units_per_env);
-    const int vec = db ? h->stream_vec_db : h->stream_vec;
-    const int block = db ? h->stream_block_db : h->stream_block;
-    const unsigned grid = (unsigned)(h->cfg.num_envs * p.units_per_env);
-    switch (h->ablate) {     // timing-only builds: 512-thread geometry, default policy
-    case 1: launch_advance_b<kStreamBlock, 1, 0>(vec, p, grid, stream); break;
-    case 2: launch_advance_b<kStreamBlock, 2, 0>(vec, p, grid, stream); break;
-    case 3: launch_advance_b<kStreamBlock, 3, 0>(vec, p, grid, stream); break;
-    case 7: launch_advance_b<kStreamBlock, 7, 0>(vec, p, grid, stream); break;
-    default:
-        if (h->stream_pol == 1) launch_advance_p<1>(block, vec, p, grid, stream);
-        else if (h->stream_pol == 2) launch_advance_p<2>(block, vec, p, grid, stream);
-        else launch_advance_p<0>(block, vec, p, grid, stream);
-    }
+// which windows take the one-launch step under `path`
+int one_bits(const pmenv* h, int path) {
+    if (path == PMENV_STEP_PATH_ONE_LAUNCH) return h->one_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
+    if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming ? 0 : -1;
+    return h->one_auto;
 }
 
 }  // namespace
@@ -386,7 +502,7 @@ void pmenv_cfg_default(pmenv_cfg* cfg, int32_t num_envs, int32_t num_assets, int
     cfg->reward_kind = PMENV_REWARD_LOG_RETURN;
     cfg->norm_mode = PMENV_NORM_AND;
     cfg->ring_mode = PMENV_RING_STORAGE;
-    cfg->ret_mode = PMENV_RET_GROSS;
+    cfg->ret_mode = PMENV_RET_AUTO;
     cfg->mu_max_iter = 100;
     cfg->init_cash = 25000.0;
     cfg->commission = 0.0;
@@ -457,11 +573,13 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         return fail(PMENV_ERR_ARG);
     }
     if (c.reward_kind < 0 || c.reward_kind > 3 || c.norm_mode < 0 || c.norm_mode > 1 || c.ring_mode < 0 ||
-        c.ring_mode > 1 || c.ret_mode < 0 || c.ret_mode > 1 || c.mu_max_iter < 0 || !(c.commission >= 0.0) ||
+        c.ring_mode > 1 || c.ret_mode < 0 || c.ret_mode > 2 || c.mu_max_iter < 0 || !(c.commission >= 0.0) ||
         !(c.commission < 1.0)) {
         set_err(h, "invalid mode/commission value in cfg");
         return fail(PMENV_ERR_ARG);
     }
+    if (h->cfg.ret_mode == PMENV_RET_AUTO)
+        h->cfg.ret_mode = c.reward_kind == PMENV_REWARD_LOG_RETURN ? PMENV_RET_GROSS : PMENV_RET_NET;
     const int64_t WF = (int64_t)c.window * c.features;
     if (WF > kTileFloats) {
         set_err(h, "window*features = %lld exceeds the %d-float LDS tile", (long long)WF, kTileFloats);
@@ -484,104 +602,120 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
-    // streaming geometry
+
+    // ---- the two-launch stream: row-kernel geometry (fallback) and the flat stream
     static const int kInplaceOrder[3] = {2, 4, 1}, kDoubleOrder[3] = {4, 2, 1};
     h->stream_block = h->stream_block_db = kStreamBlock;
-    h->stream_pol = h->flat_pol = h->flat_ip_pol = 0;
-    if (const char* knob = getenv("PMENV_STREAM_BLOCK")) {        // A/B knob: 128 | 256 | 512
-        const int bk = atoi(knob);
-        if (bk == 128 || bk == 256 || bk == 512) h->stream_block = h->stream_block_db = bk;
+    {
+        const int bk = ab_int("PMENV_STREAM_BLOCK", kStreamBlock);   // tools: 128 | 256
+        if (bk == 128 || bk == 256) h->stream_block = h->stream_block_db = bk;
     }
-    if (const char* knob = getenv("PMENV_STREAM_POL")) {          // A/B knob: 0 | 1 (nt) | 2 (sc0 nt)
+    h->streaming = plan_streaming(c, kInplaceOrder, h->stream_block, &h->unit_rows, &h->stream_vec) &&
+                   plan_streaming(c, kDoubleOrder, h->stream_block_db, &h->unit_rows_db, &h->stream_vec_db);
+    const int64_t per = (int64_t)c.num_assets * c.window * c.features;
+    const int64_t win = (int64_t)c.num_envs * per * 4;
+    // Flat 16-B stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31) in place
+    // (with the halo) and double-buffered: 512 threads x 2 chunks, side data through the
+    // scalar unit (6.38 TB/s against 5.37 for whole-row units).
+    const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
+                         (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
+    h->flat = h->flat_inplace = flat_ok;
+    h->flat_db_wg = true;
+    h->flat_block = 512;
+    h->flat_ip_block = 512;
+    h->flat_ip_vec = 2;
+    h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
+    // nt unless the stream's working set fits the 256 MiB Infinity Cache: the window in
+    // place (<= 256 MiB), the window and its double buffer otherwise (<= 128 MiB each).
+    // Step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default policy against 46.5
+    // nt; 8,192 envs (246 MB) in place 84.6 / 86.1 but double-buffered 91.2 / 86.5;
+    // 16,384: 199.6 / 164.6 (profiles/ab_r01/pol_small_r01j.log, pol_ip_r01m.log)
+    h->flat_pol = win <= (128ll << 20) ? 0 : 1;
+    h->flat_ip_pol = win <= (256ll << 20) ? 0 : 1;
+    h->stream_pol = 0;
+    if (const char* knob = ab_knob("PMENV_STREAM_POL")) {       // tools: 0 | 1 (nt) | 2 (sc0 nt)
         const int pol = atoi(knob);
         if (pol >= 0 && pol <= 2) h->stream_pol = h->flat_pol = h->flat_ip_pol = pol;
     }
-    int fused_rows = 0;
-    h->streaming = plan_streaming(c, kInplaceOrder, h->stream_block, &h->unit_rows, &h->stream_vec) &&
-                   plan_streaming(c, kDoubleOrder, h->stream_block_db, &h->unit_rows_db, &h->stream_vec_db);
-    const bool fused_geom = h->streaming &&
-                            plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
-                            fused_rows == c.num_assets;
-    // flat stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31): the default
-    // in place (with the halo) and double-buffered. Measured on MI355X at the BASELINE
-    // shape in interleaved A/B rounds (tools/gpu_ab_pol.sh, profiles/ab_r01/): a step
-    // (scalar + advance) of 647 us in place with 512 threads x 2 chunks and the wave's
-    // side data through scalar loads, against 683 us at 1 chunk per thread, 689 us with
-    // per-lane side loads and 802 us for whole-row units; double-buffered 647 us in the
-    // workgroup (LDS) form against 664 us for the ds_bpermute form; the nt cache policy
-    // 2-5 % ahead of the default.
-    h->flat = false;
-    h->flat_block = 512;
-    {
-        const int64_t per = (int64_t)c.num_assets * c.window * c.features;
-        const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
-                             (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
-        h->flat = flat_ok;
-        h->flat_inplace = flat_ok;
-        h->flat_db_wg = true;
-        h->flat_ip_block = 512;
-        h->flat_ip_vec = 2;
-        h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
-        // nt unless the stream's working set fits the 256 MiB Infinity Cache: the window
-        // in place (<= 256 MiB), the window and its double buffer otherwise (<= 128 MiB).
-        // Step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default policy against
-        // 46.5 nt (double-buffered 46.3 / 47.4); 6,144 envs in place 62.6 / 66.9;
-        // 8,192 envs (246 MB) in place 84.6 / 86.1 but double-buffered 91.2 / 86.5;
-        // 16,384: 199.6 / 164.6 (profiles/ab_r01/pol_small_r01j.log, pol_ip_r01m.log)
-        if (getenv("PMENV_STREAM_POL") == nullptr) {
-            const int64_t win = (int64_t)c.num_envs * per * 4;
-            h->flat_pol = win <= (128ll << 20) ? 0 : 1;
-            h->flat_ip_pol = win <= (256ll << 20) ? 0 : 1;
-        }
-        // A/B knobs
-        if (const char* knob = getenv("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
-        if (const char* knob = getenv("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
-        if (const char* knob = getenv("PMENV_FLAT_DB_WG")) h->flat_db_wg = atoi(knob) != 0;
-        if (const char* knob = getenv("PMENV_FLAT_IP_BLOCK")) {
-            const int bk = atoi(knob);
-            if (bk == 256 || bk == 512 || bk == 1024) h->flat_ip_block = bk;
-        }
-        if (const char* knob = getenv("PMENV_FLAT_IP_VEC")) {   // chunks per thread
-            const int v = atoi(knob);
-            if (v == 1 || v == 2 || v == 4) h->flat_ip_vec = v;
-        }
-        {   // the launcher's (block, vec) table: anything else takes the default 512 x 2
-            const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
-            if (key != 2561 && key != 2562 && key != 2564 && key != 5121 && key != 5122 && key != 10241) {
-                h->flat_ip_block = 512;
-                h->flat_ip_vec = 2;
-            }
-        }
-        if (const char* knob = getenv("PMENV_FLAT_BLOCK")) {
-            const int bk = atoi(knob);
-            if (bk == 128 || bk == 256 || bk == 512) h->flat_block = bk;
+#ifdef PMENV_AB
+    if (const char* knob = ab_knob("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
+    if (const char* knob = ab_knob("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
+    h->flat_db_wg = ab_int("PMENV_FLAT_DB_WG", 1) != 0;
+    h->flat_ip_block = ab_int("PMENV_FLAT_IP_BLOCK", 512);
+    h->flat_ip_vec = ab_int("PMENV_FLAT_IP_VEC", 2);
+    {   // the launcher's (block, vec) table: anything else takes the default 512 x 2
+        const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
+        if (key != 2561 && key != 2562 && key != 2564 && key != 5121 && key != 5122 && key != 10241) {
+            h->flat_ip_block = 512;
+            h->flat_ip_vec = 2;
         }
     }
-    if (const char* knob = getenv("PMENV_ADVANCE"))   // A/B knob: force the single-launch LDS kernel
-        if (!strcmp(knob, "lds")) h->streaming = false;
-    if (const char* knob = getenv("PMENV_ABLATE")) h->ablate = atoi(knob);
-    h->k1_groups = 1;
-    if (const char* knob = getenv("PMENV_K1_GROUPS")) h->k1_groups = atoi(knob);   // A/B knob: 1 | 2 | 4
+    {
+        const int bk = ab_int("PMENV_FLAT_BLOCK", 512);
+        if (bk == 128 || bk == 256 || bk == 512) h->flat_block = bk;
+    }
+    if (const char* knob = ab_knob("PMENV_ADVANCE"))   // force the single-launch LDS kernel
+        if (!strcmp(knob, "lds")) h->streaming = h->flat = h->flat_inplace = false;
+    h->ablate = ab_int("PMENV_ABLATE", 0);
+    h->one_s80 = ab_int("PMENV_ONE_S80", 0) != 0;
+    h->flat_s80 = ab_int("PMENV_FLAT_S80", 0) != 0;
+#endif
+    h->k1_groups = ab_int("PMENV_K1_GROUPS", 1);
     if (h->k1_groups != 2 && h->k1_groups != 4) h->k1_groups = 1;
     h->k1_vec = pick_k1_vec(c);
     if (h->streaming) {
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
         h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
         h->lds_stream = 0;
-        // fused one-launch step (whole-env units, one wave for the env's assets). The
-        // scalar step inside the streaming workgroup lengthens every workgroup's life
-        // by its compute, so it only pays where the launch is latency-bound: measured
-        // on MI355X at N = 30, W = 50 (tools/gpu_ab_envs.sh) it wins at B = 1024
-        // (18.5 vs 20.2 us in place) and loses from B = 4096 up (57.9 vs 52.9 us;
-        // 764 vs 712 us at B = 65536).
-        const bool fusable = fused_geom && c.num_assets <= 64 && !h->ablate;
-        if (fusable && c.num_envs <= 1024) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
-        if (const char* knob = getenv("PMENV_FUSED")) {    // A/B knob: 0 | db | all
-            if (!strcmp(knob, "0") || !fusable) h->fused = 0;
-            else if (!strcmp(knob, "db")) h->fused = PMENV_FUSE_DB;
-            else if (!strcmp(knob, "all")) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
+    }
+
+    // ---- the one-launch step (step_env_kernel, one workgroup per env): F = 5, W >= 2,
+    // N <= 64 (the scalar step on one wave), 16-B granular env windows whose 1 KiB
+    // blocks fit 16 waves and 64 KiB of LDS. Measured against the two-launch path
+    // (tools/gpu_ab_one6.sh, profiles/ab_r02/): it wins below 4,096 envs (64: 6.5 vs
+    // 8.4 us; 1,024: 13.1 vs 18.2; 2,048: 24.7 vs 26.9) and from 16,384 up (162.6 vs
+    // 170.0 us; 65,536: 650-658 vs 657-664), and loses to the two-launch stream where
+    // an in-place window of 3,072+ envs sits in the Infinity Cache (4,096: 46.5 vs
+    // 44.2 us; 8,192: 85.7 vs 84.6), which therefore keeps the two launches.
+    h->per4 = (uint32_t)(per / 4);
+    // 4 chunks per lane (tools: PMENV_ONE_V = 1 | 2 | 3 | 6 | 8; 4 measured best: 650 us
+    // against 662-666 for 8, 762 for 3, 860 for 2 at the BASELINE shape)
+    h->one_v = ab_int("PMENV_ONE_V", 4);
+    if (h->one_v != 1 && h->one_v != 2 && h->one_v != 3 && h->one_v != 6 && h->one_v != 8) h->one_v = 4;
+    {
+        // the env's chunks start anywhere in a 64-chunk block: up to 63 slots ahead of it
+        const uint32_t blocks = (h->per4 + 63u + 63u) / 64u;
+        h->one_waves = (int)((blocks + (uint32_t)h->one_v - 1) / (uint32_t)h->one_v);
+    }
+    h->one_ok = h->streaming && c.features == 5 && c.window >= 2 && c.num_assets <= 64 && per % 4 == 0 &&
+                h->one_waves <= 16 && ((int64_t)64 * h->one_v * h->one_waves + 2) * 16 <= 65536;
+    h->one_auto = 0;
+    if (h->one_ok) {
+        h->one_auto = PMENV_FUSE_DB;
+        if (!(h->flat_inplace && c.num_envs >= 3072 && win <= (256ll << 20))) h->one_auto |= PMENV_FUSE_INPLACE;
+    }
+#ifdef PMENV_AB
+    if (const char* knob = ab_knob("PMENV_ONE")) {    // 0 | db | ip | all
+        if (!h->one_ok || !strcmp(knob, "0")) h->one_auto = 0;
+        else if (!strcmp(knob, "db")) h->one_auto = PMENV_FUSE_DB;
+        else if (!strcmp(knob, "ip")) h->one_auto = PMENV_FUSE_INPLACE;
+        else if (!strcmp(knob, "all")) h->one_auto = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
+    }
+    {   // the previous one-launch form (advance_rows_kernel<fused>), PMENV_FUSED = db | all
+        int fused_rows = 0;
+        const bool fusable = h->streaming && c.num_assets <= 64 && !h->ablate &&
+                             plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
+                             fused_rows == c.num_assets;
+        if (const char* knob = ab_knob("PMENV_FUSED")) {
+            if (fusable && !strcmp(knob, "db")) h->fused = PMENV_FUSE_DB;
+            else if (fusable && !strcmp(knob, "all")) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
+            if (h->fused) h->one_auto &= ~h->fused;
         }
     }
+#endif
+    h->path = PMENV_STEP_PATH_AUTO;
+    h->one = h->one_auto;
+
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
     if (h->lds_tile > 160 * 1024 || h->lds_scalar > 160 * 1024) {
@@ -669,6 +803,23 @@ int pmenv_destroy(pmenv* h) {
     return PMENV_OK;
 }
 
+int pmenv_set_step_path(pmenv* h, int32_t path) {
+    if (!h) return PMENV_ERR_ARG;
+    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_TWO_LAUNCH) {
+        set_err(h, "unknown step path %d", path);
+        return PMENV_ERR_ARG;
+    }
+    const int bits = one_bits(h, path);
+    if (bits < 0) {
+        set_err(h, "step path %d does not fit this shape (one launch: F = 5, W >= 2, N <= 64, window <= 64 KiB "
+                   "of LDS; two launches: F = 5, 16-B granular env windows)", path);
+        return PMENV_ERR_ARG;
+    }
+    h->path = path;
+    h->one = bits;
+    return PMENV_OK;
+}
+
 int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
     if (obs && !aligned4(obs)) { set_err(h, "obs not 4-byte aligned"); return PMENV_ERR_ALIGN; }
@@ -717,32 +868,24 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     if (h->streaming && obs16) {
         const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
         const int fuse_bit = p.obs_out == p.obs ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
+        if (h->one & fuse_bit) {       // one launch: the whole step runs in the scalar phase
+            if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
+            launch_one(h, p, stream);
+            return check_launch(h, "step_env_kernel");
+        }
+#ifdef PMENV_AB
         if (ph == (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE) && (h->fused & fuse_bit)) {
             launch_fused(h, p, stream);
             return check_launch(h, "advance_rows_kernel<fused>");
         }
+#endif
         if (ph & PMENV_PHASE_SCALAR) {
-            if (p.obs_out == p.obs && h->flat_inplace && !h->ablate) {   // the in-place advance's halo
-                p.halo = h->halo;
-                p.halo_wgs = h->halo_wgs;
-                p.halo_block = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
-                p.halo_qtot = h->flat_qtot;
-            }
-            const int N = h->cfg.num_assets;
-            if (h->k1_vec && launch_scalar_vec(h->k1_vec, p, stream)) {
-                // packed form
-            } else if (N <= 64) {
-                launch_scalar_reg(h, p, stream);
-            } else {
-                scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar,
-                                     stream>>>(p, h->scalar_scratch_floats);
-            }
-            int rc = check_launch(h, "scalar_step_kernel");
+            const int rc = launch_scalar(h, p, stream);
             if (rc) return rc;
         }
         if (ph & PMENV_PHASE_ADVANCE) {
             launch_advance(h, p, stream);
-            return check_launch(h, "advance_rows_kernel");
+            return check_launch(h, "advance kernel");
         }
         return PMENV_OK;
     }
@@ -770,20 +913,25 @@ size_t pmenv_state_bytes(const pmenv* h) { return h ? h->state_bytes : 0; }
 const char* pmenv_step_path(const pmenv* h) {
     if (!h) return "";
     if (!h->streaming) return "step_advance_lds_kernel";
-    if (h->fused == (PMENV_FUSE_DB | PMENV_FUSE_INPLACE)) return "advance_rows_kernel<fused>";
-    // the two-launch path: the scalar step (K1) the handle launches, then the stream
+    // per window mode: the one-launch kernel, or the scalar step (K1) then the stream
     const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
                    : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
-    const char* db = h->fused ? nullptr
-                   : h->flat ? (h->flat_db_wg ? "advance_flat_wg_kernel" : "advance_flat_kernel")
-                   : "advance_rows_kernel";
-    const char* ip = h->flat && h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
-    static thread_local char buf[256];
-    if (db)
-        snprintf(buf, sizeof buf, "%s+%s (obs_out) | %s+%s (in place)", k1, db, k1, ip);
-    else
-        snprintf(buf, sizeof buf, "advance_rows_kernel<fused> (obs_out) | %s+%s (in place)", k1, ip);
-    return buf;
+    const char* db2 = h->flat ? (h->flat_db_wg ? "advance_flat_wg_kernel" : "advance_flat_kernel")
+                    : "advance_rows_kernel";
+    const char* ip2 = h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
+    static thread_local char buf[2][128], out[288];
+    const char* part[2];
+    for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
+        const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
+        if (h->one & bit) part[m] = "step_env_kernel";
+        else if (h->fused & bit) part[m] = "advance_rows_kernel<fused>";
+        else {
+            snprintf(buf[m], sizeof buf[m], "%s+%s", k1, m ? ip2 : db2);
+            part[m] = buf[m];
+        }
+    }
+    snprintf(out, sizeof out, "%s (obs_out) | %s (in place)", part[0], part[1]);
+    return out;
 }
 
 int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
@@ -853,16 +1001,15 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     // measured on MI355X (tools/bench_rows.py, profiles/rows_r01.json): the tiled scan
     // beats the per-env loop 2.7x at T = 256 x B = 65536 and 14x at 2048 x 8192; the
     // wave-per-env scan only for a handful of envs with long horizons
-    const char* knob = getenv("PMENV_GAE");        // A/B knob: loop | scan | tile
+    const char* knob = ab_knob("PMENV_GAE");      // tools: loop | scan | tile
     const bool fits = (size_t)(T + 1) * (size_t)B * 4u < (1ull << 31);   // gae_tile_kernel's buffer offsets
     const bool scan = knob ? !strcmp(knob, "scan") : (B < 64 && T >= 256);
     const bool tile = fits && (knob ? !strcmp(knob, "tile") : !scan);
-    const char* uknob = getenv("PMENV_GAE_U");    // A/B knob: steps per lane and segment (8 | 16)
-    const int U = uknob ? atoi(uknob) : (B >= 16384 ? 8 : 16);
-    // A/B knob PMENV_GAE_E: envs per lane of the pipelined tile (gae_tile_vec_kernel;
-    // 1, 2 or 4, needs B % E == 0); 0 = gae_tile_kernel
-    const char* eknob = getenv("PMENV_GAE_E");
-    int E = eknob ? atoi(eknob) : 0;
+    const int U = ab_int("PMENV_GAE_U", B >= 16384 ? 8 : 16);   // tools: steps per lane and segment
+#ifdef PMENV_AB
+    // PMENV_GAE_E: envs per lane of the pipelined tile (gae_tile_vec_kernel; 1, 2 or 4,
+    // needs B % E == 0); 0 = gae_tile_kernel
+    int E = ab_int("PMENV_GAE_E", 0);
     if (E != 1 && E != 2 && E != 4) E = 0;
     if (E && B % E) E = 0;
     if (tile && E) {
@@ -875,7 +1022,10 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
         else if (E == 2) PMENV_GAEV(8, 2);
         else PMENV_GAEV(4, 4);                    // E = 4 at U = 8 spills
 #undef PMENV_GAEV
-    } else if (tile && U == 16)
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+#endif
+    if (tile && U == 16)
         gae_tile_kernel<8, 16><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
                                                                  lam);
     else if (tile)
@@ -919,7 +1069,7 @@ int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
     int lc = 0;
     const int n = gae_chunks(T, B, &lc);
-    const char* knob = getenv("PMENV_GAE");        // an explicit kernel choice wins (A/B)
+    const char* knob = ab_knob("PMENV_GAE");      // tools: an explicit kernel choice wins
     if (!n || knob || !work || work_bytes < (size_t)2 * n * B * sizeof(double))
         return pmenv_gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream);
     const dim3 grid((unsigned)((B + 63) / 64), (unsigned)n);
@@ -960,7 +1110,7 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     // of 4 (16-B aligned groups), R*(W+1) <= 2,048 (day, asset) pairs (at most 8 per
     // thread); N = 30, W = 50: R = 30, one group per sample
     int R = 0;
-    if (F == 5 && al16 && !getenv("PMENV_REPLAY_LDS")) {   // A/B knob: the per-element staging kernel
+    if (F == 5 && al16 && !ab_knob("PMENV_REPLAY_LDS")) {   // tools: the per-element staging kernel
         // the largest group within 2,048 pairs: whole samples measured faster than
         // 10-asset groups (131 vs 148 us at N = 30, W = 50) — every workgroup pays the
         // sample's dependent index loads once
@@ -976,21 +1126,16 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
         const dim3 grid((unsigned)S, (unsigned)(N / R));
         const int pairs = R * (W + 1);
         // s / s' are written once per sample: nt stores, 129.6 -> 118.6 us at S = 8,192
-        // (tools/ab_replay.py, profiles/ab_r01/replay_nt_tpb_r01h.log). A/B knobs:
-        // PMENV_REPLAY_NT=0 (default-policy stores), PMENV_REPLAY_TPB=512
-        const bool nt = !(getenv("PMENV_REPLAY_NT") && atoi(getenv("PMENV_REPLAY_NT")) == 0);
-        const bool t512 = getenv("PMENV_REPLAY_TPB") && atoi(getenv("PMENV_REPLAY_TPB")) == 512;
-#define PMENV_RG(PPT, NTV, TPB)                                                                              \
-    replay_gather_f5_kernel<PPT, NTV, TPB><<<grid, TPB, glds, stream>>>(series, T, N, W, days, actions, rewards, \
-                                                                        H, B, h0, env, s, s_next, a_out, r_out, \
-                                                                        R, dr, dwf)
-        // persistent form (replay_gather_f5p_kernel) by default: one workgroup per CU
-        // loops over the samples with the next sample's loads in flight. One per CU is
-        // the measured optimum (S = 8,192: 96 us at 256 workgroups; 114-121 us at 192,
-        // 288, 512, 768, 1,280 and one workgroup per sample, 117 us;
-        // profiles/ab_r01/replay_grid_r01j.log). PMENV_REPLAY_PERSIST=0: one workgroup
-        // per sample; PMENV_REPLAY_GRID: G.
-        const bool persist = !t512 && !(getenv("PMENV_REPLAY_PERSIST") && atoi(getenv("PMENV_REPLAY_PERSIST")) == 0);
+        // (tools/ab_replay.py, profiles/ab_r01/replay_nt_tpb_r01h.log). Persistent form
+        // (replay_gather_f5p_kernel): one workgroup per CU loops over the samples with the
+        // next sample's loads in flight. One per CU is the measured optimum (S = 8,192:
+        // 96 us at 256 workgroups; 114-121 us at 192, 288, 512, 768, 1,280 and one
+        // workgroup per sample, 117 us; profiles/ab_r01/replay_grid_r01j.log). Tools knobs:
+        // PMENV_REPLAY_NT=0 (default-policy stores), PMENV_REPLAY_PERSIST=0 (one workgroup
+        // per sample), PMENV_REPLAY_TPB=512, PMENV_REPLAY_GRID=G.
+        const bool nt = ab_int("PMENV_REPLAY_NT", 1) != 0;
+        const bool t512 = ab_int("PMENV_REPLAY_TPB", 256) == 512;
+        const bool persist = !t512 && ab_int("PMENV_REPLAY_PERSIST", 1) != 0;
         if (persist) {
             static int cus = 0;
             if (!cus) {
@@ -1001,19 +1146,29 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
             }
             const int gy = N / R;
             int G = cus / gy > 0 ? cus / gy : 1;
-            if (const char* knob = getenv("PMENV_REPLAY_GRID")) G = atoi(knob) > 0 ? atoi(knob) : G;
+            G = ab_int("PMENV_REPLAY_GRID", G) > 0 ? ab_int("PMENV_REPLAY_GRID", G) : G;
             const dim3 pgrid((unsigned)(S < G ? S : G), (unsigned)(N / R));
             const int ppt = pairs <= 2 * 256 ? 2 : pairs <= 4 * 256 ? 4 : 8;
 #define PMENV_RGP(PPT, NTV)                                                                                   \
     replay_gather_f5p_kernel<PPT, NTV><<<pgrid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, \
                                                                      h0, env, S, s, s_next, a_out, r_out, R, dr, dwf)
-            if (nt) { if (ppt == 2) PMENV_RGP(2, 2); else if (ppt == 4) PMENV_RGP(4, 2); else PMENV_RGP(8, 2); }
-            else { if (ppt == 2) PMENV_RGP(2, 0); else if (ppt == 4) PMENV_RGP(4, 0); else PMENV_RGP(8, 0); }
+#ifdef PMENV_AB
+            if (!nt) {
+                if (ppt == 2) PMENV_RGP(2, 0); else if (ppt == 4) PMENV_RGP(4, 0); else PMENV_RGP(8, 0);
+                return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+            }
+#endif
+            if (ppt == 2) PMENV_RGP(2, 2); else if (ppt == 4) PMENV_RGP(4, 2); else PMENV_RGP(8, 2);
 #undef PMENV_RGP
             return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
         }
+#ifdef PMENV_AB
         const int tpb = t512 ? 512 : 256;
         const int ppt = pairs <= 2 * tpb ? 2 : pairs <= 4 * tpb ? 4 : 8;
+#define PMENV_RG(PPT, NTV, TPB)                                                                              \
+    replay_gather_f5_kernel<PPT, NTV, TPB><<<grid, TPB, glds, stream>>>(series, T, N, W, days, actions, rewards, \
+                                                                        H, B, h0, env, s, s_next, a_out, r_out, \
+                                                                        R, dr, dwf)
         if (t512) {
             if (nt) { if (ppt == 2) PMENV_RG(2, 2, 512); else if (ppt == 4) PMENV_RG(4, 2, 512); else PMENV_RG(8, 2, 512); }
             else { if (ppt == 2) PMENV_RG(2, 0, 512); else if (ppt == 4) PMENV_RG(4, 0, 512); else PMENV_RG(8, 0, 512); }
@@ -1022,6 +1177,10 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
             else { if (ppt == 2) PMENV_RG(2, 0, 256); else if (ppt == 4) PMENV_RG(4, 0, 256); else PMENV_RG(8, 0, 256); }
         }
 #undef PMENV_RG
+#else
+        (void)grid;
+        (void)nt;
+#endif
     } else if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
         replay_gather_lds_kernel<<<(unsigned)S, 256, lds, stream>>>(series, T, N, F, W, days, actions, rewards, H, B,
                                                                    h0, env, s, s_next, a_out, r_out);
@@ -1042,20 +1201,22 @@ int pmenv_metrics(const double* returns, const double* values, const float* weig
     const int nseg = (B + 63) / 64, nturn = (B + eb - 1) / eb;
     // one launch for both passes (metrics_fused_kernel); A/B knobs: PMENV_METRICS_FUSED=0
     // (two launches), PMENV_METRICS_SEG_FIRST=0 (turnover blocks dispatched first)
-    const bool walk = getenv("PMENV_METRICS_WALK") != nullptr;   // A/B knob: the thread-per-env walk
-    const bool fused = !walk && !(getenv("PMENV_METRICS_FUSED") && atoi(getenv("PMENV_METRICS_FUSED")) == 0);
+    const bool walk = ab_knob("PMENV_METRICS_WALK") != nullptr;  // tools: the thread-per-env walk
+    const bool fused = !walk && ab_int("PMENV_METRICS_FUSED", 1) != 0;
     if (fused) {
-        const int seg_first = !(getenv("PMENV_METRICS_SEG_FIRST") && atoi(getenv("PMENV_METRICS_SEG_FIRST")) == 0);
+        const int seg_first = ab_int("PMENV_METRICS_SEG_FIRST", 1) != 0;
         metrics_fused_kernel<<<(unsigned)(nseg + nturn), 256, 0, stream>>>(returns, values, weights, T, B, N,
                                                                            risk_free_rate, periods, tpe, eb, nseg,
                                                                            nturn, seg_first, out);
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
     }
+#ifdef PMENV_AB
     if (walk)
         metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
     else
         metrics_seg_kernel<<<(unsigned)nseg, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
     metrics_turnover_kernel<<<(unsigned)nturn, 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
+#endif
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

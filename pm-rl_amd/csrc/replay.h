@@ -53,6 +53,7 @@ __global__ void replay_gather_kernel(const float* series, int T, int N, int F, i
     s_next[i] = vn;
 }
 
+#ifdef PMENV_AB   // tools build: the thread-per-env walk (the fused kernel replaced it)
 // one thread per env walks its column of the trajectory (coalesced across envs)
 //   out[b] = {sharpe, sortino, max drawdown, average turnover, final value}
 __global__ void metrics_kernel(const double* returns, const double* values, int T, int B, double rf,
@@ -85,6 +86,7 @@ __global__ void metrics_kernel(const double* returns, const double* values, int 
     out[(size_t)b * 5 + 2] = mdd;
     out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
 }
+#endif
 
 
 // The same per-env metrics with the horizon split over the four waves of a
@@ -164,10 +166,12 @@ __device__ __forceinline__ void metrics_seg_body(const double* returns, const do
     out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
 }
 
+#ifdef PMENV_AB   // tools build: the two-launch form of metrics_fused_kernel
 __global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
                                                           double rf, double periods, double* out) {
     metrics_seg_body(returns, values, T, B, rf, periods, out, (int)blockIdx.x);
 }
+#endif
 
 // util/eval.py:32-37 average turnover, element-parallel: a workgroup owns `eb` whole
 // envs (N <= 256: one thread per (env, asset), so each day's read is eb*N contiguous
@@ -210,10 +214,12 @@ __device__ __forceinline__ void metrics_turnover_body(const float* weights, int 
     }
 }
 
+#ifdef PMENV_AB
 __global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
                                                                int eb, double* out) {
     metrics_turnover_body(weights, T, B, N, tpe, eb, out, (int)blockIdx.x);
 }
+#endif
 
 // Both metric passes in one launch: they read disjoint inputs and write disjoint
 // fields of out, so the latency-bound segment walk (returns, values) runs beside the

@@ -19,7 +19,7 @@ PMENV_ABI_VERSION = 1
 REWARD_KINDS = {"log_returns": 0, "returns": 1, "sharpe_ratio": 2, "diff_sharpe": 3}
 NORM_MODES = {"and": 0, "or": 1}
 RING_MODES = {"storage": 0, "chrono": 1}
-RET_MODES = {"gross": 0, "net": 1}
+RET_MODES = {"gross": 0, "net": 1, "auto": 2}
 BATCH_NORM_MODES = {"global_or": 0, "row_or": 1, "none": 2}
 STATE_FIELDS = 8   # value, stat_a, stat_b, counter, ring, nonfinite, last_close, w_new
 STATUS = {0: "OK", -1: "ERR_ARG", -2: "ERR_SHAPE", -3: "ERR_HIP", -4: "ERR_ALIGN"}
@@ -47,6 +47,7 @@ class PmenvStepArgs(ctypes.Structure):
 
 PHASE_SCALAR = 1
 PHASE_ADVANCE = 2
+STEP_PATHS = {"auto": 0, "one_launch": 1, "two_launch": 2}
 
 
 # (name, restype, argtypes) for every symbol include/pmenv.h declares
@@ -70,6 +71,7 @@ SIGNATURES = [
     ("pmenv_counter", _P, [_P]),
     ("pmenv_state_bytes", _SZ, [_P]),
     ("pmenv_step_path", ctypes.c_char_p, [_P]),
+    ("pmenv_set_step_path", ctypes.c_int, [_P, _I32]),
     ("pmenv_get_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_set_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_nonfinite_count", ctypes.c_int, [_P, ctypes.POINTER(_U64), _P]),

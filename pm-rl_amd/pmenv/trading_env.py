@@ -13,9 +13,12 @@ call, with a leading batch dimension B of lockstep envs:
     .info values/actions/rewards/returns       .info (opt-in, track_info=True)
 
 Every compute call goes through libpmenv.so (include/pmenv.h); there is no CPU
-path. `features` must be a float32, contiguous tensor on the env's device: it is
-written in place and returned, exactly as trading_env.py:32,103 mutate the
-caller's tensor.
+path. `features` must be a float32, contiguous tensor: it is written in place and
+returned, exactly as trading_env.py:32,103 mutate the caller's tensor. A caller that
+keeps the reference's CPU tensors (train/on_policy.py:59-67 hands the env host
+tensors) may pass them unchanged: they are staged to the env's GPU and back (a PCIe
+round trip per call — the slow path; keep tensors on the GPU for throughput), and
+the reward and `.value` come back on the host as the reference returns them.
 """
 import ctypes
 
@@ -74,7 +77,9 @@ class RingView:
 
 class TradingEnv:
     def __init__(self, num_envs=1, num_assets=None, window=None, features=5, device=None,
-                 config=None, track_info=False, **overrides):
+                 config=None, track_info=False, step_impl="auto", **overrides):
+        """step_impl: "auto" (per shape), "one_launch" (step_env_kernel, one workgroup per
+        env) or "two_launch" (scalar-step kernel + window stream); see set_step_impl."""
         if config is None:
             kw = dict(num_envs=num_envs, features=features)
             if num_assets is not None:
@@ -117,6 +122,8 @@ class TradingEnv:
         self.weights = RingView(self)
         self.track_info = track_info
         self._unbatched = False
+        self._host_io = False               # the last reset/step came with CPU tensors
+        self.set_step_impl(step_impl)
         self.info = None
         self._reset_info()
 
@@ -138,8 +145,10 @@ class TradingEnv:
     def _obs_check(self, features, name="features"):
         cfg = self.cfg
         shape = (cfg.num_envs, cfg.num_assets, cfg.window, cfg.features)
-        if features.dtype != torch.float32 or not features.is_contiguous() or features.device != self.device:
-            raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device} (written in place)")
+        if features.dtype != torch.float32 or not features.is_contiguous() or \
+                features.device not in (self.device, torch.device("cpu")):
+            raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device} or the host "
+                             "(written in place)")
         if tuple(features.shape) == shape:
             return False
         if cfg.num_envs == 1 and tuple(features.shape) == shape[1:]:
@@ -160,8 +169,20 @@ class TradingEnv:
     # ------------------------------------------------------------------ API
     @property
     def value(self):
-        """Portfolio value (trading_env.py:9,89) — f64 [B] view of the device state."""
-        return self._value[0] if self._unbatched else self._value
+        """Portfolio value (trading_env.py:9,89) — f64 [B] view of the device state
+        (a host copy when the caller drives the env with CPU tensors)."""
+        v = self._value.cpu() if self._host_io else self._value
+        return v[0] if self._unbatched else v
+
+    def set_step_impl(self, impl):
+        """Advance-mode step implementation (pmenv_set_step_path): "auto", "one_launch"
+        or "two_launch". Raises ValueError when the shape does not fit it."""
+        if impl not in _abi.STEP_PATHS:
+            raise ValueError(f"step_impl must be one of {sorted(_abi.STEP_PATHS)}")
+        rc = self._lib.pmenv_set_step_path(self._h, _abi.STEP_PATHS[impl])
+        if rc != 0:
+            raise ValueError(self._lib.pmenv_last_error(self._h).decode())
+        self.step_impl = impl
 
     @property
     def num_envs(self):
@@ -170,15 +191,22 @@ class TradingEnv:
     def reset(self, features=None, mask=None):
         """trading_env.py:21-41 for all envs (or the envs where mask is True)."""
         unb = False
+        dev_features = features
         if features is not None:
             unb = self._obs_check(features)
             self._unbatched = unb
+            self._host_io = features.device.type == "cpu"
+            if self._host_io:
+                dev_features = features.to(self.device)
         m = None
         if mask is not None:
-            m = torch.as_tensor(mask, device=self.device).reshape(-1).to(torch.uint8).contiguous()
+            m = torch.as_tensor(mask).to(self.device).reshape(-1).to(torch.uint8).contiguous()
             if m.numel() != self.cfg.num_envs:
                 raise ValueError("mask must have num_envs elements")
-        _abi.check(self._lib.pmenv_reset(self._h, _ptr(features), _ptr(m), self._stream()), self._h, "pmenv_reset")
+        _abi.check(self._lib.pmenv_reset(self._h, _ptr(dev_features), _ptr(m), self._stream()), self._h,
+                   "pmenv_reset")
+        if dev_features is not features:
+            features.copy_(dev_features)
         if mask is None:
             self._reset_info()
         return features
@@ -204,6 +232,18 @@ class TradingEnv:
         cfg = self.cfg
         B, N = cfg.num_envs, cfg.num_assets
         unb = self._obs_check(features)
+        host = features.device.type == "cpu"
+        if out is not None and (out.device.type == "cpu") != host:
+            raise ValueError("out must live where features does")
+        if host:                                   # the reference's CPU tensors: staged through the GPU
+            r, res = self.step(action, features.to(self.device), prices=prices, bar=bar,
+                               out=None if out is None else torch.empty(out.shape, dtype=out.dtype,
+                                                                        device=self.device),
+                               series=series, day=day)
+            (features if out is None else out).copy_(res)
+            self._host_io = True
+            return r.cpu(), (features if out is None else out)
+        self._host_io = False
         a = self._vec(action, N, "action")
         p = self._vec(prices, N, "prices") if prices is not None else None
         br = dy = None

@@ -47,7 +47,7 @@ def test_abi_version_and_cfg_defaults_match_reference_config():
     # config/base.py:47-53
     assert c.init_cash == 25000 and c.commission == 0.0 and c.reward_scale == 1.0
     assert c.risk_free_rate == 0.04 and c.reward_kind == 0
-    assert c.norm_mode == 0 and c.ring_mode == 0 and c.ret_mode == 0 and c.mu_tol == 1e-10
+    assert c.norm_mode == 0 and c.ring_mode == 0 and c.ret_mode == 2 and c.mu_tol == 1e-10   # ret: AUTO
     assert ctypes.sizeof(_abi.PmenvCfg) == 88
 
 
@@ -96,3 +96,28 @@ def test_product_does_not_reference_the_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")) and f != "build.py":
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in txt.lower(), f"{f} references the oracle"
+
+
+def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
+    """The product library calls no getenv (nothing in the environment can alter the
+    timed path) and carries none of the timing-only variants of the tools build
+    (tools/libpmenv_ab.so, -DPMENV_AB): no work-skipping ABL / SKIP instantiations, no
+    80-SGPR twins, no A/B-only geometries."""
+    from pmenv import _abi
+    undef = subprocess.run(["nm", "-D", "--undefined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "getenv" not in undef
+    syms = subprocess.run(["nm", "-C", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    kernels = set(re.findall(r"__device_stub__(\w+<[^>]*>)", syms))
+    assert kernels, "no kernel stubs found"
+    for k in kernels:
+        args = [a.strip() for a in k[k.index("<") + 1:-1].split(",")]
+        name = k[:k.index("<")]
+        assert "s80" not in name, k
+        if name == "advance_flat_inplace_kernel":
+            assert args == ["512", "2", args[2], "0"] and args[2] in ("0", "1"), k   # 512 x 2, no SKIP bits
+        if name == "step_env_kernel":
+            assert args[0] == "4" and args[3] == "0", k                             # V = 4, ABL = 0
+        if name == "advance_rows_kernel":
+            assert args[0] == "512" and args[3] == "0" and args[4] == "false", k    # ABL = 0, not fused
+    assert not any(k.startswith(("gae_tile_vec_kernel", "replay_gather_f5_kernel", "advance_flat_kernel<"))
+                   for k in kernels)

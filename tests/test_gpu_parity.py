@@ -63,8 +63,10 @@ def test_gpu_matches_reference_goldens(name, mode):
     compare(g, out)
 
 
-def _run_both(cfg_kw, B, N, W, T, kind="simplex", seed=0, F=5, resets=None, mode="advance", double_buffer=False):
-    """Drive pmenv and the oracle side by side on identical inputs."""
+def _run_both(cfg_kw, B, N, W, T, kind="simplex", seed=0, F=5, resets=None, mode="advance", double_buffer=False,
+              impl="auto"):
+    """Drive pmenv and the oracle side by side on identical inputs (impl: the advance
+    step's implementation, TradingEnv.set_step_impl)."""
     from pmenv import TradingEnv
     from pmenv.config import EnvConfig
     rng = np.random.default_rng(seed)
@@ -85,7 +87,7 @@ def _run_both(cfg_kw, B, N, W, T, kind="simplex", seed=0, F=5, resets=None, mode
         act = rng.uniform(0, 1, (T, B, N)) / N * 2
     act = act.astype(np.float32)
     cfg = EnvConfig(num_envs=B, num_assets=N, window=W, features=F, **cfg_kw)
-    genv = TradingEnv(config=cfg, device=DEV, track_info=True)
+    genv = TradingEnv(config=cfg, device=DEV, track_info=True, step_impl=impl)
     cenv = OracleEnv(cfg)
     gobs = _t(obs0)
     cobs = obs0.copy()
@@ -165,26 +167,28 @@ def test_gpu_double_buffered_advance(N, W, F):
 
 @pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
 @pytest.mark.parametrize("kind", ["simplex", "mixed"])
-def test_gpu_flat_obs_out_vs_oracle_modes(monkeypatch, kw, kind):
-    """The double-buffered flat stream (advance_flat_kernel, the default obs_out path
-    above B = 1024; forced here at small B by turning the one-launch step off) against
-    the oracle in every reward / ring / norm / commission mode, through the ring wrap."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
+def test_gpu_flat_obs_out_vs_oracle_modes(kw, kind):
+    """The two-launch step double-buffered (scalar_step_vec_kernel, then the flat
+    stream advance_flat_wg_kernel: the obs_out path for N > 64) against the oracle in
+    every reward / ring / norm / commission mode, through the ring wrap."""
     from pmenv import TradingEnv
-    assert "advance_flat_wg_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
+    e = TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV, step_impl="two_launch")
+    assert "advance_flat_wg_kernel" in e.step_path.split(" | ")[0]
     _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flat{kw}{kind}".encode()),
-              double_buffer=True)
+              double_buffer=True, impl="two_launch")
 
 
 @pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
 @pytest.mark.parametrize("kind", ["simplex", "mixed"])
-def test_gpu_flat_inplace_vs_oracle_modes(monkeypatch, kw, kind):
-    """The in-place flat stream (advance_flat_inplace_kernel + the halo the scalar
-    step copies), the default in-place path above B = 1024, against the oracle."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
+def test_gpu_flat_inplace_vs_oracle_modes(kw, kind):
+    """The two-launch step in place (the scalar step copying the halo, then
+    advance_flat_inplace_kernel: the in-place path for N > 64 and for cache-resident
+    windows of 3,072+ envs) against the oracle."""
     from pmenv import TradingEnv
-    assert "advance_flat_inplace_kernel" in TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path
-    _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flatip{kw}{kind}".encode()))
+    e = TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV, step_impl="two_launch")
+    assert "advance_flat_inplace_kernel" in e.step_path.split(" | ")[1]
+    _run_both(kw, B=67, N=30, W=50, T=70, kind=kind, seed=zlib.crc32(f"flatip{kw}{kind}".encode()),
+              impl="two_launch")
 
 
 @pytest.mark.parametrize("N,W,B", [
@@ -196,34 +200,40 @@ def test_gpu_flat_inplace_vs_oracle_modes(monkeypatch, kw, kind):
     (129, 50, 2),     # long envs
     (12, 10, 1),      # single env
 ])
-@pytest.mark.parametrize("knobs", ["", "PMENV_STREAM_POL=0", "PMENV_STREAM_POL=2+PMENV_FLAT_BLOCK=128",
-                                   "PMENV_FLAT_BLOCK=256", "PMENV_FLAT_DB_WG=1", "PMENV_FLAT_DB_WG=0"])
-def test_gpu_flat_obs_out_shapes(monkeypatch, N, W, B, knobs):
-    monkeypatch.setenv("PMENV_FUSED", "0")
-    for kv in filter(None, knobs.split("+")):
-        monkeypatch.setenv(*kv.split("="))
-    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 7 + W, double_buffer=True)
-    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + W, double_buffer=True)
+def test_gpu_flat_obs_out_shapes(N, W, B):
+    impl = "two_launch" if N * W * 5 % 4 == 0 else "auto"    # not 16-B granular: the LDS fallback
+    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 7 + W, double_buffer=True, impl=impl)
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + W, double_buffer=True,
+              impl=impl)
 
 
 @pytest.mark.parametrize("N,W,B", [(30, 50, 37), (5, 4, 13), (4, 2, 7), (1, 4, 9), (64, 16, 3), (129, 50, 2),
                                    (12, 10, 1), (30, 50, 600)])
-@pytest.mark.parametrize("knobs", ["", "PMENV_FLAT_IP_BLOCK=256", "PMENV_FLAT_IP_BLOCK=1024+PMENV_STREAM_POL=0",
-                                   "PMENV_FLAT_IP_VEC=1", "PMENV_FLAT_IP_BLOCK=256+PMENV_FLAT_IP_VEC=4"])
-def test_gpu_flat_inplace_shapes(monkeypatch, N, W, B, knobs):
+def test_gpu_flat_inplace_shapes(N, W, B):
     """Workgroup seams (the halo) at every alignment against rows, envs and the
     tensor's end; (30, 50, 600): hundreds of workgroups, each seam's halo exercised."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
-    for kv in filter(None, knobs.split("+")):
-        monkeypatch.setenv(*kv.split("="))
-    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 5 + W)
-    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 3 * W)
+    impl = "two_launch" if N * W * 5 % 4 == 0 else "auto"    # not 16-B granular: the LDS fallback
+    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 5 + W, impl=impl)
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 3 * W, impl=impl)
 
 
-def test_gpu_flat_resident_series_obs_out(monkeypatch):
-    """Day-indexed bars (resident series) through the flat stream == the bar batch,
-    bit for bit; an out-of-range day reads NaN market channels, counted, not read."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
+def test_gpu_auto_path_takes_two_launches_for_cache_resident_in_place_windows():
+    """3,072+ envs whose in-place window fits the Infinity Cache keep the two-launch
+    stream (measured faster there); the same shape double-buffered, and smaller env
+    counts, take the one-launch step. Checked against the oracle at such a shape
+    (3,100 envs x 5 assets x 4 days: 25 chunks per env, the flat stream's seams inside envs)."""
+    from pmenv import TradingEnv
+    e = TradingEnv(num_envs=3100, num_assets=5, window=4, device=DEV)
+    db, ip = e.step_path.split(" | ")
+    assert db.startswith("step_env_kernel") and "advance_flat_inplace_kernel" in ip
+    assert TradingEnv(num_envs=3000, num_assets=5, window=4, device=DEV).step_path.count("step_env_kernel") == 2
+    _run_both({}, B=3100, N=5, W=4, T=13, kind="mixed", seed=31)
+
+
+@pytest.mark.parametrize("impl", ["one_launch", "two_launch"])
+def test_gpu_flat_resident_series_obs_out(impl):
+    """Day-indexed bars (resident series) double-buffered == the bar batch, bit for
+    bit; an out-of-range day reads NaN market channels, counted, not read."""
     from pmenv import TradingEnv, MarketSeries
     rng = np.random.default_rng(5)
     T, N, W, B, S = 200, 30, 20, 41, 30
@@ -233,8 +243,8 @@ def test_gpu_flat_resident_series_obs_out(monkeypatch):
     start = m.random_starts(B, W, S + 1, generator=torch.Generator().manual_seed(3))
     obs_a = m.initial_window(start, W)
     obs_b = obs_a.clone()
-    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
-    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
     ea.reset(obs_a)
     eb.reset(obs_b)
     act = torch.softmax(torch.randn(S, B, N, device=DEV), -1)
@@ -251,47 +261,94 @@ def test_gpu_flat_resident_series_obs_out(monkeypatch):
     assert bool(torch.isnan(nxt[7, :, -1, :4]).all()) and not bool(torch.isnan(nxt[6]).any())
 
 
-@pytest.mark.parametrize("k1", ["reg", "8x4", "16x2", "32x2", "32x2s", "64x2s"])
-@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
-def test_gpu_k1_packed_shapes_vs_oracle_modes(monkeypatch, k1, kw):
-    """The scalar step's packed form (scalar_step_vec_kernel: L lanes x A assets per
-    env, DPP butterfly reductions) in every lane/asset split against the oracle, in
-    every reward / ring / norm / commission mode; "reg" is the one-asset-per-lane form."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
-    monkeypatch.setenv("PMENV_K1", k1)
-    _run_both(kw, B=67, N=30, W=50, T=56, kind="mixed", seed=zlib.crc32(f"k1{k1}{kw}".encode()))
-
-
 @pytest.mark.parametrize("N,W,B", [(1, 4, 9), (4, 6, 13), (8, 10, 21), (9, 4, 5), (16, 8, 33), (17, 4, 7),
                                    (33, 4, 11), (64, 16, 3), (65, 4, 6), (129, 8, 5), (256, 4, 3), (300, 8, 4),
                                    (500, 50, 4), (512, 2, 3)])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
-def test_gpu_k1_packed_asset_counts(monkeypatch, N, W, B, db):
-    """Default packed shape per asset count (partial last lane, group edges at 8 / 16 /
-    32 / 64 lanes, N up to 512) through both window modes, against the oracle."""
-    monkeypatch.setenv("PMENV_FUSED", "0")
-    _run_both({}, B=B, N=N, W=W, T=W + 5, kind="mixed", seed=N * 31 + W, double_buffer=db)
+def test_gpu_k1_packed_asset_counts(N, W, B, db):
+    """The two-launch step's packed scalar-step shape per asset count (partial last
+    lane, group edges at 8 / 16 / 32 / 64 lanes, N up to 512) through both window
+    modes, against the oracle."""
+    _run_both({}, B=B, N=N, W=W, T=W + 5, kind="mixed", seed=N * 31 + W, double_buffer=db, impl="two_launch")
     _run_both({"commission": 0.0025, "norm": "or"}, B=B, N=N, W=W, T=W + 2, kind="rawpos", seed=N + 7 * W,
-              double_buffer=db)
+              double_buffer=db, impl="two_launch")
 
 
-@pytest.mark.parametrize("fused", ["0", "db", "all"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES[:1] + MODES[4:8], ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
-def test_gpu_fused_and_two_launch_agree_with_oracle(monkeypatch, fused, db, kw):
-    """PMENV_FUSED picks the one-launch step (scalar step inside the streaming
-    workgroup) or the two-launch path; both must match the oracle, in place and
-    double-buffered."""
-    monkeypatch.setenv("PMENV_FUSED", fused)
-    _run_both(kw, B=37, N=30, W=50, T=56, kind="mixed", seed=zlib.crc32(f"{kw}{fused}{db}".encode()),
-              double_buffer=db)
+def test_gpu_one_and_two_launch_agree(db, kw):
+    """The two implementations of the advance step on identical inputs: the windows
+    bit for bit, rewards / values to the last bits of their f64 sums (the two scalar
+    steps reduce in different orders)."""
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 37, 30, 50, 56
+    ser = synth.series(W + T, B, N, seed=zlib.crc32(f"{kw}{db}".encode()), device=DEV)
+    act = synth.actions(T, B, N, seed=7, device=DEV)
+    envs, obs = [], []
+    for impl in ("one_launch", "two_launch"):
+        e = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl, **kw)
+        o = synth.window_from_series(ser, W)
+        e.reset(o)
+        envs.append(e)
+        obs.append(o)
+    for t in range(T):
+        rs = []
+        for i, e in enumerate(envs):
+            if db:
+                r, obs[i] = e.step(act[t], obs[i], bar=ser[W + t], out=torch.empty_like(obs[i]))
+            else:
+                r, _ = e.step(act[t], obs[i], bar=ser[W + t])
+            rs.append(r)
+        assert torch.equal(obs[0][..., :4], obs[1][..., :4])
+        assert torch.allclose(obs[0], obs[1], rtol=2e-7, atol=1e-12)
+        assert torch.allclose(rs[0].double(), rs[1].double(), rtol=1e-6, atol=1e-9, equal_nan=True)
+        assert torch.allclose(envs[0].value, envs[1].value, rtol=1e-12)
 
 
-@pytest.mark.parametrize("N,W", [(64, 16), (33, 20), (8, 50), (1, 4)])
-def test_gpu_fused_shapes(monkeypatch, N, W):
-    monkeypatch.setenv("PMENV_FUSED", "all")
-    for db in (False, True):
-        _run_both({}, B=11, N=N, W=W, T=W + 9, kind="mixed", seed=N + W, double_buffer=db)
+@pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+@pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+def test_gpu_one_launch_vs_oracle_modes(kind, db, kw):
+    """step_env_kernel (one workgroup per env: the scalar step on wave 0 while the
+    window is in flight, the window advanced through an LDS image) in every reward /
+    ring / norm / commission mode, in place and double-buffered, through the ring wrap."""
+    from pmenv import TradingEnv
+    assert TradingEnv(num_envs=3, num_assets=30, window=50, device=DEV).step_path.count("step_env_kernel") == 2
+    _run_both(kw, B=37, N=30, W=50, T=56, kind=kind, seed=zlib.crc32(f"one{kw}{kind}{db}".encode()),
+              double_buffer=db, impl="one_launch")
+
+
+@pytest.mark.parametrize("N,W,B", [(30, 50, 37), (5, 4, 13), (4, 2, 7), (1, 4, 9), (64, 16, 3), (12, 10, 1),
+                                   (33, 20, 5), (8, 50, 11), (4, 50, 600), (64, 47, 3)])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_one_launch_shapes(N, W, B, db):
+    """Env windows from 2 to 1,000+ chunks: rows straddling chunks, W = 2, one asset,
+    envs starting at every offset inside a 1 KiB block, partial last wave, a
+    workgroup of one wave."""
+    _run_both({}, B=B, N=N, W=W, T=W + 9, kind="mixed", seed=N * 11 + W, double_buffer=db, impl="one_launch")
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 5 * W, double_buffer=db,
+              impl="one_launch")
+
+
+def test_gpu_step_impl_selection_rules():
+    """The one-launch step takes F = 5, W >= 2, N <= 64 windows whose 1 KiB blocks fit
+    15 waves of 4 chunks (64 KiB of LDS); a forced path that does not fit the shape is
+    refused (the handle keeps its path) and AUTO falls back by itself."""
+    from pmenv import TradingEnv
+    big = TradingEnv(num_envs=2, num_assets=64, window=50, device=DEV)       # 4,000 chunks per env
+    assert "step_env_kernel" not in big.step_path
+    with pytest.raises(ValueError):
+        big.set_step_impl("one_launch")
+    assert big.step_impl == "auto"
+    assert TradingEnv(num_envs=2, num_assets=64, window=47, device=DEV).step_path.count("step_env_kernel") == 2
+    assert "step_env_kernel" not in TradingEnv(num_envs=2, num_assets=65, window=4, device=DEV).step_path
+    odd = TradingEnv(num_envs=2, num_assets=5, window=50, device=DEV)           # not 16-B granular
+    assert odd.step_path == "step_advance_lds_kernel"
+    for impl in ("one_launch", "two_launch"):
+        with pytest.raises(ValueError):
+            odd.set_step_impl(impl)
+    with pytest.raises(ValueError):
+        TradingEnv(num_envs=2, num_assets=5, window=8, device=DEV, step_impl="fastest")
 
 
 def test_gpu_out_must_not_overlap():
@@ -346,8 +403,10 @@ def test_gpu_state_roundtrip():
     assert torch.equal(obs, obs_ck) and torch.equal(e1.value, e2.value)
 
 
-def test_gpu_full_size_properties():
-    """BASELINE config (65,536 envs x 30 assets x 50 x 5) through past the ring wrap:
+@pytest.mark.parametrize("impl", ["auto", "two_launch"])
+def test_gpu_full_size_properties(impl):
+    """BASELINE config (65,536 envs x 30 assets x 50 x 5) through past the ring wrap,
+    by the default one-launch step and by the two-launch path (the nt flat streams):
     market channels are exactly the sliding window of the series, the reward is
     log(sum w*y) with y the fp32 close relative, the value compounds the returns,
     and the weight channel is the ring in the reference's storage order."""
@@ -356,12 +415,13 @@ def test_gpu_full_size_properties():
     ser = synth.series(W + T, B, N, seed=11, device=DEV)
     act = synth.actions(T, B, N, seed=12, device=DEV)
     obs = synth.window_from_series(ser, W, F)
-    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
+    assert env.step_path.count("step_env_kernel") == (2 if impl == "auto" else 0)
     env.reset(obs)
     logv = torch.full((B,), float(np.log(25000.0)), dtype=torch.float64, device=DEV)
     spare = torch.empty_like(obs)
     for t in range(T):
-        # even steps in place, odd steps double-buffered (the flat stream)
+        # even steps in place, odd steps double-buffered
         if t % 2:
             r, nxt = env.step(act[t], obs, bar=ser[W + t], out=spare)
             obs, spare = nxt, obs
@@ -381,7 +441,7 @@ def test_gpu_full_size_properties():
     assert env.nonfinite_count() == 0
     # a sample of envs against the oracle on the same inputs, from a fresh reset
     S = 64
-    sub = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=DEV)
+    sub = TradingEnv(num_envs=S, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
     sobs = synth.window_from_series(ser[:, :S].contiguous(), W, F)
     from pmenv.config import EnvConfig
     cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F))
@@ -404,19 +464,16 @@ def test_gpu_synth_matches_oracle():
     np.testing.assert_allclose(a, synth_actions(6, 9, 7, env_offset=5, seed=4), rtol=1e-6)
 
 
-@pytest.mark.parametrize("T,B,path", [(5000, 3, "scan"), (257, 64, "scan"), (64, 65536, "loop"), (300, 10, "loop"),
-                                      (1, 5, "scan"), (63, 2, "scan"),
-                                      # tiled: T below / across / not a multiple of the segment, ragged B
-                                      (1, 5, "tile"), (37, 100, "tile"), (64, 64, "tile"), (129, 4099, "tile"),
-                                      (1000, 200, "tile"), (256, 65536, "tile"), (300, 130, "tile16")])
-def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
-    """GAE(gamma, lambda) over a [T, B] rollout: tiled scan, chunked wave scan and
-    per-env loop vs the oracle's sequential recursion (parity unpinned by the
-    reference)."""
+@pytest.mark.parametrize("T,B,kernel", [(300, 10, "scan"), (257, 63, "scan"), (1, 5, "tile16"), (63, 2, "tile16"),
+                                        # tiled: T below / across / not a multiple of the segment, ragged B
+                                        (37, 100, "tile16"), (64, 64, "tile16"), (129, 4099, "tile16"),
+                                        (300, 130, "tile16"), (256, 65536, "tile8"), (37, 16385, "tile8")])
+def test_gpu_gae_kernels_match_oracle(T, B, kernel):
+    """GAE(gamma, lambda) over a [T, B] rollout through the kernel each shape takes
+    (chunked wave scan for a handful of envs with long horizons, the tiled scan with
+    16- or 8-step lane segments) vs the oracle's sequential recursion (parity unpinned
+    by the reference)."""
     from pmenv import rollout
-    monkeypatch.setenv("PMENV_GAE", path.rstrip("16"))
-    if path.endswith("16"):
-        monkeypatch.setenv("PMENV_GAE_U", "16")
     rng = np.random.default_rng(T + B)
     r = rng.standard_normal((T, B)).astype(np.float32)
     v = rng.standard_normal((T + 1, B)).astype(np.float32)
@@ -425,33 +482,30 @@ def test_gpu_gae_scan_and_loop_match_oracle(T, B, path, monkeypatch):
     oadv, oret = or_gae(r, v, d, 0.99, 0.95)
     np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize("E,U", [(1, 8), (1, 16), (2, 8), (2, 4), (4, 4)])
-@pytest.mark.parametrize("T,B", [(1, 8), (37, 100), (37, 102), (64, 64), (129, 4100), (1000, 200), (256, 65536), (300, 132)])
-def test_gpu_gae_tile_vec_matches_oracle(T, B, E, U, monkeypatch):
-    """The pipelined tile (gae_tile_vec_kernel, E envs per lane): vs the oracle's
-    recursion, and bitwise equal to gae_tile_kernel at the same segment length U
-    (ragged B falls back to E = 1 where B % E != 0)."""
-    from pmenv import rollout
-    rng = np.random.default_rng(T * 3 + B)
-    r = rng.standard_normal((T, B)).astype(np.float32)
-    v = rng.standard_normal((T + 1, B)).astype(np.float32)
-    d = rng.random((T, B)) < 0.02
-    monkeypatch.setenv("PMENV_GAE", "tile")
-    monkeypatch.setenv("PMENV_GAE_U", str(U))
-    monkeypatch.setenv("PMENV_GAE_E", str(E))
-    adv, ret = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
-    oadv, oret = or_gae(r, v, d, 0.99, 0.95)
-    np.testing.assert_allclose(adv.cpu().numpy(), oadv, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(ret.cpu().numpy(), oret, rtol=1e-5, atol=1e-5)
-    if U in (8, 16):
-        monkeypatch.delenv("PMENV_GAE_E")
-        adv0, ret0 = rollout.gae(_t(r), _t(v), _t(d, torch.bool), 0.99, 0.95)
-        assert torch.equal(adv, adv0) and torch.equal(ret, ret0)
-    adv2, _ = rollout.gae(_t(r), _t(v), None, 0.99, 1.0)            # no dones
+    adv2, _ = rollout.gae(_t(r), _t(v), None, 0.99, 1.0)            # no dones, lambda = 1: long carries
     oadv2, _ = or_gae(r, v, np.zeros_like(d), 0.99, 1.0)
     np.testing.assert_allclose(adv2.cpu().numpy(), oadv2, rtol=1e-5, atol=1e-4)
+
+
+def test_gpu_gae_per_env_loop_beyond_tile_offsets():
+    """A rollout whose [T+1, B] value array passes the tiled scan's 2^31-byte offsets
+    (T = 1, B = 2^28) takes the per-env loop kernel: vs the oracle's recursion on a
+    strided sample of envs, and the closed form adv = r + gamma*(1-d)*v1 - v0 for all."""
+    from pmenv import rollout
+    T, B = 1, 1 << 28
+    g = torch.Generator(device=DEV).manual_seed(9)
+    r = torch.randn(T, B, device=DEV, generator=g)
+    v = torch.randn(T + 1, B, device=DEV, generator=g)
+    d = torch.rand(T, B, device=DEV, generator=g) < 0.02
+    adv, ret = rollout.gae(r, v, d, 0.99, 0.95)
+    expect = (r.double() + 0.99 * (~d).double() * v[1:].double() - v[:1].double()).float()
+    assert torch.allclose(adv, expect, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(ret, adv + v[:1], rtol=1e-6, atol=1e-6)
+    pick = torch.arange(0, B, 4099, device=DEV)
+    oadv, oret = or_gae(r[:, pick].cpu().numpy(), v[:, pick].cpu().numpy(), d[:, pick].cpu().numpy(), 0.99, 0.95)
+    np.testing.assert_allclose(adv[:, pick].cpu().numpy(), oadv, rtol=1e-6, atol=1e-6)
+    del r, v, d, adv, ret, expect
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 8192), (700, 4099),
@@ -562,15 +616,8 @@ def test_gpu_step_is_graph_capturable():
     assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)
 
 
-@pytest.fixture(params=["fused", "flat"])
-def step_kernels(request, monkeypatch):
-    """B = 97 takes the one-launch step by default; "flat" forces the two-launch flat path."""
-    if request.param == "flat":
-        monkeypatch.setenv("PMENV_FUSED", "0")
-    return request.param
-
-
-def test_gpu_resident_series_equals_bar_batch(step_kernels):
+@pytest.mark.parametrize("impl", ["one_launch", "two_launch"])
+def test_gpu_resident_series_equals_bar_batch(impl):
     """Resident-series data path (env b reads series[day[b]]) == stepping with the
     gathered bar batch, bit for bit; windows initialised from per-env start days."""
     from pmenv import TradingEnv, MarketSeries
@@ -584,8 +631,8 @@ def test_gpu_resident_series_equals_bar_batch(step_kernels):
     ref = np.stack([bars[int(s):int(s) + W].transpose(1, 0, 2) for s in start.cpu()]).astype(np.float32)
     assert np.array_equal(obs_a[..., :4].cpu().numpy(), ref)
     obs_b = obs_a.clone()
-    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
-    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
     ea.reset(obs_a)
     eb.reset(obs_b)
     act = torch.softmax(torch.randn(S, B, N, device=DEV), -1)
@@ -602,26 +649,18 @@ def test_gpu_resident_series_equals_bar_batch(step_kernels):
     assert ea.nonfinite_count() == 1
 
 
-@pytest.mark.parametrize("T,N,W,B,H,knob", [
-    (200, 30, 12, 33, 40, ""),                   # F = 5 vector staging (4 pairs per thread)
-    (200, 30, 12, 33, 40, "PMENV_REPLAY_LDS"),   # per-element LDS staging, 16-B stores
-    (300, 30, 50, 17, 80, ""),                   # F = 5 vector staging, 8 pairs per thread (BASELINE shape)
-    (60, 3, 5, 4, 9, ""),                        # LDS-staged, sample block not 16-B granular
-    (120, 300, 50, 3, 60, ""),                   # staged days > 64 KiB: per-float kernel
-    (200, 30, 12, 33, 40, "PMENV_REPLAY_GRID=5"),      # persistent F = 5 loop: 13 samples per workgroup
-    (300, 30, 50, 17, 80, "PMENV_REPLAY_GRID=3"),      # persistent, 8 pairs per thread, ragged tail
-    (300, 30, 50, 17, 80, "PMENV_REPLAY_PERSIST=0"),   # one workgroup per sample, nt stores
-    (300, 30, 50, 17, 80, "PMENV_REPLAY_TPB=512"),     # one workgroup per sample, 512 threads
-    (300, 30, 50, 17, 80, "PMENV_REPLAY_NT=0")])       # persistent, default-policy stores
-def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch):
+@pytest.mark.parametrize("T,N,W,B,H,S", [
+    (200, 30, 12, 33, 40, 64),     # F = 5 vector staging (4 pairs per thread), persistent gather
+    (300, 30, 50, 17, 80, 64),     # F = 5, 8 pairs per thread (BASELINE shape)
+    (200, 30, 12, 33, 40, 1301),   # persistent loop: several samples per workgroup, ragged tail
+    (60, 3, 5, 4, 9, 64),          # LDS-staged, sample block not 16-B granular
+    (120, 300, 50, 3, 60, 16)])    # staged days > 64 KiB: per-float kernel
+def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, S):
     """replay/buffer.py:39-79 sample on device vs the numpy restatement
     (the reference module is not importable: parity restated from its text)."""
     from pmenv import MarketSeries
     from pmenv.replay import DeviceReplay
     from oracle import replay_gather
-    if knob:
-        k, _, v = knob.partition("=")
-        monkeypatch.setenv(k, v or "1")
     rng = np.random.default_rng(4)
     bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
     m = MarketSeries(bars, device=DEV)
@@ -629,7 +668,7 @@ def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch)
     for h in range(H + 17):                      # wraps the ring; some windows run off the series ends
         rb.add(torch.full((B,), (W + h) % (T + 3) - 2, dtype=torch.int32, device=DEV),
                torch.rand(B, N, device=DEV), torch.randn(B, device=DEV))
-    h0, env = rb.indices(64, generator=torch.Generator().manual_seed(1))
+    h0, env = rb.indices(S, generator=torch.Generator().manual_seed(1))
     s, a, r, s2 = rb.gather(h0, env)
     es, ea, er, es2 = replay_gather(bars, rb.days.cpu().numpy(), rb.actions.cpu().numpy(), rb.rewards.cpu().numpy(),
                                     h0.cpu().numpy(), env.cpu().numpy(), W)
@@ -640,10 +679,8 @@ def test_gpu_replay_gather_matches_restatement(T, N, W, B, H, knob, monkeypatch)
 
 def test_gpu_replay_gather_full_size_persistent():
     """The replay at the f4 bench shape (4,096 envs x 256 recorded steps, 8,192 samples
-    of 30 assets x 50 days): the default persistent gather (one workgroup per CU, ~32
-    samples each, the next sample's loads in flight) vs the restatement on 512 of the
-    samples, and bitwise equal to the one-workgroup-per-sample form on all of them."""
-    import os
+    of 30 assets x 50 days): the persistent gather (one workgroup per CU, ~32 samples
+    each, the next sample's loads in flight) vs the restatement on 512 of the samples."""
     from pmenv import MarketSeries
     from pmenv.replay import DeviceReplay
     from oracle import replay_gather
@@ -658,12 +695,6 @@ def test_gpu_replay_gather_full_size_persistent():
         rb.add(day0 + h % H, torch.rand(B, N, device=DEV, generator=g), torch.randn(B, device=DEV, generator=g))
     h0, env = rb.indices(S, generator=torch.Generator().manual_seed(6))
     s, a, r, s2 = rb.gather(h0, env)
-    os.environ["PMENV_REPLAY_PERSIST"] = "0"
-    try:
-        s_b, a_b, r_b, s2_b = rb.gather(h0, env)
-    finally:
-        del os.environ["PMENV_REPLAY_PERSIST"]
-    assert torch.equal(s, s_b) and torch.equal(s2, s2_b) and torch.equal(a, a_b) and torch.equal(r, r_b)
     pick = np.sort(np.random.default_rng(7).choice(S, 512, replace=False))
     es, ea, er, es2 = replay_gather(bars, rb.days.cpu().numpy(), rb.actions.cpu().numpy(), rb.rewards.cpu().numpy(),
                                     h0.cpu().numpy()[pick], env.cpu().numpy()[pick], W)
@@ -672,29 +703,8 @@ def test_gpu_replay_gather_full_size_persistent():
     assert np.array_equal(a.cpu().numpy()[pick, :, 0], ea) and np.array_equal(r.cpu().numpy()[pick, 0, 0], er)
 
 
-@pytest.mark.parametrize("B,N,T", [(300, 30, 80), (4097, 30, 252), (9, 257, 5), (70, 1, 2)])
-def test_gpu_metrics_one_launch_equals_two(B, N, T, monkeypatch):
-    """metrics_fused_kernel (both passes in one launch, either block order) writes
-    bitwise what the two launches write."""
-    from pmenv.replay import trajectory_metrics
-    g = torch.Generator(device=DEV).manual_seed(B + N + T)
-    rets = 0.01 * torch.randn(T, B, device=DEV, dtype=torch.float64, generator=g)
-    vals = torch.cumprod(torch.cat([torch.ones(1, B, device=DEV, dtype=torch.float64), 1 + rets]), 0)
-    wts = torch.softmax(torch.randn(T + 1, B, N, device=DEV, generator=g), -1)
-    outs = []
-    for knobs in ({}, {"PMENV_METRICS_SEG_FIRST": "0"}, {"PMENV_METRICS_FUSED": "0"}):
-        for k in ("PMENV_METRICS_SEG_FIRST", "PMENV_METRICS_FUSED"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in knobs.items():
-            monkeypatch.setenv(k, v)
-        m = trajectory_metrics(rets, vals, wts)
-        outs.append(torch.stack([m[k] for k in ("sharpe", "sortino", "max_drawdown", "average_turnover",
-                                                "final_value")]))
-    for o in outs[1:]:
-        assert torch.equal(o.view(torch.int64), outs[0].view(torch.int64))
-
-
-@pytest.mark.parametrize("B,N,W,T", [(300, 30, 20, 80), (5, 300, 4, 9), (70, 1, 3, 2), (9, 257, 2, 5)])
+@pytest.mark.parametrize("B,N,W,T", [(300, 30, 20, 80), (5, 300, 4, 9), (70, 1, 3, 2), (9, 257, 2, 5),
+                                     (4097, 30, 10, 252)])
 def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
     """util/eval.py:14-37 metrics over an env trajectory vs the numpy restatement
     (quantstats is absent: parity unpinned by the reference)."""
@@ -719,25 +729,31 @@ def test_gpu_trajectory_metrics_match_restatement(B, N, W, T):
 
 def test_gpu_beyond_flat_index_range_in_place():
     """A window past the flat stream's 32-bit chunk index (1.2 M envs x 30 x 50 x 5 =
-    36 GB, 2.25e9 chunks): the handle falls back to the row kernel, and one in-place
-    step still shifts every sampled env's window by one day, appends its bar and
-    writes a finite reward (start, middle and end of the tensor)."""
+    36 GB, 2.25e9 chunks): the one-launch step (64-bit env offsets) and the two-launch
+    fallback (the row kernel) each step in place, shifting every sampled env's window
+    by one day, appending its bar and writing a finite reward (start, middle and end
+    of the tensor)."""
     from pmenv import TradingEnv
     B, N, W = 1_200_000, 30, 50
     env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
-    assert "advance_flat_inplace_kernel" not in env.step_path.split("|")[-1]
+    assert env.step_path.split(" | ")[1].startswith("step_env_kernel")
     g = torch.Generator(device=DEV).manual_seed(3)
     obs = torch.rand(B, N, W, 5, device=DEV, generator=g) + 0.5
     env.reset(obs)
-    bar = torch.rand(B, N, 4, device=DEV, generator=g) + 0.5
-    act = torch.softmax(torch.randn(B, N, device=DEV, generator=g), -1)
     pick = torch.tensor([0, 1, B // 2, B - 2, B - 1], device=DEV)
-    before = obs[pick].clone()
-    r, out = env.step(act, obs, bar=bar)
-    assert out is obs
-    after = obs[pick]
-    assert torch.equal(after[:, :, :-1, :], before[:, :, 1:, :])
-    assert torch.equal(after[:, :, -1, :4], bar[pick])
-    assert torch.isfinite(r).all() and env.nonfinite_count() == 0
-    del obs, bar, env
+    for impl in ("one_launch", "two_launch"):
+        env.set_step_impl(impl)
+        if impl == "two_launch":
+            assert "advance_rows_kernel" in env.step_path.split(" | ")[1]
+        bar = torch.rand(B, N, 4, device=DEV, generator=g) + 0.5
+        act = torch.softmax(torch.randn(B, N, device=DEV, generator=g), -1)
+        before = obs[pick].clone()
+        r, out = env.step(act, obs, bar=bar)
+        assert out is obs
+        after = obs[pick]
+        assert torch.equal(after[:, :, :-1, :], before[:, :, 1:, :])
+        assert torch.equal(after[:, :, -1, :4], bar[pick])
+        assert torch.isfinite(r).all() and env.nonfinite_count() == 0
+        del bar, act
+    del obs, env
     torch.cuda.empty_cache()

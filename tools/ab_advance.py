@@ -8,6 +8,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("PMENV_LIB", os.path.join(ROOT, "tools", "libpmenv_ab.so"))  # the A/B knobs: tools build
 sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
 import torch  # noqa: E402
 from pmenv import TradingEnv, synth, _abi  # noqa: E402
@@ -35,7 +36,8 @@ day0 = torch.randint(W, a.series_days - a.H, (B,), generator=torch.Generator().m
 days = [day0 + t for t in range(a.H)]
 KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED", "PMENV_K1_GROUPS",
          "PMENV_STREAM_BLOCK", "PMENV_STREAM_POL", "PMENV_FLAT", "PMENV_FLAT_BLOCK",
-         "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK", "PMENV_FLAT_IP_VEC", "PMENV_FLAT_DB_WG", "PMENV_K1")
+         "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK", "PMENV_FLAT_IP_VEC", "PMENV_FLAT_DB_WG", "PMENV_K1",
+         "PMENV_ONE", "PMENV_ONE_V", "PMENV_ONE_S80", "PMENV_FLAT_S80")
 for v in a.variants.split(","):
     # "base+KNOB=val+...": extra env knobs at creation (e.g. "o+PMENV_FUSED=0")
     base, *extra = v.split("+")
@@ -104,7 +106,7 @@ for v, (e, obs, rew, obs2) in envs.items():
     else:
         # variants of the scalar step's reduction shape (PMENV_K1) differ in the last f64
         # bits of the sums; every other variant must agree bit for bit
-        if "PMENV_K1" in v:
+        if "PMENV_K1" in v or ("PMENV_ONE" in v) != ("PMENV_ONE" in next(iter(envs))):
             assert torch.equal(obs[..., :4], ref[0][..., :4]), f"{v}: market channels differ"
             assert torch.allclose(obs, ref[0], rtol=2e-7, atol=1e-12), f"{v}: weights differ"
             assert torch.allclose(rew, ref[1], rtol=1e-6, atol=1e-9), f"{v}: reward differs"

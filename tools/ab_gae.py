@@ -14,6 +14,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("PMENV_LIB", os.path.join(ROOT, "tools", "libpmenv_ab.so"))  # the A/B knobs: tools build
 sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
 import torch  # noqa: E402
 from pmenv import _abi  # noqa: E402

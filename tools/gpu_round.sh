@@ -1,16 +1,19 @@
-# Full GPU pass: parity tests, smoke, bench, rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes.
+# Full GPU pass: parity tests, smoke, bench (default and the driver's short form),
+# rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes.
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1
+timeout -k 10 1200 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
+    > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests_$TAG.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 tail -1 gpurun_out/bench_$TAG.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_short_$TAG.json 2> gpurun_out/bench_short_$TAG.err || exit $?
 ARGS="--steps 200 --warmup 20 --cpu-baseline 0 --alt-steps 50"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_$TAG.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --alt-steps 0 > gpurun_out/pmc_fetch_$TAG.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --alt-steps 0 > gpurun_out/pmc_write_$TAG.log 2>&1 || exit $?
-grep -E "advance_|scalar_step" gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -c1-170
+grep -E "step_env|advance_|scalar_step" gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -c1-170
