@@ -88,7 +88,7 @@ struct pmenv {
     int fused;            // PMENV_FUSE_* bits: advance_rows_kernel<fused> (PMENV_FUSED)
     int fused_vec;
     int ablate;           // PMENV_ABLATE timing-only variants
-    bool one_s80, flat_s80;
+    bool one_nocap, flat_s80;
     size_t lds_scalar, lds_stream;
     char err[512];
 };
@@ -343,15 +343,15 @@ void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
 }
 
 bool launch_scalar_vec(int vec, const StepParams& p, hipStream_t stream) {
-    switch (vec) {   // the shapes pick_k1_vec chooses per asset count
-    case 801: launch_scalar_vec_la<8, 1, false>(p, stream); return true;
-    case 802: launch_scalar_vec_la<8, 2, false>(p, stream); return true;
-    case 1602: launch_scalar_vec_la<16, 2, false>(p, stream); return true;
-    case 1604: launch_scalar_vec_la<16, 4, false>(p, stream); return true;
+    switch (vec) {   // the shapes pick_k1_vec chooses per asset count (N > 64)
     case kK1Str + 6402: launch_scalar_vec_la<64, 2, true>(p, stream); return true;
     case kK1Str + 6404: launch_scalar_vec_la<64, 4, true>(p, stream); return true;
     case kK1Str + 6408: launch_scalar_vec_la<64, 8, true>(p, stream); return true;
 #ifdef PMENV_AB
+    case 801: launch_scalar_vec_la<8, 1, false>(p, stream); return true;
+    case 802: launch_scalar_vec_la<8, 2, false>(p, stream); return true;
+    case 1602: launch_scalar_vec_la<16, 2, false>(p, stream); return true;
+    case 1604: launch_scalar_vec_la<16, 4, false>(p, stream); return true;
     case 804: launch_scalar_vec_la<8, 4, false>(p, stream); return true;
     case 1601: launch_scalar_vec_la<16, 1, false>(p, stream); return true;
     case 1608: launch_scalar_vec_la<16, 8, false>(p, stream); return true;
@@ -366,14 +366,24 @@ bool launch_scalar_vec(int vec, const StepParams& p, hipStream_t stream) {
 
 // K1 shape per asset count (tools build: the PMENV_K1 knob "reg" | "LxA" | "LxAs"
 // strided, e.g. "16x2", "64x8s"). 0: the register form (N <= 64) or the LDS form (N > 512).
+// N <= 64 takes the register form: its reductions (one asset per lane, DPP row shifts,
+// the fixed-order row combine) are bitwise those of the one-launch step's scalar part,
+// so the two paths — and therefore sharded and unsharded runs, whose path can differ
+// by env count — give the same bits. It costs 4.6 us at 65,536 envs over the packed
+// 16 x 2 form (29.1 vs 24.5 us), and the two-launch path runs for N <= 64 only on
+// cache-resident in-place windows (<= 8,192 envs at N = 30): < 1 us per step.
 int pick_k1_vec(const pmenv_cfg& c) {
     const int N = c.num_assets;
     if ((int64_t)c.num_envs * N * 4 >= (1ll << 32)) return 0;     // descriptors span the [B*N] arrays
     int v = 0;
+#ifdef PMENV_AB
     if (N <= 8) v = 801;
     else if (N <= 16) v = 802;
     else if (N <= 32) v = 1602;
     else if (N <= 64) v = 1604;
+    else
+#endif
+    if (N <= 64) v = 0;
     else if (N <= 128) v = kK1Str + 6402;
     else if (N <= 256) v = kK1Str + 6404;
     else if (N <= 512) v = kK1Str + 6408;
@@ -419,9 +429,10 @@ void launch_one_v(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const bool out = p.obs_out != p.obs;
     const int pol = out ? h->flat_pol : h->flat_ip_pol;
     const unsigned threads = 64u * (unsigned)h->one_waves;
-    const size_t lds = ((size_t)threads * V + 2) * 16;
+    size_t lds = ((size_t)threads * V + 2) * 16;
     const unsigned grid = (unsigned)h->cfg.num_envs;
 #ifdef PMENV_AB
+    lds += (size_t)ab_int("PMENV_ONE_LDS_PAD", 0);    // occupancy study: fewer workgroups per CU
     if (h->ablate == 128 || h->ablate == 130) {    // timing-only: no scalar step / unconditional side reads
         if (h->ablate == 128 && out) step_env_kernel<V, true, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
         else if (h->ablate == 128) step_env_kernel<V, false, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
@@ -429,11 +440,11 @@ void launch_one_v(const pmenv* h, const StepParams& p, hipStream_t stream) {
         else step_env_kernel<V, false, 1, 2><<<grid, threads, lds, stream>>>(p, h->per4);
         return;
     }
-    if (h->one_s80) {
-        if (out && pol == 1) step_env_s80_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (out) step_env_s80_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (pol == 1) step_env_s80_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else step_env_s80_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+    if (h->one_nocap) {
+        if (out && pol == 1) step_env_nocap_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (out) step_env_nocap_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
+        else if (pol == 1) step_env_nocap_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
+        else step_env_nocap_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
         return;
     }
 #endif
@@ -657,7 +668,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     if (const char* knob = ab_knob("PMENV_ADVANCE"))   // force the single-launch LDS kernel
         if (!strcmp(knob, "lds")) h->streaming = h->flat = h->flat_inplace = false;
     h->ablate = ab_int("PMENV_ABLATE", 0);
-    h->one_s80 = ab_int("PMENV_ONE_S80", 0) != 0;
+    h->one_nocap = ab_int("PMENV_ONE_NOCAP", 0) != 0;
     h->flat_s80 = ab_int("PMENV_FLAT_S80", 0) != 0;
 #endif
     h->k1_groups = ab_int("PMENV_K1_GROUPS", 1);

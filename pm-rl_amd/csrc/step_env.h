@@ -119,18 +119,19 @@ __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4
     }
 }
 
+// Held to 80 SGPRs (the compiler spills ~20 to VGPR lanes): gfx950 admits
+// floor(800 / (ceil(sgpr / 16) * 16 + 16)) waves per SIMD — 7 at 82-96 SGPRs, 8 at
+// <= 80 (MI355X_MICROARCH.md, Residency); measured 647-651 against 651-658 us per step
+// uncapped at the BASELINE shape (profiles/ab_r02/r02e_*, r02f_*, r02j_*).
 template <int V, bool OUT, int POL, int ABL = 0>
-__global__ __launch_bounds__(1024) void step_env_kernel(StepParams p, uint32_t per4) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_sgpr(80))) void step_env_kernel(StepParams p,
+                                                                                             uint32_t per4) {
     step_env_body<V, OUT, POL, ABL>(p, per4);
 }
 
-// The same kernel held to 80 SGPRs (the spill goes to VGPR lanes): gfx950 admits
-// floor(800 / (ceil(sgpr / 16) * 16 + 16)) waves per SIMD, 7 at 82-96 SGPRs and 8 at
-// <= 80 (MI355X_MICROARCH.md, Residency), i.e. four 8-wave workgroups per CU instead
-// of three.
+// tools build: the same kernel without the SGPR cap
 template <int V, bool OUT, int POL, int ABL = 0>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_sgpr(80))) void step_env_s80_kernel(StepParams p,
-                                                                                                 uint32_t per4) {
+__global__ __launch_bounds__(1024) void step_env_nocap_kernel(StepParams p, uint32_t per4) {
     step_env_body<V, OUT, POL, ABL>(p, per4);
 }
 

@@ -52,6 +52,7 @@ class OffPolicy:
             raise ValueError("series too short for start + window + steps")
         obs = self.series.initial_window(start, self.W)
         self.env.reset(obs)
+        self.replay.new_episode()                 # no sampled window spans the reset
         day = start + self.W                      # the bar each env appends next
         rewards = []
         for _ in range(steps):

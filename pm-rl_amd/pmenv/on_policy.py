@@ -36,6 +36,18 @@ class WindowPolicy(torch.nn.Module):
         return self.net(x.reshape(S, N, W * F))
 
 
+class WindowCritic(torch.nn.Module):
+    """Value head over the whole window (a stand-in critic: the reference's A2C has
+    none): [S, N, W, F] -> [S]."""
+
+    def __init__(self, window, features=5, hidden=32):
+        super().__init__()
+        self.body = WindowPolicy(window, features, hidden)
+
+    def forward(self, s):
+        return self.body(s).mean(dim=(1, 2))
+
+
 class OnPolicy:
     def __init__(self, env, policy, horizon, series=None, lr=1e-3, batch_size=256, generator=None):
         cfg = env.cfg
@@ -74,5 +86,39 @@ class OnPolicy:
             loss = a2c_loss(self.policy(s), v_prev, a_prev, p)
             loss.backward()
             self.optim.step()
+            losses.append(loss.detach())
+        return torch.stack(losses) if losses else torch.empty(0)
+
+    def advantages(self, critic, gamma=0.99, lam=0.95, group=None, eps=1e-8):
+        """The return pass the north star adds to replay/rollout_buffer.py (which stores
+        (s, a, v, r) and computes nothing, :43-57): the critic's values of every stored
+        window -> GAE(gamma, lambda) as the HIP scan (DeviceRolloutBuffer.returns) ->
+        advantages normalised with moments summed over every rank (pmenv.parallel.normalize:
+        HIP moments kernel + one 24-byte all-reduce, RCCL over xGMI under "nccl").
+        critic: [S, N, W, F] windows -> [S] (or [S, 1]) values. Returns (normalised
+        advantages [T, B], returns [T, B], values [T+1, B])."""
+        from . import parallel
+        T = len(self.buf)
+        with torch.no_grad():
+            values = torch.stack([critic(self.buf.obs(t)).reshape(-1) for t in range(T + 1)]).float()
+        adv, ret = self.buf.returns(values, gamma, lam)
+        return parallel.normalize(adv, group=group, eps=eps), ret, values
+
+    def update_critic(self, critic, optim, returns, batch_size=None, generator=None):
+        """Regress the critic on the GAE returns (the value baseline of an actor-critic),
+        over random minibatches of the stored (step, env) windows. Returns the losses."""
+        T, B = returns.shape
+        n = T * B
+        bs = n if not batch_size or batch_size < 0 else batch_size
+        perm = torch.randperm(n, generator=generator).to(returns.device)
+        losses = []
+        for i in range(0, n - bs + 1, bs):
+            idx = perm[i:i + bs]
+            t, env = idx // B, idx % B
+            pred = critic(self.buf.s[t, env]).reshape(-1)
+            loss = torch.nn.functional.mse_loss(pred, returns[t, env])
+            optim.zero_grad(set_to_none=True)
+            loss.backward()
+            optim.step()
             losses.append(loss.detach())
         return torch.stack(losses) if losses else torch.empty(0)

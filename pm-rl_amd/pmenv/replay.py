@@ -20,6 +20,16 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def valid_starts(row_episode, oldest, count, W, H):
+    """Offsets st (from the oldest recorded row) whose W+1 rows st .. st+W all belong to
+    one episode — the reference samples a window inside one epoch of its [epoch, step]
+    layout (buffer.py:17-21, :47-51). Episode ids only grow along the ring, so the
+    first and the last row of a window decide. st < count - W - 1, as buffer.py:50
+    draws starts below epoch_len - WINDOW_SIZE - 1."""
+    return [st for st in range(max(count - W - 1, 0))
+            if row_episode[(oldest + st) % H] == row_episode[(oldest + st + W) % H]]
+
+
 class DeviceReplay:
     def __init__(self, num_envs, num_assets, window, capacity, series, features=5):
         if capacity < window + 2:
@@ -32,9 +42,19 @@ class DeviceReplay:
         self.rewards = torch.zeros(capacity, num_envs, dtype=torch.float32, device=dev)
         self.head = 0
         self.count = 0
+        # episode id of every ring row (all envs record in lockstep, so one id per row)
+        self.episode = 0
+        self._row_ep = [0] * capacity
+        self._starts = None           # device tensor of valid starts when some windows straddle episodes
+        self._starts_key = None
 
     def __len__(self):
         return self.count
+
+    def new_episode(self):
+        """Steps added from now on belong to a new episode (the env was reset): no sampled
+        window spans the boundary (buffer.py keeps each epoch in its own row)."""
+        self.episode += 1
 
     def add(self, day, action, reward):
         """buffer.py:23-37: one recorded step for every env."""
@@ -42,11 +62,13 @@ class DeviceReplay:
         self.days[h].copy_(torch.as_tensor(day).reshape(self.B))
         self.actions[h].copy_(torch.as_tensor(action).reshape(self.B, self.N))
         self.rewards[h].copy_(torch.as_tensor(reward).reshape(self.B))
+        self._row_ep[h] = self.episode
         self.head = (h + 1) % self.H
         self.count = min(self.count + 1, self.H)
 
     def indices(self, batch_size, generator=None):
-        """Random (start, env) pairs with W+1 consecutive recorded steps (buffer.py:47-51)."""
+        """Random (start, env) pairs with W+1 consecutive recorded steps of one episode
+        (buffer.py:47-51)."""
         span = self.count - self.W - 1
         if span < 1:
             raise ValueError("not enough recorded steps to sample a window")
@@ -54,9 +76,21 @@ class DeviceReplay:
         # costs a host->device copy per batch; no generator or a device one stays on the GPU
         dev = self.days.device
         gdev = generator.device if generator is not None else dev
-        st = torch.randint(0, span, (batch_size,), generator=generator, device=gdev)
-        env = torch.randint(0, self.B, (batch_size,), generator=generator, device=gdev)
         oldest = (self.head - self.count) % self.H
+        key = (oldest, self.count, self._row_ep[oldest], self._row_ep[(oldest + self.count - 1) % self.H])
+        if self._starts_key != key:
+            self._starts_key = key
+            ok = valid_starts(self._row_ep, oldest, self.count, self.W, self.H)
+            if not ok:
+                raise ValueError("no episode holds W + 1 recorded steps")
+            self._starts = None if len(ok) == span else torch.tensor(ok, dtype=torch.int64, device=gdev)
+        if self._starts is None:
+            st = torch.randint(0, span, (batch_size,), generator=generator, device=gdev)
+        else:
+            if self._starts.device != torch.device(gdev):
+                self._starts = self._starts.to(gdev)
+            st = self._starts[torch.randint(0, self._starts.numel(), (batch_size,), generator=generator, device=gdev)]
+        env = torch.randint(0, self.B, (batch_size,), generator=generator, device=gdev)
         h0 = (oldest + st) % self.H
         return h0.to(dev, torch.int32), env.to(dev, torch.int32)
 

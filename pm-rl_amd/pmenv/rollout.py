@@ -24,9 +24,14 @@ def gae(rewards, values, dones=None, gamma=0.99, lam=0.95):
     T, B = rewards.shape
     if tuple(values.shape) != (T + 1, B):
         raise ValueError(f"values must be [T+1, B] = {(T + 1, B)}, got {tuple(values.shape)}")
+    if not rewards.is_cuda:
+        raise ValueError("rewards must be a GPU tensor (the pass runs on its device)")
+    if dones is not None and tuple(dones.shape) != (T, B):
+        raise ValueError(f"dones must be [T, B] = {(T, B)}, got {tuple(dones.shape)}")
+    # every operand on the rewards' device: a host pointer would fault the kernel
     r = rewards.to(torch.float32).contiguous()
-    v = values.to(torch.float32).contiguous()
-    d = dones.to(torch.uint8).contiguous() if dones is not None else None
+    v = values.to(device=r.device, dtype=torch.float32).contiguous()
+    d = dones.to(device=r.device, dtype=torch.uint8).contiguous() if dones is not None else None
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
     s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
@@ -40,6 +45,8 @@ def gae(rewards, values, dones=None, gamma=0.99, lam=0.95):
 def moments(x):
     """{count, sum, sum of squares} of x in f64 (device tensor [3])."""
     lib = _abi.load()
+    if not x.is_cuda:
+        raise ValueError("moments needs a GPU tensor")
     x = x.to(torch.float32).contiguous().reshape(-1)
     out = torch.empty(3, dtype=torch.float64, device=x.device)
     work = torch.empty(lib.pmenv_moments_workspace() // 8, dtype=torch.float64, device=x.device)

@@ -112,7 +112,7 @@ def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
     for k in kernels:
         args = [a.strip() for a in k[k.index("<") + 1:-1].split(",")]
         name = k[:k.index("<")]
-        assert "s80" not in name, k
+        assert "s80" not in name and "nocap" not in name, k
         if name == "advance_flat_inplace_kernel":
             assert args == ["512", "2", args[2], "0"] and args[2] in ("0", "1"), k   # 512 x 2, no SKIP bits
         if name == "step_env_kernel":

@@ -88,3 +88,28 @@ def test_gpu_off_policy_collect_update_evaluate(B, N, W, steps, cap):
     for k in ("sharpe", "sortino", "max_drawdown", "average_turnover"):
         assert torch.isfinite(met[k]).all(), k
     assert env.info is not None and len(env.info["values"]) == 31
+
+
+def test_gpu_replay_windows_never_straddle_collect_calls():
+    """Two collect calls from different start days into one replay ring: every sampled
+    window's W+1 rows belong to one episode and hold consecutive days of one env
+    (advisor finding: a window spanning the reset mixed two episodes' actions)."""
+    from pmenv import MarketSeries, TradingEnv
+    from pmenv.off_policy import OffPolicy
+    B, N, W, T = 40, 7, 6, 300
+    rng = np.random.default_rng(3)
+    bars = (100 * np.exp(0.01 * rng.standard_normal((T, N, 4)).cumsum(0))).astype(np.float32)
+    m = MarketSeries(bars, device=DEV)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    loop = OffPolicy(env, m, capacity=50, batch_size=16)
+    g = torch.Generator().manual_seed(5)
+    loop.collect(m.random_starts(B, W, 30, generator=g), 30)
+    loop.collect(m.random_starts(B, W, 30, generator=g), 30)   # a reset: a new episode in the same ring
+    rb = loop.replay
+    h0, e = rb.indices(4000, generator=torch.Generator().manual_seed(6))
+    rows = (h0.long().cpu()[:, None] + torch.arange(W + 1)[None, :]) % rb.H
+    eps = torch.tensor(rb._row_ep)[rows]
+    assert bool((eps == eps[:, :1]).all())
+    days = rb.days.cpu()[rows, e.long().cpu()[:, None]]
+    assert bool((days[:, 1:] - days[:, :-1] == 1).all())
+    assert len(set(eps[:, 0].tolist())) == 2                   # both episodes are sampled

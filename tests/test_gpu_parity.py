@@ -277,9 +277,10 @@ def test_gpu_k1_packed_asset_counts(N, W, B, db):
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES[:1] + MODES[4:8], ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
 def test_gpu_one_and_two_launch_agree(db, kw):
-    """The two implementations of the advance step on identical inputs: the windows
-    bit for bit, rewards / values to the last bits of their f64 sums (the two scalar
-    steps reduce in different orders)."""
+    """The two implementations of the advance step on identical inputs agree bit for
+    bit (N <= 64: the two-launch path's register-form scalar step reduces in the same
+    order as the one-launch step's), so a run sharded over ranks — whose path can
+    differ from the unsharded run's by env count — gives the same bits."""
     from pmenv import TradingEnv, synth
     B, N, W, T = 37, 30, 50, 56
     ser = synth.series(W + T, B, N, seed=zlib.crc32(f"{kw}{db}".encode()), device=DEV)
@@ -299,10 +300,9 @@ def test_gpu_one_and_two_launch_agree(db, kw):
             else:
                 r, _ = e.step(act[t], obs[i], bar=ser[W + t])
             rs.append(r)
-        assert torch.equal(obs[0][..., :4], obs[1][..., :4])
-        assert torch.allclose(obs[0], obs[1], rtol=2e-7, atol=1e-12)
-        assert torch.allclose(rs[0].double(), rs[1].double(), rtol=1e-6, atol=1e-9, equal_nan=True)
-        assert torch.allclose(envs[0].value, envs[1].value, rtol=1e-12)
+        assert torch.equal(obs[0], obs[1]), f"step {t}: windows"
+        assert torch.equal(rs[0].nan_to_num(7.0), rs[1].nan_to_num(7.0)), f"step {t}: rewards"
+        assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
 
 
 @pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])

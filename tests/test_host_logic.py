@@ -120,3 +120,34 @@ def test_off_policy_host_checks_cpu():
         loop.collect(torch.full((4,), 30, dtype=torch.int32), 10)
     a = loop._random_action()
     assert a.shape == (4, 3) and torch.all(a >= 0) and torch.allclose(a.sum(-1), torch.ones(4))
+
+
+def test_gae_refuses_host_rewards():
+    """A host tensor would hand the kernel a host pointer: refused before any launch."""
+    import torch
+    from pmenv import rollout
+    with pytest.raises(ValueError):
+        rollout.gae(torch.zeros(4, 3), torch.zeros(5, 3))
+    with pytest.raises(ValueError):
+        rollout.gae(torch.zeros(4, 3), torch.zeros(4, 3))          # values must be [T+1, B]
+    with pytest.raises(ValueError):
+        rollout.moments(torch.zeros(7))
+
+
+def test_replay_valid_starts_stay_inside_one_episode():
+    """The replay samples W+1 consecutive rows of one episode (buffer.py:17-21 keeps
+    every epoch in its own row): starts whose window crosses a reset are excluded, on
+    a wrapped ring too."""
+    from pmenv.replay import valid_starts
+    W, H = 3, 10
+    # rows 0..9 written in order; episodes 0 (rows 0-5) then 1 (rows 6-9), oldest = 0
+    ep = [0] * 6 + [1] * 4
+    assert valid_starts(ep, 0, 10, W, H) == [0, 1, 2]
+    # the same ring after 4 more adds of episode 2 (rows 0-3 overwritten, oldest = 4)
+    ep = [2] * 4 + [0, 0, 1, 1, 1, 1]
+    got = valid_starts(ep, 4, 10, W, H)                  # st counts from the oldest row (row 4)
+    for st in got:
+        rows = [(4 + st + i) % H for i in range(W + 1)]
+        assert len({ep[r] for r in rows}) == 1
+    assert got == [2]                                      # rows 6..9 are the only whole window
+    assert valid_starts([5] * H, 0, H, W, H) == list(range(H - W - 1))
