@@ -433,12 +433,17 @@ void launch_one_v(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const unsigned grid = (unsigned)h->cfg.num_envs;
 #ifdef PMENV_AB
     lds += (size_t)ab_int("PMENV_ONE_LDS_PAD", 0);    // occupancy study: fewer workgroups per CU
-    if (h->ablate == 128 || h->ablate == 130) {    // timing-only: no scalar step / unconditional side reads
-        if (h->ablate == 128 && out) step_env_kernel<V, true, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (h->ablate == 128) step_env_kernel<V, false, 1, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (out) step_env_kernel<V, true, 1, 2><<<grid, threads, lds, stream>>>(p, h->per4);
-        else step_env_kernel<V, false, 1, 2><<<grid, threads, lds, stream>>>(p, h->per4);
-        return;
+    if (h->ablate >= 128 && h->ablate < 144) {    // timing-only / A/B bits (step_env.h ABL), nt policy
+#define PMENV_ONEABL(X)                                                                                     \
+        case 128 + X:                                                                                     \
+            if (out) step_env_kernel<V, true, 1, X><<<grid, threads, lds, stream>>>(p, h->per4);            \
+            else step_env_kernel<V, false, 1, X><<<grid, threads, lds, stream>>>(p, h->per4);               \
+            return;
+        switch (h->ablate) {
+            PMENV_ONEABL(1) PMENV_ONEABL(2) PMENV_ONEABL(4) PMENV_ONEABL(8) PMENV_ONEABL(12)
+            default: break;
+        }
+#undef PMENV_ONEABL
     }
     if (h->one_nocap) {
         if (out && pol == 1) step_env_nocap_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);

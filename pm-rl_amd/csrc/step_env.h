@@ -35,7 +35,8 @@ namespace pmenv_dev {
 
 // POL: cache policy of the window stream (0 default, 1 nt); OUT: double-buffered;
 // ABL (timing-only ablation, tools build): 1 = no scalar step (constant w' / bar),
-// 2 = every chunk reads the bar / w' from LDS (the unconditional form)
+// 2 = every chunk reads the bar / w' from LDS (the unconditional form), 4 = XCD-contiguous
+// env ranges, 8 = default-policy loads (nt stores)
 template <int V, bool OUT, int POL, int ABL>
 __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4) {
     constexpr int kAux = POL == 1 ? 2 : 0;
@@ -45,7 +46,11 @@ __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4
     __shared__ float sh_wp[64];
     __shared__ int32_t sh_k;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b = blockIdx.x;
+    int b = blockIdx.x;
+    if (ABL & 4) {   // A/B: XCD-contiguous env ranges (workgroups go round-robin over the 8 XCDs)
+        const int G = gridDim.x, q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
+        b = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+    }
     const int WF = p.W * F;
     // The env's chunks [e0, e0 + per4) of the flat [B, N, W, F] tensor, covered by the
     // 1 KiB-aligned 64-chunk blocks from g0 = e0 / 64 on: slot s of the workgroup is
@@ -66,7 +71,7 @@ __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4
     f4 own[V];
 #pragma unroll
     for (int v = 0; v < V; ++v)
-        own[v] = buf_load4<kAux>(rs, ((uint32_t)(64 * V * wave + 64 * v + lane) - a) * 16u);
+        own[v] = buf_load4<(ABL & 8) ? 0 : kAux>(rs, ((uint32_t)(64 * V * wave + 64 * v + lane) - a) * 16u);
     __builtin_amdgcn_sched_barrier(0);
     // 3. the scalar step, on wave 0, while the window is in flight
     if ((ABL & 1) && wave == 0) {
