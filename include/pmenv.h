@@ -294,6 +294,17 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
                         int32_t H, int32_t B, const int32_t* h0, const int32_t* env, int32_t S,
                         float* s, float* s_next, float* a_out, float* r_out, hipStream_t stream);
 
+/* The compact on-policy rollout (replay/rollout_buffer.py:43-57 stores s per step;
+ * here the windows are re-materialised instead): for each of the S
+ * samples (t_idx[j], env[j]) writes s[j] = env b's window after t updates, [N, W, F]:
+ * market channels from series [T, N, F-1] at days start[b] + t .. start[b] + t + W - 1
+ * (start [B] = first day of the reset window; days outside read NaN), channel F-1 =
+ * ActionBuffer.get_all() rebuilt from the post-drift weights [T_rec, B, N] of updates
+ * 1 .. T_rec (weight_buffer.py:32-44; ring_mode = pmenv_ring_mode). t_idx <= T_rec. */
+int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W, const int32_t* start,
+                         const float* weights, int32_t T_rec, int32_t B, int32_t ring_mode,
+                         const int32_t* t_idx, const int32_t* env, int32_t S, float* s, hipStream_t stream);
+
 /* util/eval.py:14-37 per env over a trajectory: returns [T, B] (simple returns),
  * values [T+1, B] f64, weights [T+1, B, N]; out [B, 5] f64 =
  * {sharpe, sortino, max drawdown, average turnover, final value} from f64 simple

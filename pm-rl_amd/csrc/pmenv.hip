@@ -1208,6 +1208,18 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
+int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W, const int32_t* start,
+                         const float* weights, int32_t T_rec, int32_t B, int32_t ring_mode, const int32_t* t_idx,
+                         const int32_t* env, int32_t S, float* s, hipStream_t stream) {
+    if (!series || !start || (!weights && T_rec > 0) || !t_idx || !env || !s || T < 1 || N < 1 || F < 2 || W < 1 ||
+        T_rec < 0 || B < 1 || S < 1 || ring_mode < 0 || ring_mode > 1)
+        return PMENV_ERR_ARG;
+    const int64_t threads = (int64_t)S * N * W * F;
+    rollout_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(series, T, N, F, W, start, weights,
+                                                                                T_rec, B, ring_mode, t_idx, env, S, s);
+    return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+}
+
 int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B, int32_t N,
                   double risk_free_rate, double periods, double* out, hipStream_t stream) {
     if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;

@@ -53,6 +53,46 @@ __global__ void replay_gather_kernel(const float* series, int T, int N, int F, i
     s_next[i] = vn;
 }
 
+// The compact on-policy rollout (the device rollout keeps actions,
+// rewards and values, not windows): env b's window after t steps is re-materialised
+// from the resident market series and the env's post-drift weight history —
+//   market f < F-1:  series[start[b] + t + p, n, f]          (p = day in the window)
+//   weight f = F-1:  ActionBuffer.get_all() after t updates (weight_buffer.py:32-44)
+// with the history rows r = 0 .. T_rec+W-1 of env b: rows < W-1 zero, row W-1 = e0 (the
+// reset ring, weight_buffer.py:46-51), row W-1+j = w' of update j (weights [T_rec, B, N]).
+// Chronological position c of the window after u = t updates reads row t + c; once the
+// ring is full (u >= W-1) the reference returns it in storage order (:38-39): position
+// p holds update j with j % W == p, i.e. chronological c = (p - u - 1) mod W.
+// One thread per output float ([S, N, W, F], coalesced stores). Days outside the series
+// read NaN.
+__global__ void rollout_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* start,
+                                      const float* weights, int T_rec, int B, int ring_mode, const int32_t* t_idx,
+                                      const int32_t* env, int S, float* s) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = (int64_t)N * W * F;
+    if (i >= (int64_t)S * per) return;
+    const int Fm = F - 1;
+    const int j = (int)(i / per);
+    int rem = (int)(i - (int64_t)j * per);
+    const int n = rem / (W * F);
+    rem -= n * W * F;
+    const int p = rem / F, f = rem - p * F;
+    const int b = env[j], t = t_idx[j];
+    float v;
+    if (f < Fm) {
+        const int d = start[b] + t + p;
+        v = (d >= 0 && d < T) ? series[((size_t)d * N + n) * Fm + f] : NAN;
+    } else {
+        const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
+        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
+        const int r = t + c;                       // history row
+        if (r < W - 1) v = 0.0f;
+        else if (r == W - 1) v = n == 0 ? 1.0f : 0.0f;
+        else v = weights[((size_t)(r - W) * B + b) * N + n];
+    }
+    s[i] = v;
+}
+
 #ifdef PMENV_AB   // tools build: the thread-per-env walk (the fused kernel replaced it)
 // one thread per env walks its column of the trajectory (coalesced across envs)
 //   out[b] = {sharpe, sortino, max drawdown, average turnover, final value}

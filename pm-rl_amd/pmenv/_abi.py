@@ -86,6 +86,8 @@ SIGNATURES = [
     ("pmenv_moments", ctypes.c_int, [_P, _I64, _P, _P, _P]),
     ("pmenv_replay_gather", ctypes.c_int,
      [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P]),
+    ("pmenv_rollout_gather", ctypes.c_int,
+     [_P, _I32, _I32, _I32, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
     ("pmenv_metrics", ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P]),
     ("pmenv_batch_reward_workspace", _SZ, [_I32]),
     ("pmenv_batch_reward_forward", ctypes.c_int,

@@ -50,10 +50,15 @@ class WindowCritic(torch.nn.Module):
 
 class OnPolicy:
     def __init__(self, env, policy, horizon, series=None, lr=1e-3, batch_size=256, generator=None):
+        """series: a pmenv.MarketSeries — every env trades it from its own start day, in
+        place, and the rollout buffer keeps actions, w', values and rewards only (compact,
+        windows re-materialised at sample time); None: bars fed per step, the env advancing
+        straight into the buffer's window slab."""
         cfg = env.cfg
         self.env, self.policy = env, policy
         self.buf = DeviceRolloutBuffer(cfg.num_envs, cfg.num_assets, cfg.window, horizon, cfg.features,
-                                       device=env.device, init_cash=cfg.init_cash, close_channel=cfg.close_channel)
+                                       device=env.device, init_cash=cfg.init_cash, close_channel=cfg.close_channel,
+                                       series=series, ring=cfg.ring)
         self.optim = torch.optim.Adam(policy.parameters(), lr=lr)
         self.batch_size = batch_size
         self.generator = generator
@@ -64,13 +69,30 @@ class OnPolicy:
         with torch.no_grad():
             return torch.softmax(self.policy(s).squeeze(-1), dim=-1)
 
-    def rollout(self, obs0, bars):
-        """train/on_policy.py:59-67 for every env at once. obs0 [B, N, W, F] is the
-        reset window; bars[t] the day's [B, N, F-1] bars (t = 0 .. horizon-1)."""
+    def rollout(self, obs0=None, bars=None, start=None):
+        """train/on_policy.py:59-67 for every env at once. Slab form: obs0 [B, N, W, F] is
+        the reset window and bars[t] the day's [B, N, F-1] bars (t = 0 .. horizon-1).
+        Compact form (series given at construction): start [B] is every env's first day
+        on the series; the window lives in the env (stepped in place) and only the
+        action, w', value and reward of each step are recorded."""
         buf, env = self.buf, self.env
+        rewards = []
+        if buf.compact:
+            series = buf.series
+            start = torch.as_tensor(start, device=env.device).to(torch.int32).reshape(buf.B)
+            buf.reset(start=start)
+            obs = series.initial_window(start, buf.W)
+            env.reset(obs)
+            w = torch.empty(buf.B, buf.N, device=env.device)
+            for t in range(1, buf.T + 1):
+                a = self.act(obs)
+                r, _ = env.step(a, obs, series=series, day=start + buf.W + t - 1, weights_out=w)
+                buf.add(a, env.value, r, weights=w)
+                rewards.append(r)
+            self.obs = obs
+            return torch.stack(rewards)
         buf.reset(obs0)
         env.reset(buf.obs(0))
-        rewards = []
         for t in range(1, buf.T + 1):
             a = self.act(buf.obs(t - 1))
             r, _ = env.step(a, buf.obs(t - 1), bar=bars[t - 1], out=buf.obs(t))
@@ -115,7 +137,7 @@ class OnPolicy:
         for i in range(0, n - bs + 1, bs):
             idx = perm[i:i + bs]
             t, env = idx // B, idx % B
-            pred = critic(self.buf.s[t, env]).reshape(-1)
+            pred = critic(self.buf.windows(t, env)).reshape(-1)
             loss = torch.nn.functional.mse_loss(pred, returns[t, env])
             optim.zero_grad(set_to_none=True)
             loss.backward()

@@ -211,7 +211,7 @@ class TradingEnv:
             self._reset_info()
         return features
 
-    def step(self, action, features, prices=None, bar=None, out=None, series=None, day=None):
+    def step(self, action, features, prices=None, bar=None, out=None, series=None, day=None, weights_out=None):
         """trading_env.py:44-105 for all B envs in one kernel launch.
 
         prices given, bar None : the reference contract — `features` is the next
@@ -227,6 +227,8 @@ class TradingEnv:
                                  in place (double-buffered windows, as the
                                  reference's data path hands the env a fresh
                                  window every day); returns (r, out).
+        weights_out            : a float32 [B, N] GPU tensor that receives the
+                                 post-drift weights w' (info["actions"], :83-85)
         Returns (r, features); r is f32 [B] (0-dim for unbatched single-env input).
         """
         cfg = self.cfg
@@ -239,7 +241,7 @@ class TradingEnv:
             r, res = self.step(action, features.to(self.device), prices=prices, bar=bar,
                                out=None if out is None else torch.empty(out.shape, dtype=out.dtype,
                                                                         device=self.device),
-                               series=series, day=day)
+                               series=series, day=day, weights_out=weights_out)
             (features if out is None else out).copy_(res)
             self._host_io = True
             return r.cpu(), (features if out is None else out)
@@ -281,16 +283,22 @@ class TradingEnv:
             args.obs_out = out.data_ptr()
         args.reward = r.data_ptr()
         ret = w = None
+        if weights_out is not None:
+            if weights_out.dtype != torch.float32 or not weights_out.is_contiguous() or \
+                    weights_out.device != self.device or weights_out.numel() != B * N:
+                raise ValueError(f"weights_out must be a contiguous float32 [{B}, {N}] tensor on {self.device}")
+            args.weights = weights_out.data_ptr()
         if self.track_info:
             ret = torch.empty(B, dtype=torch.float64, device=self.device)
-            w = torch.empty(B, N, dtype=torch.float32, device=self.device)
             args.ret = ret.data_ptr()
-            args.weights = w.data_ptr()
+            if weights_out is None:
+                w = torch.empty(B, N, dtype=torch.float32, device=self.device)
+                args.weights = w.data_ptr()
         _abi.check(self._lib.pmenv_step_ex(self._h, ctypes.byref(args), self._stream()), self._h, "pmenv_step")
         if self.track_info:
             # trading_env.py:80,85,90,100
             self.info["values"].append(self._value.clone())
-            self.info["actions"].append(w)
+            self.info["actions"].append(w if weights_out is None else weights_out.reshape(B, N).clone())
             self.info["returns"].append(ret)
             self.info["rewards"].append(r)
         self._unbatched = unb

@@ -58,3 +58,72 @@ def test_gpu_on_policy_rollout_and_update(B, N, W, T):
     adv, ret = buf.returns(values, 0.99, 0.95)
     adv2, _ = gae(buf.r[1:].contiguous(), values, None, 0.99, 0.95)
     assert torch.equal(adv, adv2) and torch.allclose(ret, adv + values[:T], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("ring", ["storage", "chrono"])
+@pytest.mark.parametrize("B,N,W,T", [(33, 7, 6, 20), (5, 30, 50, 60), (64, 1, 2, 9)])
+def test_gpu_compact_rollout_rematerialises_the_env_windows(ring, B, N, W, T):
+    """The compact rollout (resident series, O(T*B*N) storage) re-materialises, for
+    every step t and env, exactly the window the env held after t steps — market
+    channels from the series, the weight channel from the recorded w' in the ring's
+    order (storage order past the wrap, T > W) — and the price relatives of the step."""
+    from pmenv import MarketSeries, TradingEnv
+    from pmenv.rollout_buffer import DeviceRolloutBuffer
+    rng = np.random.default_rng(B + N + W)
+    Ts = W + T + 40
+    bars = (100 * np.exp(0.01 * rng.standard_normal((Ts, N, 4)).cumsum(0))).astype(np.float32)
+    m = MarketSeries(bars, device=DEV)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, ring=ring)
+    buf = DeviceRolloutBuffer(B, N, W, T, device=DEV, series=m, ring=ring)
+    start = m.random_starts(B, W, T, generator=torch.Generator().manual_seed(1))
+    buf.reset(start=start)
+    obs = m.initial_window(start, W)
+    env.reset(obs)
+    assert torch.equal(buf.obs(0), obs)
+    w = torch.empty(B, N, device=DEV)
+    for t in range(1, T + 1):
+        a = torch.softmax(torch.randn(B, N, device=DEV), -1)
+        r, _ = env.step(a, obs, series=m, day=start + W + t - 1, weights_out=w)
+        buf.add(a, env.value, r, weights=w)
+        assert torch.equal(buf.obs(t), obs), f"window after {t} steps"
+        assert torch.equal(buf.price_relatives(t), m.bars[start.long() + W + t - 1, :, 3] /
+                           m.bars[start.long() + W + t - 2, :, 3])
+    s, a_, r_, v_prev, a_prev, p = buf.gather(torch.tensor([T, 1, T // 2], device=DEV), torch.tensor([0, B - 1, B // 2],
+                                                                                                    device=DEV))
+    assert s.shape == (3, N, W, 5) and p.shape == (3, N, 1) and v_prev.shape == (3, 1, 1)
+    assert buf.nbytes() < 4 * (T + 1) * B * N * 4 + 64 * B      # O(T * B * N): no windows kept
+
+
+def test_gpu_on_policy_compact_loop():
+    """OnPolicy over a resident series with the compact buffer: the rewards equal an
+    independent env fed the gathered bar batch bit for bit, an update pass and the
+    critic's GAE / normalised advantages run on re-materialised windows."""
+    from pmenv import MarketSeries, TradingEnv
+    from pmenv.on_policy import OnPolicy, WindowCritic, WindowPolicy
+    B, N, W, T, Ts = 256, 30, 50, 24, 400
+    rng = np.random.default_rng(7)
+    bars = (100 * np.exp(0.01 * rng.standard_normal((Ts, N, 4)).cumsum(0))).astype(np.float32)
+    m = MarketSeries(bars, device=DEV)
+    torch.manual_seed(1)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    policy = WindowPolicy(W).to(DEV)
+    loop = OnPolicy(env, policy, horizon=T, series=m, batch_size=B, generator=torch.Generator().manual_seed(2))
+    start = m.random_starts(B, W, T, generator=torch.Generator().manual_seed(3))
+    rewards = loop.rollout(start=start)
+    buf = loop.buf
+    assert buf.compact and rewards.shape == (T, B)
+    ref = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
+    robs = m.initial_window(start, W)
+    ref.reset(robs)
+    for t in range(1, T + 1):
+        r, _ = ref.step(buf.a[t].contiguous(), robs, bar=m.bars[start.long() + W + t - 1].contiguous())
+        assert torch.equal(r, rewards[t - 1]) and torch.equal(ref.value, buf.v[t])
+    assert torch.equal(robs, loop.obs) and torch.equal(buf.obs(T), robs)
+    w0 = [q.detach().clone() for q in policy.parameters()]
+    losses = loop.update()
+    assert losses.numel() == T and bool(torch.isfinite(losses).all())
+    assert any(not torch.equal(a, b) for a, b in zip(w0, policy.parameters()))
+    critic = WindowCritic(W).to(DEV)
+    adv, ret, values = loop.advantages(critic)
+    assert adv.shape == (T, B) and bool(torch.isfinite(adv).all())
+    assert abs(float(adv.mean())) < 1e-4 and abs(float(adv.std(unbiased=False)) - 1.0) < 1e-3
