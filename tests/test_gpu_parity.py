@@ -26,11 +26,15 @@ def _t(x, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
 
 
-def replay_gpu(g, mode):
+def replay_gpu(g, mode, host=False):
+    """host=True: the reference's own call shape with CPU tensors (train/on_policy.py:59-67
+    hands the env host tensors); the env stages them through the GPU."""
     from pmenv import TradingEnv
     m = g["meta"]
     N, W, F, T = m["N"], m["W"], m["F"], m["T"]
     env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True)
+    _t = (lambda x, dtype=torch.float32: torch.as_tensor(np.ascontiguousarray(x), dtype=dtype)) if host else \
+        globals()["_t"]
     out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
            "wpost": np.full((T + 1, N), np.nan), "chans": {}, "market_ok": True}
     obs = None
@@ -45,7 +49,7 @@ def replay_gpu(g, mode):
             else:
                 r, obs2 = env.step(_t(g["actions"][i]).reshape(N, 1), obs, bar=_t(gu.bar(g, i)))
                 out["market_ok"] &= np.array_equal(obs[..., :-1].cpu().numpy(), gu.window(g, i)[0, ..., :-1])
-            assert obs2 is obs and r.dim() == 0
+            assert obs2 is obs and r.dim() == 0 and r.device == obs.device
             out["rewards"][i] = float(r)
             out["rets"][i] = float(env.info["returns"][-1][0])
             out["wpost"][i] = env.info["actions"][-1][0].cpu().numpy()
@@ -60,6 +64,18 @@ def test_gpu_matches_reference_goldens(name, mode):
     g = gu.load(name)
     out = replay_gpu(g, mode)
     assert out["market_ok"]
+    compare(g, out)
+
+
+@pytest.mark.parametrize("name", ["simplex_n30_w50_t256_f64", "mixed_n30_w50_t64_f32", "wrap_n5_w8_t40_f64", "reset_n5_w8_t40_f64"])
+def test_gpu_reference_goldens_with_host_tensors(name):
+    """The reference's callers drive the env with CPU tensors, unchanged: features,
+    actions and prices on the host in, reward and value back on the host, the
+    features mutated in place and returned (trading_env.py:102-105)."""
+    if name not in gu.cases():
+        pytest.skip("golden case absent")
+    g = gu.load(name)
+    out = replay_gpu(g, "surface", host=True)
     compare(g, out)
 
 
