@@ -687,12 +687,13 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
 
     // ---- the one-launch step (step_env_kernel, one workgroup per env): F = 5, W >= 2,
     // N <= 64 (the scalar step on one wave), 16-B granular env windows whose 1 KiB
-    // blocks fit 16 waves and 64 KiB of LDS. Measured against the two-launch path
-    // (tools/gpu_ab_one6.sh, profiles/ab_r02/): it wins below 4,096 envs (64: 6.5 vs
-    // 8.4 us; 1,024: 13.1 vs 18.2; 2,048: 24.7 vs 26.9) and from 16,384 up (162.6 vs
-    // 170.0 us; 65,536: 650-658 vs 657-664), and loses to the two-launch stream where
-    // an in-place window of 3,072+ envs sits in the Infinity Cache (4,096: 46.5 vs
-    // 44.2 us; 8,192: 85.7 vs 84.6), which therefore keeps the two launches.
+    // blocks fit 16 waves and 64 KiB of LDS. AUTO gives it the windows of at most
+    // 48 MiB, where launch latency dominates and it wins by 7-38 % (tools/gpu_ab_smallb.sh,
+    // profiles/ab_r02/r02u_*: N = 8..64, 256..4,096 envs; N = 30: 64 envs 6.5 vs 9.6 us,
+    // 1,024: 13.1 vs 18.2). Larger windows take the two-launch stream: its fixed 16 KiB
+    // workgroups run 640-670 us on a 2 GB window at every asset count measured, while the
+    // one-workgroup-per-env geometry ties it only at N = 30 (650-658 us) and loses 4-15 %
+    // at N = 8, 16, 24, 32, 40, 48, 60, 64 (profiles/ab_r02/r02r_*, r02s_*, r02t_*).
     h->per4 = (uint32_t)(per / 4);
     // 4 chunks per lane (tools: PMENV_ONE_V = 1 | 2 | 3 | 6 | 8; 4 measured best: 650 us
     // against 662-666 for 8, 762 for 3, 860 for 2 at the BASELINE shape)
@@ -705,11 +706,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     }
     h->one_ok = h->streaming && c.features == 5 && c.window >= 2 && c.num_assets <= 64 && per % 4 == 0 &&
                 h->one_waves <= 16 && ((int64_t)64 * h->one_v * h->one_waves + 2) * 16 <= 65536;
-    h->one_auto = 0;
-    if (h->one_ok) {
-        h->one_auto = PMENV_FUSE_DB;
-        if (!(h->flat_inplace && c.num_envs >= 3072 && win <= (256ll << 20))) h->one_auto |= PMENV_FUSE_INPLACE;
-    }
+    // (also beyond the flat stream's 2^31-chunk index, where the two-launch path would fall
+    // back to the whole-row stream)
+    h->one_auto = h->one_ok && (win <= (48ll << 20) || !h->flat_inplace) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
 #ifdef PMENV_AB
     if (const char* knob = ab_knob("PMENV_ONE")) {    // 0 | db | ip | all
         if (!h->one_ok || !strcmp(knob, "0")) h->one_auto = 0;

@@ -233,17 +233,19 @@ def test_gpu_flat_inplace_shapes(N, W, B):
     _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 3 * W, impl=impl)
 
 
-def test_gpu_auto_path_takes_two_launches_for_cache_resident_in_place_windows():
-    """3,072+ envs whose in-place window fits the Infinity Cache keep the two-launch
-    stream (measured faster there); the same shape double-buffered, and smaller env
-    counts, take the one-launch step. Checked against the oracle at such a shape
-    (3,100 envs x 5 assets x 4 days: 25 chunks per env, the flat stream's seams inside envs)."""
+def test_gpu_auto_path_rule():
+    """AUTO takes the one-launch step for windows up to 48 MiB (launch-latency bound:
+    it wins there at every asset count measured) and the two-launch stream above (its
+    fixed geometry is the faster one on large windows at most asset counts); checked
+    against the oracle just above the threshold (1,700 envs x 30 x 50: 51 MB)."""
     from pmenv import TradingEnv
-    e = TradingEnv(num_envs=3100, num_assets=5, window=4, device=DEV)
-    db, ip = e.step_path.split(" | ")
-    assert db.startswith("step_env_kernel") and "advance_flat_inplace_kernel" in ip
-    assert TradingEnv(num_envs=3000, num_assets=5, window=4, device=DEV).step_path.count("step_env_kernel") == 2
-    _run_both({}, B=3100, N=5, W=4, T=13, kind="mixed", seed=31)
+    small = TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV)          # 45 MB
+    assert small.step_path.count("step_env_kernel") == 2
+    big = TradingEnv(num_envs=1700, num_assets=30, window=50, device=DEV)            # 51 MB
+    db, ip = big.step_path.split(" | ")
+    assert "advance_flat_wg_kernel" in db and "advance_flat_inplace_kernel" in ip
+    _run_both({}, B=1700, N=30, W=50, T=9, kind="mixed", seed=31)
+    _run_both({"ring": "chrono"}, B=1700, N=30, W=50, T=5, kind="simplex", seed=32, double_buffer=True)
 
 
 @pytest.mark.parametrize("impl", ["one_launch", "two_launch"])
@@ -419,10 +421,11 @@ def test_gpu_state_roundtrip():
     assert torch.equal(obs, obs_ck) and torch.equal(e1.value, e2.value)
 
 
-@pytest.mark.parametrize("impl", ["auto", "two_launch"])
+@pytest.mark.parametrize("impl", ["one_launch", "two_launch"])
 def test_gpu_full_size_properties(impl):
     """BASELINE config (65,536 envs x 30 assets x 50 x 5) through past the ring wrap,
-    by the default one-launch step and by the two-launch path (the nt flat streams):
+    by the one-launch step and by the two-launch path (the default here; the nt flat
+    streams):
     market channels are exactly the sliding window of the series, the reward is
     log(sum w*y) with y the fp32 close relative, the value compounds the returns,
     and the weight channel is the ring in the reference's storage order."""
@@ -432,7 +435,7 @@ def test_gpu_full_size_properties(impl):
     act = synth.actions(T, B, N, seed=12, device=DEV)
     obs = synth.window_from_series(ser, W, F)
     env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
-    assert env.step_path.count("step_env_kernel") == (2 if impl == "auto" else 0)
+    assert env.step_path.count("step_env_kernel") == (2 if impl == "one_launch" else 0)
     env.reset(obs)
     logv = torch.full((B,), float(np.log(25000.0)), dtype=torch.float64, device=DEV)
     spare = torch.empty_like(obs)
@@ -752,7 +755,7 @@ def test_gpu_beyond_flat_index_range_in_place():
     from pmenv import TradingEnv
     B, N, W = 1_200_000, 30, 50
     env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV)
-    assert env.step_path.split(" | ")[1].startswith("step_env_kernel")
+    assert env.step_path.split(" | ")[1].startswith("step_env_kernel")     # AUTO: no flat stream here
     g = torch.Generator(device=DEV).manual_seed(3)
     obs = torch.rand(B, N, W, 5, device=DEV, generator=g) + 0.5
     env.reset(obs)
