@@ -185,14 +185,23 @@ const char* pmenv_step_path(const pmenv* h);
 /* Advance-mode step implementation. AUTO (the default) picks per shape and window
  * mode; ONE_LAUNCH forces step_env_kernel (one workgroup per env: F = 5, W >= 2,
  * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
- * kernel followed by the window stream (F = 5, 16-B granular env windows). Returns
- * PMENV_ERR_ARG (handle unchanged) when the shape does not fit the requested path.
- * Results are the same either way up to the last bits of the f64 sums (the two
- * scalar-step forms reduce in different orders). */
+ * kernel followed by the window stream (F = 5, 16-B granular env windows); FLAT forces
+ * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:
+ * F = 5, W >= 2, N <= 64, env windows of >= 148 16-B chunks). Returns PMENV_ERR_ARG
+ * (handle unchanged) when the shape does not fit the requested path. For N <= 64 every
+ * path gives the same bits; the N > 64 scalar-step forms reduce in another order.
+ *
+ * FLAT keeps a per-step snapshot of the state its scalar step reads and, in place, the
+ * halo of its tiles, both produced by the previous step: a caller that writes the state
+ * blob (pmenv_create_in) or an in-place window outside this API must go through
+ * pmenv_set_state / pmenv_reset before the next step (both re-prime them; so does every
+ * other step path). A step enqueued while `stream` is being captured into a hipGraph
+ * takes the two-launch path instead (the parity is a launch argument). */
 typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,
-    PMENV_STEP_PATH_TWO_LAUNCH = 2
+    PMENV_STEP_PATH_TWO_LAUNCH = 2,
+    PMENV_STEP_PATH_FLAT = 3
 } pmenv_step_path_kind;
 int pmenv_set_step_path(pmenv* h, int32_t path);
 

@@ -65,6 +65,21 @@ struct StepParams {
     // first two chunks here (advance_flat_inplace_kernel's halo); null: no copy
     float* halo;
     uint32_t halo_wgs, halo_block, halo_qtot;
+    // one-launch flat step (step_flat.h): the state snapshot the scalar step reads
+    // (parity p: value, counter, get_last(), last close) and the one the env's owner
+    // writes for the next step (parity 1 - p); in place, the halo of this step and the
+    // one this step leaves for the next
+    const double* sv_in;
+    const int32_t* sk_in;
+    const float* sw_in;
+    const float* slc_in;
+    double* sv_out;
+    int32_t* sk_out;
+    float* sw_out;
+    float* slc_out;
+    const float* halo_in;
+    float* halo_out;
+    uint32_t per4;         // 16-B chunks per env window
     FastDiv div_wf, div_f, div_w, div_units;
 };
 

@@ -334,9 +334,11 @@ __device__ __forceinline__ ScalarIn scalar_load_row(const StepParams& p, int b, 
     return in;
 }
 
-template <int L, bool ROW = false>
+// SNAP (step_flat_kernel): only the env's owner workgroup (`owner`) writes the state,
+// reward and ring slot, and it also writes the next step's snapshot (sv_out .. slc_out)
+template <int L, bool ROW = false, bool SNAP = false>
 __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int lane, const ScalarIn& in,
-                                               int32_t& k_before) {
+                                               int32_t& k_before, bool owner = true) {
     const int n = lane % L;
     const int N = p.N, W = p.W;
     const bool env_ok = b < p.B;
@@ -409,14 +411,19 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
     const double pv = act ? V * (w * y) : 0.0;
     const double value = group_sum<L>(pv, lane);
     const int slot = (int)((1 + (int64_t)k) % W);
-    if (act) {
+    const bool wr = !SNAP || owner;
+    if (act && wr) {
         const float wp = (float)(pv / value);     // the value returned below
         p.ring[(size_t)b * W * N + (size_t)slot * N + n] = wp;
         p.w_new[i] = wp;
         if (p.weights) p.weights[i] = wp;
         if (p.bar) p.last_close[i] = cn;
+        if (SNAP) {
+            p.sw_out[i] = wp;
+            p.slc_out[i] = cn;
+        }
     }
-    if (env_ok && n == 0) {
+    if (env_ok && n == 0 && wr) {
         // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
         const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
         double r;
@@ -448,6 +455,10 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
         }
         p.value[b] = value;
         p.k[b] = k + 1;
+        if (SNAP) {
+            p.sv_out[b] = value;
+            p.sk_out[b] = k + 1;
+        }
         if (p.reward) p.reward[b] = (float)r;
         if (p.ret) p.ret[b] = ret;
         if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);

@@ -25,6 +25,7 @@
 #include "env_step.h"
 #include "scalar_vec.h"
 #include "step_env.h"
+#include "step_flat.h"
 #include "rollout.h"
 #include "gae_vec.h"
 #include "replay.h"
@@ -83,6 +84,21 @@ struct pmenv {
     int one;              // PMENV_FUSE_* bits: which windows take step_env_kernel now
     int one_v, one_waves; // step_env_kernel: chunks per lane, waves per workgroup
     uint32_t per4;        // 16-B chunks per env window
+    // one launch over the flat stream (step_flat_kernel)
+    bool flat1_ok;        // the shape fits step_flat_kernel
+    int flat1_auto;       // PMENV_FUSE_* bits the automatic choice gives step_flat_kernel
+    int flat1;            // PMENV_FUSE_* bits: which windows take step_flat_kernel now
+    void* snap;           // the state snapshot, two parities: value f64 | counter i32 | get_last() | last close
+    double* sv[2];
+    int32_t* sk[2];
+    float* sw[2];
+    float* slc[2];
+    float* halo1[2];      // [halo1_wgs][2] float4 per parity: the next tile's first two chunks
+    uint32_t halo1_wgs;
+    int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread (tools: PMENV_FLAT1_GEOM)
+    int par;              // parity of the snapshot / halo the next step reads
+    bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
+    const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
     int path;             // pmenv_step_path_kind
     // tools build only
     int fused;            // PMENV_FUSE_* bits: advance_rows_kernel<fused> (PMENV_FUSED)
@@ -494,11 +510,87 @@ void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
 }
 #endif
 
-// which windows take the one-launch step under `path`
+// the whole step in one launch over the flat stream (step_flat.h): prime the snapshot
+// and the halo when something other than this kernel touched them, then one launch
+void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
+    const bool out = p.obs_out != p.obs;
+    const int q = h->par;
+    p.per4 = h->per4;
+    p.div_units = make_fastdiv(h->per4);
+    const bool need_halo = !out && h->halo1_obs != p.obs;
+    if (!h->snap_ok || need_halo) {
+        StepParams pp = p;
+        pp.sv_out = h->sv[q]; pp.sk_out = h->sk[q]; pp.sw_out = h->sw[q]; pp.slc_out = h->slc[q];
+        pp.halo = need_halo ? h->halo1[q] : nullptr;
+        pp.halo_wgs = h->halo1_wgs;
+        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
+        pp.halo_qtot = h->flat_qtot;
+        const int64_t work = (int64_t)h->cfg.num_envs * h->cfg.num_assets;
+        const unsigned g = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
+        flat_prime_kernel<<<g, 256, 0, stream>>>(pp);
+    }
+    p.sv_in = h->sv[q]; p.sk_in = h->sk[q]; p.sw_in = h->sw[q]; p.slc_in = h->slc[q];
+    p.sv_out = h->sv[1 - q]; p.sk_out = h->sk[1 - q]; p.sw_out = h->sw[1 - q]; p.slc_out = h->slc[1 - q];
+    p.halo_in = h->halo1[q];
+    p.halo_out = h->halo1[1 - q];
+    const int pol = out ? h->flat_pol : h->flat_ip_pol;
+    const unsigned grid = (h->flat_qtot + (uint32_t)(h->flat1_block * h->flat1_vec) - 1) /
+                          (uint32_t)(h->flat1_block * h->flat1_vec);
+#define PMENV_FLAT1_LAUNCH(BK, VV)                                                                           \
+    if (out) {                                                                                              \
+        if (pol == 1) step_flat_kernel<BK, VV, 1, true><<<grid, BK, 0, stream>>>(p, h->flat_qtot);          \
+        else step_flat_kernel<BK, VV, 0, true><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                   \
+    } else {                                                                                                \
+        if (pol == 1) step_flat_kernel<BK, VV, 1, false><<<grid, BK, 0, stream>>>(p, h->flat_qtot);         \
+        else step_flat_kernel<BK, VV, 0, false><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                  \
+    }
+    const int key = h->flat1_block * 100 + h->flat1_vec;
+#ifdef PMENV_AB
+    if (key == 51204) { PMENV_FLAT1_LAUNCH(512, 4) }
+    else if (key == 102402) { PMENV_FLAT1_LAUNCH(1024, 2) }
+    else if (key == 25608) { PMENV_FLAT1_LAUNCH(256, 8) }
+    else if (key == 25602) { PMENV_FLAT1_LAUNCH(256, 2) }
+    else if (key == 12808) { PMENV_FLAT1_LAUNCH(128, 8) }
+    else if (key == 12804) { PMENV_FLAT1_LAUNCH(128, 4) }
+    else
+#endif
+    if (key == 25604) { PMENV_FLAT1_LAUNCH(256, 4) }
+    else { PMENV_FLAT1_LAUNCH(512, 2) }
+#undef PMENV_FLAT1_LAUNCH
+    h->par = 1 - q;
+    h->snap_ok = true;
+    h->halo1_obs = out ? nullptr : p.obs;
+}
+
+// anything but step_flat_kernel that writes the state or a window leaves the snapshot
+// and the halo stale
+inline void flat1_invalidate(pmenv* h) {
+    h->snap_ok = false;
+    h->halo1_obs = nullptr;
+}
+
+// the stream is being captured into a hipGraph: step_flat_kernel's parity is a launch
+// argument (frozen under replay), so a captured step takes another path
+bool capturing(hipStream_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
+// which windows take the one-launch steps under `path`
 int one_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_ONE_LAUNCH) return h->one_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
     if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming ? 0 : -1;
+    if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? 0 : -1;
     return h->one_auto;
+}
+int flat1_bits(const pmenv* h, int path) {
+    if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
+    if (path == PMENV_STEP_PATH_AUTO) return h->flat1_auto;
+    return 0;
 }
 
 }  // namespace
@@ -576,6 +668,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         snprintf(g_create_err, sizeof(g_create_err), "%s", h->err);
         if (h->state && h->owns_state) (void)hipFree(h->state);
         if (h->halo) (void)hipFree(h->halo);
+        if (h->snap) (void)hipFree(h->snap);
         free(h);
         return code;
     };
@@ -728,8 +821,54 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
     }
 #endif
+    // ---- the one-launch flat step (step_flat_kernel): the flat stream's shape rules, the
+    // scalar step on one wave per env (N <= 64), at most one env per wave in a tile.
+    // Geometry: 256 threads x 4 chunks (16 KiB tiles, 4 waves) where env windows have
+    // >= 511 chunks, 512 x 2 (8 waves) from 148 chunks. 256 x 4 against 512 x 2 / 512 x 4 /
+    // 1024 x 2 / 256 x 8 / 256 x 2 / 128 x 8 / 128 x 4 at 65,536 x 30 in place: 629.5 against
+    // 714 / 678 / 790 / 695 / 675 / 624 / 641 us; 128 x 8 loses 15 % at N = 16 and 64 where
+    // 256 x 4 wins (profiles/ab_r02/r02w_flat1b_*, r02w_flat1c_*). A persistent form that
+    // keeps the next tile's loads in flight needs 160 VGPRs (3 waves per SIMD): 2x slower.
+    auto flat1_fits = [&](int block, int vec) {
+        const uint32_t cpw = (uint32_t)(block * vec);
+        const uint32_t ne_max = h->per4 ? (cpw + h->per4 - 2u) / h->per4 + 1u : 0u;
+        return flat_ok && c.num_assets <= 64 && ne_max <= (uint32_t)(block / 64);
+    };
+    h->flat1_block = flat1_fits(256, 4) ? 256 : 512;
+    h->flat1_vec = h->flat1_block == 256 ? 4 : 2;
+    h->flat1_ok = flat1_fits(h->flat1_block, h->flat1_vec);
+    // AUTO: above the one-launch-per-env windows (48 MiB) the flat step beats the two-launch
+    // stream by 1-3.5 % for env windows of >= 1,000 chunks (N >= 16 at W = 50): 65,536 x 30
+    // 629.5 / 639.7 against 642.4 / 648.8 us on two boxes, N = 24 / 40 / 48 / 64 by 1-3.4 %,
+    // N = 16 681 vs 689; it loses at N = 8 (500 chunks, 4 envs per tile: 713 vs 691) and in
+    // place on cache-resident windows (4,096 envs: 46.3 vs 44.2 us, 8,192: 85.2 vs 84.2);
+    // double-buffered it wins from 2,048 envs (25.4 vs 27.0) (profiles/ab_r02/r02w_flat1d_*).
+    h->flat1_auto = 0;
+    if (h->flat1_ok && h->flat1_block == 256 && h->per4 >= 1000u) {
+        if (win > (48ll << 20)) h->flat1_auto |= PMENV_FUSE_DB;
+        if (win > (256ll << 20)) h->flat1_auto |= PMENV_FUSE_INPLACE;
+        h->one_auto &= ~h->flat1_auto;
+    }
+#ifdef PMENV_AB
+    if (const char* knob = ab_knob("PMENV_FLAT1")) {   // tools: 1 = the flat step for every window, 0 = never
+        h->flat1_auto = h->flat1_ok && atoi(knob) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
+        if (h->flat1_auto) h->one_auto = 0;
+    }
+    if (const char* knob = ab_knob("PMENV_FLAT1_GEOM")) {   // "512x2" | "512x4" | "1024x2" | "256x8" | ...
+        int bk = 0, vv = 0;
+        if (sscanf(knob, "%dx%d", &bk, &vv) == 2) {
+            const int key = bk * 100 + vv;
+            if ((key == 51202 || key == 51204 || key == 102402 || key == 25604 || key == 25608 || key == 25602 ||
+                 key == 12808 || key == 12804) && flat1_fits(bk, vv)) {
+                h->flat1_block = bk;
+                h->flat1_vec = vv;
+            }
+        }
+    }
+#endif
     h->path = PMENV_STEP_PATH_AUTO;
     h->one = h->one_auto;
+    h->flat1 = h->flat1_auto;
 
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
@@ -775,6 +914,31 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             return fail(PMENV_ERR_HIP);
         }
     }
+    if (h->flat1_ok) {
+        // two parities of the snapshot (16-B aligned fields) and of the tile halo
+        const size_t B = (size_t)c.num_envs, BN = B * (size_t)c.num_assets;
+        auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
+        const size_t one = up16(B * 8) + up16(B * 4) + 2 * up16(BN * 4);
+        const uint32_t cpw = (uint32_t)(h->flat1_block * h->flat1_vec);
+        const uint32_t wgs = (h->flat_qtot + cpw - 1) / cpw;
+        h->halo1_wgs = wgs > 0 ? wgs - 1 : 0;
+        const size_t hal = up16(((size_t)h->halo1_wgs + 1) * 32);
+        hipError_t ae = hipMalloc(&h->snap, 2 * (one + hal));
+        if (ae != hipSuccess) {
+            set_err(h, "hipMalloc(snapshot) failed: %s", hipGetErrorString(ae));
+            h->snap = nullptr;
+            return fail(PMENV_ERR_HIP);
+        }
+        for (int q = 0; q < 2; ++q) {
+            char* sb = (char*)h->snap + (size_t)q * (one + hal);
+            h->sv[q] = (double*)sb;
+            h->sk[q] = (int32_t*)(sb + up16(B * 8));
+            h->sw[q] = (float*)(sb + up16(B * 8) + up16(B * 4));
+            h->slc[q] = (float*)(sb + up16(B * 8) + up16(B * 4) + up16(BN * 4));
+            h->halo1[q] = (float*)(sb + one);
+        }
+    }
+    flat1_invalidate(h);
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
     h->sa = (double*)(base + off[1]);
@@ -814,24 +978,28 @@ int pmenv_destroy(pmenv* h) {
     DeviceGuard g(h->device);
     if (h->state && h->owns_state) (void)hipFree(h->state);
     if (h->halo) (void)hipFree(h->halo);
+    if (h->snap) (void)hipFree(h->snap);
     free(h);
     return PMENV_OK;
 }
 
 int pmenv_set_step_path(pmenv* h, int32_t path) {
     if (!h) return PMENV_ERR_ARG;
-    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_TWO_LAUNCH) {
+    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_FLAT) {
         set_err(h, "unknown step path %d", path);
         return PMENV_ERR_ARG;
     }
     const int bits = one_bits(h, path);
-    if (bits < 0) {
+    const int fbits = flat1_bits(h, path);
+    if (bits < 0 || fbits < 0) {
         set_err(h, "step path %d does not fit this shape (one launch: F = 5, W >= 2, N <= 64, window <= 64 KiB "
-                   "of LDS; two launches: F = 5, 16-B granular env windows)", path);
+                   "of LDS; two launches: F = 5, 16-B granular env windows; flat: F = 5, W >= 2, N <= 64, "
+                   "16-B granular env windows of >= 148 chunks)", path);
         return PMENV_ERR_ARG;
     }
     h->path = path;
     h->one = bits;
+    h->flat1 = fbits;
     return PMENV_OK;
 }
 
@@ -840,6 +1008,7 @@ int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
     if (obs && !aligned4(obs)) { set_err(h, "obs not 4-byte aligned"); return PMENV_ERR_ALIGN; }
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
+    flat1_invalidate(h);
     reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, obs, mask);
     return check_launch(h, "reset_kernel");
 }
@@ -874,15 +1043,23 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     }
     p.reward = a->reward; p.ret = a->ret; p.weights = a->weights;
     const int B = h->cfg.num_envs;
+    const bool obs16 = (((uintptr_t)a->obs | (uintptr_t)p.obs_out) & 15u) == 0;
+    const int fuse_bit = p.obs_out == p.obs ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
+    if (a->bar && h->streaming && obs16 && (h->flat1 & fuse_bit) && !capturing(stream)) {
+        // one launch over the flat stream: the whole step runs in the scalar phase
+        const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
+        launch_flat1(h, p, stream);
+        return check_launch(h, "step_flat_kernel");
+    }
+    flat1_invalidate(h);             // every other path writes the state without the snapshot
     if (!a->bar) {
         if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
         step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
         return check_launch(h, "step_surface_kernel");
     }
-    const bool obs16 = (((uintptr_t)a->obs | (uintptr_t)p.obs_out) & 15u) == 0;
     if (h->streaming && obs16) {
         const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
-        const int fuse_bit = p.obs_out == p.obs ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
         if (h->one & fuse_bit) {       // one launch: the whole step runs in the scalar phase
             if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
             launch_one(h, p, stream);
@@ -938,7 +1115,8 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-        if (h->one & bit) part[m] = "step_env_kernel";
+        if (h->flat1 & bit) part[m] = "step_flat_kernel";
+        else if (h->one & bit) part[m] = "step_env_kernel";
         else if (h->fused & bit) part[m] = "advance_rows_kernel<fused>";
         else {
             snprintf(buf[m], sizeof buf[m], "%s+%s", k1, m ? ip2 : db2);
@@ -960,6 +1138,7 @@ int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
 int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
     if (!h || !src) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
+    flat1_invalidate(h);
     hipError_t e = hipMemcpyAsync(h->state, src, h->state_bytes, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) { set_err(h, "set_state: %s", hipGetErrorString(e)); return PMENV_ERR_HIP; }
     return PMENV_OK;

@@ -1,0 +1,187 @@
+// step_flat.h — the whole env step in ONE launch over the flat window stream.
+//
+// TradingEnv.step (zachramsey/pm-rl env/sim/trading_env.py:44-105) and the one-day
+// window advance (data/instrument.py:79 price relatives, :339-356 sliding window) for
+// every env of the batch, with the workgroup geometry of the fastest window stream
+// (advance_flat_inplace_kernel: fixed 16 KiB tiles of the flat [B, N, W, F] tensor,
+// independent of the env size) and the scalar step folded in:
+//
+//   workgroup g owns output chunks [1024 g, 1024 g + 1024) of the flat tensor (16 KiB;
+//   256 threads x 4 chunks), which touch envs e_lo .. e_hi (at most one per wave;
+//   host-checked).
+//   1. wave w < ne issues env (e_lo + w)'s scalar loads (action, bar row, and the
+//      state snapshot: value, counter, get_last(), last close);
+//   2. every wave issues its aligned 16-B window loads (one coalesced 1 KiB per wave
+//      instruction), and lanes 0-1 the two chunks past the tile (the halo);
+//   3. wave w < ne runs env (e_lo + w)'s scalar step (scalar_finish: f64 DPP
+//      reductions, bitwise the same as every other step path) while the window is in
+//      flight, and leaves w', the bar rows and the counter in LDS;
+//   4. the window image goes to LDS; ONE barrier;
+//   5. each lane composes its output chunks (shifted source from LDS neighbours, the
+//      env's bar / w' where a row's last day or weight slot falls) and stores them.
+//
+// Several workgroups run the scalar step of an env that straddles their tiles; only the
+// workgroup holding the env's first chunk (its owner) writes the env's state, reward and
+// ring slot. The others must read the state from before the step whatever the owner's
+// timing, and a launch has no ordering between workgroups (cdna_hip_programming.md
+// Guideline 16), so the state the scalar step reads — value, counter, get_last() and the
+// window's last close — is a per-step snapshot: read from parity p, written by the owner
+// into parity 1 - p; the host flips p every step (pmenv.hip). In place, the two chunks
+// past a tile belong to the next tile, which may already have advanced them: they are
+// the next tile's first two output chunks of the previous step, which that tile also
+// stored into the halo buffer of parity 1 - p. After anything else touched the state or
+// the window (reset, set_state, another step path, a different obs), the host primes
+// the snapshot and the halo from the canonical state and the window (flat_prime_kernel)
+// before the step. Under hipGraph capture the host takes another path (the parity is a
+// launch argument, frozen under replay).
+#pragma once
+#include "env_step.h"
+
+namespace pmenv_dev {
+
+// the snapshot loads of scalar_load_row: value / counter / get_last() / last close from
+// parity p, the rest as scalar_load_row (reward statistics: only the owner uses them)
+__device__ __forceinline__ ScalarIn scalar_load_snap(const StepParams& p, int b, int lane) {
+    const int N = p.N;
+    const uint32_t nb = (uint32_t)N * 4u, off = (uint32_t)lane * 4u;
+    ScalarIn in;
+    in.k = p.sk_in[b];
+    in.v_prev = p.sv_in[b];
+    in.sa = p.sa[b];
+    in.sb = p.sb[b];
+    in.a = buf_load1(make_rsrc(p.action + (size_t)b * N, nb), off);
+    in.wlf = buf_load1(make_rsrc(p.sw_in + (size_t)b * N, nb), off);
+    in.pl = buf_load1(make_rsrc((p.prices ? p.prices : p.slc_in) + (size_t)b * N, nb), off);
+    const float* barb = env_bar(p, b);            // null: out-of-range day -> the descriptor reads 0
+    in.bar = buf_load4(make_rsrc(barb ? barb : p.bar, barb ? nb * 4u : 0u), off * 4u);
+    in.bar_ok = barb != nullptr;
+    in.cn = 0.0f;
+    return in;
+}
+
+// What a tile needs from memory: its window chunks, the two chunks past it (halo), and
+// wave w's env scalar inputs (w < ne).
+template <int V>
+struct FlatTile {
+    uint32_t c0, nblk, e_lo;
+    int ne;
+    f4 own[V];
+    f4 hal;
+    ScalarIn sin;
+};
+
+template <int BLOCK, int V, int POL, bool OUT>
+__device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, uint32_t tile, FlatTile<V>& t) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    t.c0 = tile * (uint32_t)CPW;
+    t.nblk = min((uint32_t)CPW, qtot - t.c0);
+    t.e_lo = fdiv(t.c0, p.div_units);                                  // div_units: per4
+    t.ne = (int)(fdiv(t.c0 + t.nblk - 1u, p.div_units) - t.e_lo) + 1;  // <= BLOCK / 64 (host-checked)
+    // 1. the scalar step's loads (wave-uniform branch), 2. the window stream and the halo
+    if (wave < t.ne) t.sin = scalar_load_snap(p, (int)t.e_lo + wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const auto rs = make_rsrc(p.obs + (size_t)t.c0 * 4, t.nblk * 16u);
+#pragma unroll
+    for (int v = 0; v < V; ++v) t.own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    const uint32_t ntiles = (qtot + CPW - 1) / CPW;
+    const uint32_t nh = tile + 1 < ntiles ? min(2u, qtot - t.c0 - t.nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(t.c0 + t.nblk) * 4 : p.halo_in + (size_t)tile * 8;
+    t.hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int BLOCK, int V, int POL, bool OUT>
+__device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot, uint32_t tile, const FlatTile<V>& t,
+                                              f4* sh4, f4 (*sh_bar)[64], float (*sh_wp)[64], int32_t* sh_k) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V, F = 5;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t per4 = p.per4;
+    // 3. the scalar steps, one env per wave
+    if (wave < t.ne) {
+        const int b = (int)t.e_lo + wave;
+        int32_t kb;
+        const bool owner = (uint64_t)b * per4 >= t.c0;                 // the env's first chunk is ours
+        const float wp = scalar_finish<64, true, true>(p, b, lane, t.sin, kb, owner);
+        sh_wp[wave][lane] = wp;
+        sh_bar[wave][lane] = t.sin.bar_ok ? t.sin.bar : f4{NAN, NAN, NAN, NAN};   // day outside the series
+        if (lane == 0) sh_k[wave] = kb;
+    }
+    // 4. the window image
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = t.own[v];
+    if (tid < 2) sh4[CPW + tid] = t.hal;
+    __syncthreads();
+    // 5. compose and store; only chunks holding a row's last day or (ring full, storage
+    // order) its weight slot read the env's bar / w' from LDS
+    const int WF = p.W * F;
+    const auto rd = make_rsrc((OUT ? p.obs_out : p.obs) + (size_t)t.c0 * 4, t.nblk * 16u);
+    const bool first_out = !OUT && tile > 0;                            // feeds the previous tile's halo
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(t.c0 + (uint32_t)j, qtot - 1u);          // lanes past the end: any chunk
+        const uint32_t e = fdiv(q, p.div_units);
+        const int le = (int)(e - t.e_lo);
+        const uint32_t j0 = 4u * (q - e * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        FlatSide sd;
+        sd.kk = (int)(j0 - row * (uint32_t)WF);
+        sd.bar_nan = false;
+        sd.k = sh_k[le];
+        const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && sd.k >= p.W - 1);
+        const int slot_w =
+            (int)(((uint32_t)(1 + sd.k) - fdiv((uint32_t)(1 + sd.k), p.div_w) * (uint32_t)p.W) * F + (F - 1));
+        const bool need = sd.kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - sd.kk) <= 3u);
+        sd.xb = f4{0.f, 0.f, 0.f, 0.f};
+        sd.xwp = 0.f;
+        if (need) {
+            sd.xb = sh_bar[le][row];
+            sd.xwp = sh_wp[le][row];
+        }
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {t.own[v].x, t.own[v].y, t.own[v].z, t.own[v].w};
+        const f4 o = flat_compose(p, sd, un, sh);
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                     // past the end: dropped
+        if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
+    }
+}
+
+// POL: cache policy of the window stream (0 default, 1 nt); OUT: double-buffered (the
+// two chunks past a tile are read straight from obs, no halo). BLOCK x V: 256 x 4 (env
+// windows of >= 511 chunks) or 512 x 2 (148 .. 510), host-chosen. Held to 80 SGPRs where
+// the compiler can (512 x 2: 8 waves per SIMD instead of 7).
+template <int BLOCK, int V, int POL, bool OUT>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void step_flat_kernel(StepParams p,
+                                                                                              uint32_t qtot) {
+    constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64;
+    __shared__ f4 sh4[CPW + 2];
+    __shared__ f4 sh_bar[WAVES][64];
+    __shared__ float sh_wp[WAVES][64];
+    __shared__ int32_t sh_k[WAVES];
+    FlatTile<V> t;
+    flat1_load<BLOCK, V, POL, OUT>(p, qtot, blockIdx.x, t);
+    flat1_process<BLOCK, V, POL, OUT>(p, qtot, blockIdx.x, t, sh4, sh_bar, sh_wp, sh_k);
+}
+
+// Prime the snapshot (parity p) from the canonical state and, in place, the halo of
+// parity p from the window: halo[i] = chunks (i+1)*CPW and (i+1)*CPW + 1 (copy_halo).
+__global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) {
+    copy_halo(p);
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t BN = (size_t)p.B * p.N;
+    for (size_t i = tid; i < (size_t)p.B; i += nthr) {
+        p.sv_out[i] = p.value[i];
+        p.sk_out[i] = p.k[i];
+    }
+    for (size_t i = tid; i < BN; i += nthr) {
+        p.sw_out[i] = p.w_new[i];
+        p.slc_out[i] = p.last_close[i];
+    }
+}
+
+}  // namespace pmenv_dev

@@ -79,7 +79,8 @@ class TradingEnv:
     def __init__(self, num_envs=1, num_assets=None, window=None, features=5, device=None,
                  config=None, track_info=False, step_impl="auto", **overrides):
         """step_impl: "auto" (per shape), "one_launch" (step_env_kernel, one workgroup per
-        env) or "two_launch" (scalar-step kernel + window stream); see set_step_impl."""
+        env), "flat" (step_flat_kernel, one launch over 16 KiB window tiles) or
+        "two_launch" (scalar-step kernel + window stream); see set_step_impl."""
         if config is None:
             kw = dict(num_envs=num_envs, features=features)
             if num_assets is not None:
@@ -175,8 +176,8 @@ class TradingEnv:
         return v[0] if self._unbatched else v
 
     def set_step_impl(self, impl):
-        """Advance-mode step implementation (pmenv_set_step_path): "auto", "one_launch"
-        or "two_launch". Raises ValueError when the shape does not fit it."""
+        """Advance-mode step implementation (pmenv_set_step_path): "auto", "one_launch",
+        "flat" or "two_launch". Raises ValueError when the shape does not fit it."""
         if impl not in _abi.STEP_PATHS:
             raise ValueError(f"step_impl must be one of {sorted(_abi.STEP_PATHS)}")
         rc = self._lib.pmenv_set_step_path(self._h, _abi.STEP_PATHS[impl])
@@ -317,7 +318,9 @@ class TradingEnv:
         st = sd["state"]
         if st.numel() != self._state.numel():
             raise ValueError("state blob size mismatch (different env shape)")
-        self._state.copy_(st.to(self.device))
+        # through pmenv_set_state: the handle re-primes what it derives from the state
+        src = st.to(device=self.device, dtype=torch.uint8).contiguous()
+        _abi.check(self._lib.pmenv_set_state(self._h, _ptr(src), self._stream()), self._h, "pmenv_set_state")
 
     @property
     def step_path(self):

@@ -1,0 +1,232 @@
+"""step_flat_kernel: the whole advance step in ONE launch over fixed 16 KiB tiles of the
+flat window (the scalar step run by every workgroup an env straddles, the env's state
+written by its owner, a per-step snapshot and in-place halo by parity; step_flat.h).
+
+Checked against the CPU oracle in every mode, bit for bit against the two-launch path
+(and so against every other path) across resets, masked resets, checkpoint restores,
+path switches, resident-series days and hipGraph capture, and at the BASELINE shape.
+Needs an MI355X."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import DEV, MODES, _gpu, _run_both  # noqa: F401  (_gpu: autouse fixture)
+
+pytestmark = pytest.mark.gpu
+
+# (N, W, B): envs of 150 .. 3,760 chunks, i.e. 1 .. 8 envs per 1,024-chunk tile, rows
+# straddling chunks, envs at every offset in a tile, a partial last tile
+SHAPES = [(30, 50, 37), (4, 50, 600), (4, 30, 301), (12, 10, 97), (64, 47, 3), (8, 50, 11), (64, 16, 5),
+          (33, 20, 5), (2, 60, 130), (1, 600, 9)]
+
+
+def _mode_id(k):
+    return "-".join(f"{a}={b}" for a, b in k.items()) or "reference"
+
+
+@pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+@pytest.mark.parametrize("kw", MODES, ids=_mode_id)
+def test_gpu_flat_vs_oracle_modes(kind, db, kw):
+    """Every reward / ring / norm / commission mode, in place and double-buffered, past
+    the ring wrap, against the oracle."""
+    _run_both(kw, B=37, N=30, W=50, T=56, kind=kind, seed=zlib.crc32(f"flat{kw}{kind}{db}".encode()),
+              double_buffer=db, impl="flat")
+
+
+@pytest.mark.parametrize("N,W,B", SHAPES)
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_flat_shapes_vs_oracle(N, W, B, db):
+    _run_both({}, B=B, N=N, W=W, T=W + 7, kind="mixed", seed=N * 13 + W, double_buffer=db, impl="flat")
+    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 7 * W, double_buffer=db,
+              impl="flat")
+
+
+def _state(e):
+    return (e._value.clone(), e._counter.clone(), e._ring.clone(), e._w_new.clone(), e._last_close.clone(),
+            e._stat_a.clone(), e._stat_b.clone())
+
+
+def _same(ga, gb, what):
+    for i, (x, y) in enumerate(zip(ga, gb)):
+        assert torch.equal(x.nan_to_num(7.0), y.nan_to_num(7.0)), f"{what}: state field {i}"
+
+
+@pytest.mark.parametrize("N,W,B", [(30, 50, 37), (4, 30, 301), (64, 47, 3)])
+@pytest.mark.parametrize("kw", [dict(), dict(commission=0.0025, reward="sharpe_ratio"),
+                                dict(ring="chrono", reward="diff_sharpe")], ids=_mode_id)
+def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw):
+    """The flat one-launch step and the two-launch path, driven with the same inputs
+    through everything that invalidates the snapshot / halo — full and masked resets,
+    a checkpoint restore, a switch to another path and back, a different window buffer,
+    in place and double-buffered steps, prices given, resident-series days — agree on
+    every window, reward, returned weight and state field, bit for bit."""
+    from pmenv import TradingEnv, synth
+    T = W + 24
+    ser = synth.series(W + T, B, N, seed=zlib.crc32(f"{N}{W}{kw}".encode()), device=DEV)
+    act = synth.actions(T, B, N, seed=5, device=DEV)
+    kind_mixed = torch.randn(T, B, N, device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+    res = synth.series(T + W + 8, 1, N, seed=9, device=DEV)[:, 0].contiguous()
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i, track_info=True, **kw)
+            for i in ("flat", "two_launch")]
+    assert "step_flat_kernel" in envs[0].step_path and "step_flat_kernel" not in envs[1].step_path
+    obs = [synth.window_from_series(ser, W) for _ in envs]
+    for e, o in zip(envs, obs):
+        e.reset(o)
+    cks, obs_cks = [None, None], [None, None]
+    rng = np.random.default_rng(N + W)
+    for t in range(T):
+        a = kind_mixed[t] if t % 5 == 3 else act[t]
+        mask9 = torch.as_tensor(rng.random(B) < 0.4, device=DEV) if t == 9 else None
+        outs = []
+        for i, e in enumerate(envs):
+            if mask9 is not None:                         # masked reset mid-run
+                e.reset(obs[i], mask=mask9)
+            if t == 14:                                   # checkpoint (state and window)
+                cks[i], obs_cks[i] = e.state_dict(), obs[i].clone()
+            if t == 20 and i == 0:
+                e.set_step_impl("two_launch")             # another path writes the state...
+            if t == 22 and i == 0:
+                e.set_step_impl("flat")                   # ...and the flat step re-primes
+            if t == 26:                                   # restore the t = 14 checkpoint
+                e.load_state_dict(cks[i])
+                obs[i].copy_(obs_cks[i])
+            wo = torch.empty(B, N, device=DEV)
+            if t % 4 == 1:                                # double-buffered
+                r, obs[i] = e.step(a, obs[i], bar=ser[W + t], out=torch.empty_like(obs[i]), weights_out=wo)
+            elif t % 7 == 5:                              # a fresh window buffer, in place
+                obs[i] = obs[i].clone()
+                r, _ = e.step(a, obs[i], bar=ser[W + t], weights_out=wo)
+            elif t % 6 == 2:                              # resident-series days
+                day = torch.full((B,), t + W, dtype=torch.int32, device=DEV)
+                day[::3] += 2
+                r, _ = e.step(a, obs[i], series=res, day=day, weights_out=wo)
+            elif t % 9 == 4:                              # caller prices
+                r, _ = e.step(a, obs[i], bar=ser[W + t], prices=ser[W + t, ..., 3] / ser[W + t - 1, ..., 3],
+                              weights_out=wo)
+            else:
+                r, _ = e.step(a, obs[i], bar=ser[W + t], weights_out=wo)
+            outs.append((r.clone(), wo, e.info["returns"][-1]))
+        assert torch.equal(obs[0], obs[1]), f"step {t}: windows"
+        assert torch.equal(outs[0][0].nan_to_num(7.0), outs[1][0].nan_to_num(7.0)), f"step {t}: rewards"
+        assert torch.equal(outs[0][1], outs[1][1]), f"step {t}: weights"
+        assert torch.equal(outs[0][2].nan_to_num(7.0), outs[1][2].nan_to_num(7.0)), f"step {t}: returns"
+        _same(_state(envs[0]), _state(envs[1]), f"step {t}")
+
+
+def test_gpu_flat_masked_reset_same_mask():
+    """Masked resets every sixth step on both paths, state compared after each step."""
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 300, 4, 30, 40
+    ser = synth.series(W + T, B, N, seed=1, device=DEV)
+    act = synth.actions(T, B, N, seed=2, device=DEV)
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
+    obs = [synth.window_from_series(ser, W) for _ in envs]
+    for e, o in zip(envs, obs):
+        e.reset(o)
+    g = torch.Generator(DEV).manual_seed(4)
+    for t in range(T):
+        mask = torch.rand(B, device=DEV, generator=g) < 0.2 if t % 6 == 5 else None
+        rs = []
+        for e, o in zip(envs, obs):
+            if mask is not None:
+                e.reset(o, mask=mask)
+            rs.append(e.step(act[t], o, bar=ser[W + t])[0])
+        assert torch.equal(obs[0], obs[1]) and torch.equal(rs[0], rs[1]), f"step {t}"
+        _same(_state(envs[0]), _state(envs[1]), f"step {t}")
+
+
+def test_gpu_flat_graph_capture_takes_another_path():
+    """A step captured into a hipGraph cannot carry the flat step's per-step parity; the
+    captured step takes the two-launch path, and replays equal the eager flat step."""
+    import ctypes
+    from pmenv import TradingEnv, synth, _abi
+    B, N, W, T = 2048, 30, 50, 6
+    ser = synth.series(W + T, B, N, device=DEV)
+    act = synth.actions(T, B, N, device=DEV)
+    obs_a = synth.window_from_series(ser, W)
+    obs_b = obs_a.clone()
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    torch.cuda.synchronize()
+    lib = _abi.load()
+    rew = torch.empty(T, B, device=DEV)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for t in range(T):
+            _abi.check(lib.pmenv_step(eb._h, ctypes.c_void_p(act[t].data_ptr()), None,
+                                      ctypes.c_void_p(ser[W + t].data_ptr()), ctypes.c_void_p(obs_b.data_ptr()),
+                                      ctypes.c_void_p(rew[t].data_ptr()), s), eb._h)
+    obs_b.copy_(synth.window_from_series(ser, W))
+    eb.reset(obs_b)
+    g.replay()
+    ref = torch.stack([ea.step(act[t], obs_a, bar=ser[W + t])[0] for t in range(T)])
+    torch.cuda.synchronize()
+    assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)
+    # and the eager flat step after the replay re-primes from the graph's state
+    ra, _ = ea.step(act[0], obs_a, bar=ser[W])
+    rb, _ = eb.step(act[0], obs_b, bar=ser[W])
+    assert torch.equal(ra, rb) and torch.equal(obs_a, obs_b)
+
+
+def test_gpu_flat_path_rules():
+    """FLAT takes F = 5, W >= 2, N <= 64 windows of >= 148 chunks (at most one env per
+    wave of a tile: 256 x 4 from 511 chunks, 512 x 2 below); a forced FLAT that does not
+    fit is refused and the handle keeps its path."""
+    from pmenv import TradingEnv
+    ok = TradingEnv(num_envs=5, num_assets=30, window=50, device=DEV, step_impl="flat")
+    assert ok.step_path == "step_flat_kernel (obs_out) | step_flat_kernel (in place)"
+    for n, w in [(1, 4), (4, 20), (65, 50)]:           # 5 / 100 chunks per env; N > 64
+        e = TradingEnv(num_envs=5, num_assets=n, window=w, device=DEV)
+        before = e.step_path
+        with pytest.raises(ValueError):
+            e.set_step_impl("flat")
+        assert e.step_path == before
+
+
+def test_gpu_flat_full_size_properties():
+    """BASELINE config (65,536 envs x 30 x 50 x 5) by the flat one-launch step, through
+    the ring wrap, alternating in place and double-buffered: the market channels are the
+    sliding series, the reward log(sum w*y), the value compounds the returns, the weight
+    channel is get_all(); and a 64-env sample against the oracle."""
+    from oracle import OracleEnv
+    from pmenv import TradingEnv, synth
+    from pmenv.config import EnvConfig
+    B, N, W, F, T = 65536, 30, 50, 5, 60
+    ser = synth.series(W + T, B, N, seed=21, device=DEV)
+    act = synth.actions(T, B, N, seed=22, device=DEV)
+    obs = synth.window_from_series(ser, W, F)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, step_impl="flat")
+    env.reset(obs)
+    logv = torch.full((B,), float(np.log(25000.0)), dtype=torch.float64, device=DEV)
+    spare = torch.empty_like(obs)
+    for t in range(T):
+        if t % 3 == 2:
+            r, nxt = env.step(act[t], obs, bar=ser[W + t], out=spare)
+            obs, spare = nxt, obs
+        else:
+            r, _ = env.step(act[t], obs, bar=ser[W + t])
+        y = (ser[W + t, ..., 3] / ser[W + t - 1, ..., 3]).double()
+        ref = torch.log((act[t].double() * y).sum(-1))
+        err = (r.double() - ref).abs()
+        assert bool((err <= 1e-6 * ref.abs() + 1e-8).all()), f"step {t}: {float(err.max()):.3e}"
+        logv += ref
+    assert torch.equal(obs[..., :4], ser[T:T + W].permute(1, 2, 0, 3))
+    assert torch.allclose(env.value.log(), logv, rtol=0, atol=1e-9)
+    assert torch.equal(obs[..., 4], env.weights.get_all())
+    assert env.nonfinite_count() == 0
+    S = 64
+    cenv = OracleEnv(EnvConfig(num_envs=S, num_assets=N, window=W, features=F))
+    cobs = synth.window_from_series(ser[:, :S].contiguous(), W, F).cpu().numpy().copy()
+    cenv.reset(cobs)
+    ser_h, act_h = ser[:, :S].cpu().numpy(), act[:, :S].cpu().numpy()
+    for t in range(T):
+        cr, _, _ = cenv.step(act_h[t], cobs, bar=ser_h[W + t])
+    np.testing.assert_allclose(env.value[:S].cpu().numpy(), cenv.value, rtol=1e-12)
+    assert np.array_equal(obs[:S, ..., :4].cpu().numpy(), cobs[..., :4])
+    np.testing.assert_allclose(obs[:S, ..., 4].cpu().numpy(), cobs[..., 4], rtol=2e-7, atol=1e-12)

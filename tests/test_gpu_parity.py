@@ -234,18 +234,27 @@ def test_gpu_flat_inplace_shapes(N, W, B):
 
 
 def test_gpu_auto_path_rule():
-    """AUTO takes the one-launch step for windows up to 48 MiB (launch-latency bound:
-    it wins there at every asset count measured) and the two-launch stream above (its
-    fixed geometry is the faster one on large windows at most asset counts); checked
-    against the oracle just above the threshold (1,700 envs x 30 x 50: 51 MB)."""
+    """AUTO: windows up to 48 MiB take the one-workgroup-per-env step (launch-latency
+    bound: it wins there at every asset count measured); above, env windows of >= 1,000
+    chunks take the flat one-launch step (step_flat_kernel) — double-buffered from 48 MiB,
+    in place from 256 MiB (in place, cache-resident windows are faster on the two-launch
+    stream) — and smaller env windows the two-launch stream. Checked against the oracle
+    just above the 48 MiB threshold (1,700 envs x 30 x 50: 51 MB)."""
     from pmenv import TradingEnv
     small = TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV)          # 45 MB
     assert small.step_path.count("step_env_kernel") == 2
     big = TradingEnv(num_envs=1700, num_assets=30, window=50, device=DEV)            # 51 MB
     db, ip = big.step_path.split(" | ")
-    assert "advance_flat_wg_kernel" in db and "advance_flat_inplace_kernel" in ip
+    assert db.startswith("step_flat_kernel") and "advance_flat_inplace_kernel" in ip
+    huge = TradingEnv(num_envs=9000, num_assets=30, window=50, device=DEV)           # 270 MB
+    assert huge.step_path.count("step_flat_kernel") == 2
+    thin = TradingEnv(num_envs=9000, num_assets=8, window=50, device=DEV)            # 500 chunks per env
+    assert "step_flat_kernel" not in thin.step_path and "step_env_kernel" not in thin.step_path
+    wide = TradingEnv(num_envs=2000, num_assets=65, window=50, device=DEV)           # N > 64
+    assert "step_flat_kernel" not in wide.step_path
     _run_both({}, B=1700, N=30, W=50, T=9, kind="mixed", seed=31)
     _run_both({"ring": "chrono"}, B=1700, N=30, W=50, T=5, kind="simplex", seed=32, double_buffer=True)
+    _run_both({}, B=9000, N=30, W=50, T=7, kind="mixed", seed=33)
 
 
 @pytest.mark.parametrize("impl", ["one_launch", "two_launch"])

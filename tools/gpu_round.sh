@@ -16,4 +16,4 @@ ARGS="--steps 200 --warmup 20 --cpu-baseline 0 --alt-steps 50"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_$TAG.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --alt-steps 0 > gpurun_out/pmc_fetch_$TAG.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --alt-steps 0 > gpurun_out/pmc_write_$TAG.log 2>&1 || exit $?
-grep -E "step_env|advance_|scalar_step" gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -c1-170
+grep -E "step_env|step_flat|flat_prime|advance_|scalar_step" gpurun_out/prof_$TAG/run_kernel_stats.csv | cut -c1-170

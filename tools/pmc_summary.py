@@ -37,13 +37,14 @@ alg = (8 * N * W * F + 20) * B
 res = {"tag": tag, "workload": shape, "algorithmic_bytes_per_launch": alg, "kernels": {}}
 for k in sorted(set(fetch) | set(write)):
     if "advance_rows" not in k and "advance_flat" not in k and "scalar_step" not in k and "step_advance" not in k \
-            and "step_env" not in k:
+            and "step_env" not in k and "step_flat" not in k and "flat_prime" not in k:
         continue
     fb = fetch.get(k, 0.0) * 1024 * 2
     wb = write.get(k, 0.0) * 1024
     res["kernels"][k] = {"fetch_size_kib_raw": fetch.get(k), "write_size_kib": write.get(k),
                          "hbm_read_bytes_corrected": fb, "hbm_write_bytes": wb, "hbm_bytes": fb + wb}
-main = [k for k in res["kernels"] if "step_env_kernel<4, false" in k] or \
+main = [k for k in res["kernels"] if "step_flat_kernel" in k and ", false>" in k] or \
+       [k for k in res["kernels"] if "step_env_kernel<4, false" in k] or \
        [k for k in res["kernels"] if "advance_flat_inplace_kernel" in k] or \
        [k for k in res["kernels"] if "advance_flat_wg_kernel" in k] or \
        [k for k in res["kernels"] if "advance_flat_kernel" in k] or \
