@@ -23,6 +23,8 @@ ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--H", type=int, default=64)
 ap.add_argument("--phases", type=int, default=0, help="pmenv_step_args.phases (1: scalar step only)")
 ap.add_argument("--series-days", type=int, default=512, help="resident series length for '+DAY' variants")
+ap.add_argument("--commission", type=float, default=0.0)
+ap.add_argument("--reward", default="log_returns")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 B, N, W = a.envs, a.assets, a.window
@@ -60,7 +62,7 @@ for v in a.variants.split(","):
     else:
         os.environ["PMENV_ADVANCE"] = base
     obs = synth.window_from_series(ser, W)
-    e = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
+    e = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev, commission=a.commission, reward=a.reward)
     e.reset(obs)
     print(v, e.step_path, file=sys.stderr)
     envs[v] = (e, obs, torch.empty(B, device=dev), obs.clone() if base.endswith("o") else None)
