@@ -220,7 +220,10 @@ def reference_golden_mae(dev, torch, TradingEnv):
 
 
 def spread(us):
-    return {"min": min(us), "median": statistics.median(us), "max": max(us), "samples": len(us)}
+    """min / median / max of the sampled kernel times, and which sample was the slowest
+    (sample i brackets timed step EVENT_EVERY * i)."""
+    return {"min": min(us), "median": statistics.median(us), "max": max(us), "samples": len(us),
+            "slowest_sample": max(range(len(us)), key=us.__getitem__)}
 
 
 def main():

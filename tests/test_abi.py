@@ -119,5 +119,17 @@ def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
             assert args[0] == "4" and args[3] == "0", k                             # V = 4, ABL = 0
         if name == "advance_rows_kernel":
             assert args[0] == "512" and args[3] == "0" and args[4] == "false", k    # ABL = 0, not fused
+        if name == "step_flat_kernel":
+            assert args[:2] in (["256", "4"], ["512", "2"]), k                      # the two product geometries
     assert not any(k.startswith(("gae_tile_vec_kernel", "replay_gather_f5_kernel", "advance_flat_kernel<"))
                    for k in kernels)
+
+
+def test_step_path_kinds_match_the_header():
+    """pmenv_step_path_kind in include/pmenv.h and the Python wrapper's names agree."""
+    from pmenv import _abi
+    hdr = open(os.path.join(ROOT, "include", "pmenv.h")).read()
+    kinds = dict((m.group(1).lower(), int(m.group(2)))
+                 for m in re.finditer(r"PMENV_STEP_PATH_(\w+) = (\d+)", hdr))
+    assert kinds == {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3}
+    assert _abi.STEP_PATHS == kinds
