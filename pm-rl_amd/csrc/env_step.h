@@ -419,7 +419,7 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
         if (p.weights) p.weights[i] = wp;
         if (p.bar) p.last_close[i] = cn;
         if (SNAP) {
-            p.sw_out[i] = wp;
+            if (p.commission > 0.0) p.sw_out[i] = wp;      // get_last() feeds only the fixed point
             p.slc_out[i] = cn;
         }
     }

@@ -96,6 +96,7 @@ struct pmenv {
     float* halo1[2];      // [halo1_wgs][2] float4 per parity: the next tile's first two chunks
     uint32_t halo1_wgs;
     int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread (tools: PMENV_FLAT1_GEOM)
+    bool flat1_xcd;               // tools: XCD-contiguous tile ranges (PMENV_FLAT1_XCD)
     int par;              // parity of the snapshot / halo the next step reads
     bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
     const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
@@ -546,7 +547,11 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     }
     const int key = h->flat1_block * 100 + h->flat1_vec;
 #ifdef PMENV_AB
-    if (key == 51204) { PMENV_FLAT1_LAUNCH(512, 4) }
+    if (key == 25604 && h->flat1_xcd) {
+        if (out) step_flat_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        else step_flat_kernel<256, 4, 1, false, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+    }
+    else if (key == 51204) { PMENV_FLAT1_LAUNCH(512, 4) }
     else if (key == 102402) { PMENV_FLAT1_LAUNCH(1024, 2) }
     else if (key == 25608) { PMENV_FLAT1_LAUNCH(256, 8) }
     else if (key == 25602) { PMENV_FLAT1_LAUNCH(256, 2) }
@@ -860,6 +865,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->flat1_auto = h->flat1_ok && atoi(knob) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
         h->one_auto = h->flat1_auto ? 0 : one_auto_base;
     }
+    h->flat1_xcd = ab_int("PMENV_FLAT1_XCD", 0) != 0;
     if (const char* knob = ab_knob("PMENV_FLAT1_GEOM")) {   // "512x2" | "512x4" | "1024x2" | "256x8" | ...
         int bk = 0, vv = 0;
         if (sscanf(knob, "%dx%d", &bk, &vv) == 2) {

@@ -50,7 +50,9 @@ __device__ __forceinline__ ScalarIn scalar_load_snap(const StepParams& p, int b,
     in.sa = p.sa[b];
     in.sb = p.sb[b];
     in.a = buf_load1(make_rsrc(p.action + (size_t)b * N, nb), off);
-    in.wlf = buf_load1(make_rsrc(p.sw_in + (size_t)b * N, nb), off);
+    // get_last() only feeds the commission fixed point (a handle constant): without it
+    // the snapshot carries no weights (the descriptor has no records: no traffic)
+    in.wlf = buf_load1(make_rsrc(p.sw_in + (size_t)b * N, p.commission > 0.0 ? nb : 0u), off);
     in.pl = buf_load1(make_rsrc((p.prices ? p.prices : p.slc_in) + (size_t)b * N, nb), off);
     const float* barb = env_bar(p, b);            // null: out-of-range day -> the descriptor reads 0
     in.bar = buf_load4(make_rsrc(barb ? barb : p.bar, barb ? nb * 4u : 0u), off * 4u);
@@ -154,7 +156,7 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
 // two chunks past a tile are read straight from obs, no halo). BLOCK x V: 256 x 4 (env
 // windows of >= 511 chunks) or 512 x 2 (148 .. 510), host-chosen. Held to 80 SGPRs where
 // the compiler can (512 x 2: 8 waves per SIMD instead of 7).
-template <int BLOCK, int V, int POL, bool OUT>
+template <int BLOCK, int V, int POL, bool OUT, bool XCD = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void step_flat_kernel(StepParams p,
                                                                                               uint32_t qtot) {
     constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64;
@@ -162,9 +164,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void st
     __shared__ f4 sh_bar[WAVES][64];
     __shared__ float sh_wp[WAVES][64];
     __shared__ int32_t sh_k[WAVES];
+    uint32_t tile = blockIdx.x;
+    if (XCD) {   // tools A/B: XCD x (workgroups x, x + 8, ...) takes a contiguous range of tiles
+        const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = tile & 7, i = tile >> 3;
+        tile = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+    }
     FlatTile<V> t;
-    flat1_load<BLOCK, V, POL, OUT>(p, qtot, blockIdx.x, t);
-    flat1_process<BLOCK, V, POL, OUT>(p, qtot, blockIdx.x, t, sh4, sh_bar, sh_wp, sh_k);
+    flat1_load<BLOCK, V, POL, OUT>(p, qtot, tile, t);
+    flat1_process<BLOCK, V, POL, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
 }
 
 // Prime the snapshot (parity p) from the canonical state and, in place, the halo of
