@@ -18,6 +18,8 @@
  *      - the one-launch step (step_env.h): a workgroup owns one env; its slots are the
  *        env's 1 KiB-aligned 64-chunk blocks, lanes outside the env read 0 and store
  *        nothing. Reads outside the env are checked never to feed a kept position.
+ * 3. Emulates the flat one-launch step (step_flat.h) over consecutive steps: tiles in a
+ *    random order, the halo and the state snapshot by parity, one owner per env (below).
  * Exit status 0 = clean (UBSan built with -fno-sanitize-recover: any report aborts).
  */
 #include <math.h>
@@ -252,6 +254,139 @@ static void emulate(int B, int N, int W, int CPW, int shift_w, int slot) {
     free(mem); free(init); free(ref); free(bar); free(wp); free(stored); free(halo); free(order); free(lds); free(img);
 }
 
+/* ------------------------------------------------------------ 3. the flat one-launch step */
+/* step_flat.h over T consecutive steps: tiles of CPW chunks in a random order each step,
+ * every store visible at once. A tile reads only its own chunks from the window (checked:
+ * no chunk read after a store), the two chunks past it from the halo of parity p (checked:
+ * nothing writes parity p during the step) and each env's scalar inputs from the state
+ * snapshot of parity p (checked likewise); the env's owner — the tile holding its first
+ * chunk, exactly one per env (checked) — writes the canonical state and the snapshot of
+ * parity 1 - p, and every tile its first two output chunks into the halo of parity 1 - p.
+ * w' and the counter that every tile of an env uses come from the snapshot, so all tiles of
+ * an env must agree with the owner (checked through the result). Mid-run the canonical
+ * state changes outside the step (a reset) and the snapshot and halo are re-primed. The
+ * window after each step must equal the out-of-place advance, bit for bit. */
+static float flat1_wp(double v, int32_t k, int64_t b, int n) {          /* stands in for w' */
+    return (float)(fmod(v * 1e-3 + 0.37 * n + 0.11 * k + 0.05 * (double)b, 1.0));
+}
+
+static void emulate_flat1(int B, int N, int W, int CPW, int T, int storage) {
+    const int F = 5, WF = W * F;
+    const int64_t per = (int64_t)N * WF, tot = per * B;
+    if (per % 4) return;
+    const int64_t per4 = per / 4, qtot = tot / 4, ntiles = (qtot + CPW - 1) / CPW;
+    float* mem = malloc(sizeof(float) * tot);
+    float* ref = malloc(sizeof(float) * tot);
+    float* nxt = malloc(sizeof(float) * tot);
+    float* bar = malloc(sizeof(float) * B * N * 4);
+    float* wp = malloc(sizeof(float) * B * N);
+    double* value = malloc(sizeof(double) * B);
+    int32_t* k = malloc(sizeof(int32_t) * B);
+    double* sv[2] = {malloc(sizeof(double) * B), malloc(sizeof(double) * B)};
+    int32_t* sk[2] = {malloc(sizeof(int32_t) * B), malloc(sizeof(int32_t) * B)};
+    float* halo[2] = {calloc((size_t)ntiles * 8, sizeof(float)), calloc((size_t)ntiles * 8, sizeof(float))};
+    uint8_t* halo_w[2] = {calloc((size_t)ntiles, 1), calloc((size_t)ntiles, 1)};   /* written this step */
+    uint8_t* snap_w[2] = {calloc((size_t)B, 1), calloc((size_t)B, 1)};
+    uint8_t* owners = calloc((size_t)B, 1);
+    uint8_t* stored = calloc((size_t)qtot, 1);
+    int* order = malloc(sizeof(int) * (size_t)ntiles);
+    float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
+    for (int64_t i = 0; i < tot; ++i) mem[i] = ref[i] = (float)nrand();
+    for (int b = 0; b < B; ++b) { value[b] = 25000.0 + b; k[b] = (int32_t)(urand() * 2 * W); }
+    int par = 0, primed = 0;
+    for (int t = 0; t < T; ++t) {
+        if (t == T / 2) {                               /* a reset outside the step: re-prime */
+            for (int b = 0; b < B; b += 2) { value[b] = 25000.0; k[b] = 0; }
+            primed = 0;
+        }
+        if (!primed) {                                  /* flat_prime_kernel */
+            for (int b = 0; b < B; ++b) { sv[par][b] = value[b]; sk[par][b] = k[b]; }
+            for (int64_t i = 0; i + 1 < ntiles; ++i)
+                for (int h = 0; h < 2; ++h) {
+                    const int64_t q = (i + 1) * CPW + h;
+                    for (int e = 0; e < 4; ++e) halo[par][i * 8 + h * 4 + e] = q < qtot ? mem[q * 4 + e] : 0.0f;
+                }
+            primed = 1;
+        }
+        for (int i = 0; i < B * N * 4; ++i) bar[i] = (float)nrand();
+        /* the expected result: the out-of-place advance with each env's own counter */
+        for (int b = 0; b < B; ++b) {
+            for (int n = 0; n < N; ++n) wp[b * N + n] = flat1_wp(value[b], k[b], b, n);
+            const int shift_w = !(storage && k[b] >= W - 1), slot = (int)((1 + (int64_t)k[b]) % W);
+            advance_ref(ref + (size_t)b * per, nxt + (size_t)b * per, 1, N, W, bar + (size_t)b * N * 4,
+                        wp + (size_t)b * N, shift_w, slot);
+        }
+        memset(stored, 0, (size_t)qtot);
+        for (int h = 0; h < 2; ++h) {
+            memset(halo_w[h], 0, (size_t)ntiles);
+            memset(snap_w[h], 0, (size_t)B);
+        }
+        memset(owners, 0, (size_t)B);
+        shuffle(order, (int)ntiles);
+        for (int o = 0; o < ntiles; ++o) {
+            const int64_t tile = order[o], c0 = tile * CPW;
+            const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
+            const int64_t e_lo = c0 / per4, e_hi = (c0 + nblk - 1) / per4;
+            for (int64_t q = 0; q < CPW + 2; ++q) {
+                for (int e = 0; e < 4; ++e) lds[q * 4 + e] = 0.0f;
+                if (q < nblk) {
+                    CHECK(!stored[c0 + q], "flat1: chunk %lld read after a store", (long long)(c0 + q));
+                    for (int e = 0; e < 4; ++e) lds[q * 4 + e] = mem[(c0 + q) * 4 + e];
+                } else if (q >= CPW && tile + 1 < ntiles) {
+                    CHECK(!halo_w[par][tile], "flat1: halo %lld read after this step wrote it", (long long)tile);
+                    for (int e = 0; e < 4; ++e) lds[q * 4 + e] = halo[par][tile * 8 + (q - CPW) * 4 + e];
+                }
+            }
+            /* the scalar steps of the tile's envs, from the snapshot of parity p */
+            float* twp = malloc(sizeof(float) * (size_t)(e_hi - e_lo + 1) * N);
+            int32_t* tk = malloc(sizeof(int32_t) * (size_t)(e_hi - e_lo + 1));
+            for (int64_t b = e_lo; b <= e_hi; ++b) {
+                CHECK(!snap_w[par][b], "flat1: env %lld snapshot read after this step wrote it", (long long)b);
+                tk[b - e_lo] = sk[par][b];
+                for (int n = 0; n < N; ++n) twp[(b - e_lo) * N + n] = flat1_wp(sv[par][b], sk[par][b], b, n);
+                if (b * per4 >= c0) {                   /* the owner */
+                    CHECK(!owners[b]++, "flat1: env %lld has two owners", (long long)b);
+                    value[b] = value[b] * 1.0001 + 1.0;
+                    k[b] = k[b] + 1;
+                    sv[1 - par][b] = value[b];
+                    sk[1 - par][b] = k[b];
+                    snap_w[1 - par][b] = 1;
+                }
+            }
+            for (int64_t q = 0; q < nblk; ++q) {
+                const int64_t gq = c0 + q;
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t j = gq * 4 + e, env = j / per;
+                    const int32_t kb = tk[env - e_lo];
+                    const int shift_w = !(storage && kb >= W - 1), slot = (int)((1 + (int64_t)kb) % W);
+                    const float sh = lds[q * 4 + e + 5];
+                    /* compose_float reads w' from a [B, N] array: hand it the tile's copy */
+                    const float v = compose_float(j - env * per + 0, lds[q * 4 + e], sh, N, W,
+                                                  bar + (size_t)env * N * 4, twp + (env - e_lo) * N, 0, shift_w, slot);
+                    mem[j] = v;
+                    if (tile > 0 && q < 2) halo[1 - par][(tile - 1) * 8 + q * 4 + e] = v;
+                }
+                stored[gq] = 1;
+            }
+            if (tile > 0) halo_w[1 - par][tile - 1] = 1;
+            free(twp);
+            free(tk);
+        }
+        for (int b = 0; b < B; ++b) CHECK(owners[b] == 1, "flat1: env %d owned %d times", b, owners[b]);
+        par = 1 - par;
+        float* sw = ref; ref = nxt; nxt = sw;
+        for (int64_t i = 0; i < tot; ++i)
+            if (memcmp(&mem[i], &ref[i], 4)) {
+                CHECK(0, "flat1: step %d float %lld differs (B%d N%d W%d CPW%d)", t, (long long)i, B, N, W, CPW);
+                break;
+            }
+    }
+    free(mem); free(ref); free(nxt); free(bar); free(wp); free(value); free(k); free(sv[0]); free(sv[1]);
+    free(sk[0]); free(sk[1]); free(halo[0]); free(halo[1]); free(halo_w[0]); free(halo_w[1]);
+    free(snap_w[0]); free(snap_w[1]); free(owners); free(stored);
+    free(order); free(lds);
+}
+
 int main(void) {
     /* every reward kind x norm x ring x ret mode, with and without commission */
     for (int kind = 0; kind < 4; ++kind)
@@ -271,6 +406,15 @@ int main(void) {
             for (int cpw = 0; cpw < 2; ++cpw)
                 emulate(shapes[i][0], shapes[i][1], shapes[i][2], cpw ? 1024 : 96, mode == 0,
                         mode ? (int)(urand() * shapes[i][2]) : 0);
+    /* the flat one-launch step: the product's 1,024-chunk tiles (256 x 4 and 512 x 2) and
+     * small tiles that put several tiles in one env and several envs in one tile, both ring
+     * orders, through the wrap and a re-prime */
+    const int fshapes[][3] = {{37, 30, 50}, {301, 4, 30}, {3, 64, 47}, {13, 5, 4}, {9, 1, 4}, {130, 2, 60}};
+    for (size_t i = 0; i < sizeof fshapes / sizeof fshapes[0]; ++i)
+        for (int storage = 0; storage < 2; ++storage)
+            for (int cpw = 0; cpw < 2; ++cpw)
+                emulate_flat1(fshapes[i][0], fshapes[i][1], fshapes[i][2], cpw ? 1024 : 96, 2 * fshapes[i][2] + 3,
+                              storage);
     if (fails) { fprintf(stderr, "%d check(s) failed\n", fails); return 1; }
     printf("sanitize ok\n");
     return 0;
