@@ -278,36 +278,41 @@ def main():
     bar_ptrs = [series[W + t].data_ptr() for t in range(H)]
     act_ptrs = [actions[t].data_ptr() for t in range(H)]
     step_fn = lib.pmenv_step_ex
-    args_s = _abi.PmenvStepArgs()
-    args_s.reward = reward.data_ptr()
-    args_a = _abi.PmenvStepArgs()
-    args_a.reward = reward.data_ptr()
-    ping = [obs, obs_b]
+    ping_ptr = [obs.data_ptr(), obs_b.data_ptr() if obs_b is not None else None]
     paths = env.step_path.split(" | ")              # "<double-buffered> (obs_out) | <in place> (in place)"
+    # one prebuilt argument block per (day, window mode, ping-pong side, phase): the host
+    # work per step is then one ctypes call (small configs are otherwise host-bound)
+    arg_cache = {}
+
+    def step_args(t, double, side, phases):
+        key = (t, double, side, phases)
+        hit = arg_cache.get(key)
+        if hit is None:
+            a = _abi.PmenvStepArgs()
+            a.reward = reward.data_ptr()
+            a.action, a.bar = act_ptrs[t], bar_ptrs[t]
+            a.obs = ping_ptr[side] if double else ping_ptr[0]
+            a.obs_out = ping_ptr[1 - side] if double else None
+            a.phases = phases
+            hit = arg_cache[key] = (a, ctypes.byref(a))
+        return hit[1]
 
     def one_step(i, double, phase_events=None):
         phased = "+" in paths[0 if double else -1]  # two launches: time the window stream on its own
         t = i % H
-        src, dst = (ping[i % 2], ping[(i + 1) % 2]) if double else (obs, None)
-        for a in (args_s, args_a):
-            a.action, a.bar = act_ptrs[t], bar_ptrs[t]
-            a.obs = src.data_ptr()
-            a.obs_out = dst.data_ptr() if dst is not None else None
+        side = i % 2
         if phase_events is None:
-            args_s.phases = 0
-            rc = step_fn(h, ctypes.byref(args_s), sp)
+            rc = step_fn(h, step_args(t, double, side, 0), sp)
         elif phased:
             # same two launches as phases=0, with an event between them so the
             # streaming kernel is timed on its own stream
-            args_s.phases, args_a.phases = _abi.PHASE_SCALAR, _abi.PHASE_ADVANCE
-            rc = step_fn(h, ctypes.byref(args_s), sp)
+            rc = step_fn(h, step_args(t, double, side, _abi.PHASE_SCALAR), sp)
             phase_events[0].record(stream)
-            rc = rc or step_fn(h, ctypes.byref(args_a), sp)
+            rc = rc or step_fn(h, step_args(t, double, side, _abi.PHASE_ADVANCE), sp)
             phase_events[1].record(stream)
         else:                                        # one launch per step: time that launch
-            args_s.phases = 0
             phase_events[0].record(stream)
-            rc = step_fn(h, ctypes.byref(args_s), sp)
+            rc = step_fn(h, step_args(t, double, side, 0), sp)
             phase_events[1].record(stream)
         if rc != 0:
             _abi.check(rc, h, "pmenv_step_ex")
