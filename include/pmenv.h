@@ -178,7 +178,9 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
 
 /* Which kernels the advance path launches for this handle's shape (diagnostics):
  * "<obs_out path> (obs_out) | <in-place path> (in place)", each either
- * "step_env_kernel" (the whole step in one launch) or "<scalar step>+<window stream>"
+ * "step_flat_kernel" (the whole step in one launch over 16 KiB window tiles),
+ * "step_env_kernel" (the whole step in one launch, one workgroup per env) or
+ * "<scalar step>+<window stream>"
  * (two launches); or "step_advance_lds_kernel" (single-launch fallback, any F). */
 const char* pmenv_step_path(const pmenv* h);
 
