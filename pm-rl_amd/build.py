@@ -57,10 +57,30 @@ def build_oracle(force=False):
     return ORACLE_LIB
 
 
+C_ABI_SRC = os.path.join(ROOT, "tests", "c_abi", "c_abi_step.c")
+C_ABI_BIN = os.path.join(ROOT, "tests", "c_abi", "c_abi_step")
+
+
+def build_c_abi_test(force=False):
+    """A plain C caller of the C ABI linked against libpmenv.so and the parity checker
+    (test infrastructure: tests/test_gpu_c_abi.py runs it on the GPU box)."""
+    hdrs = [os.path.join(ROOT, "include", "pmenv.h"), os.path.join(ROOT, "oracle", "pmenv_oracle.h")]
+    if not force and not _stale(C_ABI_BIN, C_ABI_SRC, LIB, ORACLE_LIB, *hdrs):
+        return C_ABI_BIN
+    rocm = os.path.dirname(os.path.dirname(os.path.realpath(HIPCC)))
+    _run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-D__HIP_PLATFORM_AMD__",
+          "-I", os.path.join(rocm, "include"), "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+          "-o", C_ABI_BIN, C_ABI_SRC, "-L", os.path.dirname(LIB), "-lpmenv", "-L", os.path.dirname(ORACLE_LIB),
+          "-loracle", "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-lm",
+          "-Wl,-rpath,$ORIGIN/../../pm-rl_amd/pmenv:$ORIGIN/../../oracle:" + os.path.join(rocm, "lib")])
+    return C_ABI_BIN
+
+
 def build_all(force=False):
     build_pmenv(force)
     build_pmenv(force, ab=True)
     build_oracle(force)
+    build_c_abi_test(force)
 
 
 if __name__ == "__main__":

@@ -133,3 +133,15 @@ def test_step_path_kinds_match_the_header():
                  for m in re.finditer(r"PMENV_STEP_PATH_(\w+) = (\d+)", hdr))
     assert kinds == {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3}
     assert _abi.STEP_PATHS == kinds
+
+
+def test_c_caller_links_the_abi():
+    """tests/c_abi/c_abi_step (a plain C caller, built by pm-rl_amd/build.py) resolves
+    libpmenv.so from the tree."""
+    binary = os.path.join(ROOT, "tests", "c_abi", "c_abi_step")
+    if not os.path.exists(binary):
+        pytest.skip("not built")
+    out = subprocess.run(["ldd", binary], capture_output=True, text=True).stdout
+    line = next(l for l in out.splitlines() if "libpmenv.so" in l)
+    assert "not found" not in line and os.path.realpath(line.split("=>")[1].split()[0]) == \
+        os.path.realpath(os.path.join(ROOT, "pm-rl_amd", "pmenv", "libpmenv.so"))
