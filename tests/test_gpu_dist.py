@@ -25,20 +25,20 @@ def _free_port():
     return p
 
 
-def _run(lo, hi, dev):
+def _run(lo, hi, dev, impl="auto"):
     """Rank work: the global envs [lo, hi) of the synthetic BASELINE workload."""
     from pmenv import TradingEnv, synth
     B = hi - lo
     ser = synth.series(W + T, B, N, env_offset=lo, seed=42, device=dev)
     act = synth.actions(T, B, N, env_offset=lo, seed=43, device=dev)
     obs = synth.window_from_series(ser, W)
-    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev, step_impl=impl)
     env.reset(obs)
     rew = torch.stack([env.step(act[t], obs, bar=ser[W + t])[0] for t in range(T)])   # [T, B]
     return rew, env.value, obs
 
 
-def _worker(rank, world, port, root, q):
+def _worker(rank, world, port, root, q, impl):
     import sys
     for p in (os.path.join(root, "pm-rl_amd"), os.path.join(root, "oracle")):
         sys.path.insert(0, p)
@@ -51,7 +51,7 @@ def _worker(rank, world, port, root, q):
         from pmenv import parallel
         from pmenv.rollout import moments
         lo, hi = parallel.shard_range(G, rank, world)
-        rew, val, obs = _run(lo, hi, dev)
+        rew, val, obs = _run(lo, hi, dev, impl)
         m = moments(rew)                                          # HIP moments kernel, [3] f64 on the GPU
         n, mean, var = parallel.allreduce_moments(m.clone())     # the 24-byte all-reduce
         z = parallel.normalize(rew)
@@ -61,14 +61,17 @@ def _worker(rank, world, port, root, q):
         dist.destroy_process_group()
 
 
-def test_gpu_sharded_ranks_equal_unsharded_run():
+@pytest.mark.parametrize("impl_shards,impl_full", [("auto", "auto"), ("flat", "two_launch")])
+def test_gpu_sharded_ranks_equal_unsharded_run(impl_shards, impl_full):
+    """("flat", "two_launch"): the ranks step with the one-launch flat kernel, the
+    unsharded run with the two-launch path — still the same bits."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, root, q, impl_shards)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])
@@ -77,7 +80,7 @@ def test_gpu_sharded_ranks_equal_unsharded_run():
         assert p.exitcode == 0
     dev = torch.device("cuda:0")
     from pmenv.rollout import moments
-    rew, val, obs = _run(0, G, dev)
+    rew, val, obs = _run(0, G, dev, impl_full)
     full = rew.cpu().numpy()
     fv, fo = val.cpu().numpy(), obs.cpu().numpy()
     m_full = moments(rew).cpu().numpy()
