@@ -296,7 +296,8 @@ void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
     PMENV_FIP(256, 1) PMENV_FIP(256, 2) PMENV_FIP(256, 4) PMENV_FIP(512, 1) PMENV_FIP(1024, 1)
 #undef PMENV_FIP
 #endif
-    if (h->flat_ip_pol == 1) advance_flat_inplace_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
+    if (h->flat_ip_block == 256) advance_flat_inplace_kernel<256, 2, 0><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+    else if (h->flat_ip_pol == 1) advance_flat_inplace_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
     else advance_flat_inplace_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
 }
 
@@ -736,7 +737,10 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->flat = h->flat_inplace = flat_ok;
     h->flat_db_wg = true;
     h->flat_block = 512;
-    h->flat_ip_block = 512;
+    // in place, cache-resident windows (<= 256 MiB) take 8 KiB workgroups: 80.2 vs 83.2 us
+    // at 8,192 x 30, 44.4 vs 44.7 at 4,096 (profiles/ab_r02/r02w_smallip_*); above, 16 KiB
+    // (round 1: 512 x 2 against 256 x 1 / 2 / 4, 512 x 1, 1024 x 1)
+    h->flat_ip_block = (int64_t)c.num_envs * per * 4 <= (256ll << 20) ? 256 : 512;
     h->flat_ip_vec = 2;
     h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
     // nt unless the stream's working set fits the 256 MiB Infinity Cache: the window in
@@ -755,7 +759,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     if (const char* knob = ab_knob("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
     if (const char* knob = ab_knob("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
     h->flat_db_wg = ab_int("PMENV_FLAT_DB_WG", 1) != 0;
-    h->flat_ip_block = ab_int("PMENV_FLAT_IP_BLOCK", 512);
+    h->flat_ip_block = ab_int("PMENV_FLAT_IP_BLOCK", h->flat_ip_block);
     h->flat_ip_vec = ab_int("PMENV_FLAT_IP_VEC", 2);
     {   // the launcher's (block, vec) table: anything else takes the default 512 x 2
         const int key = h->flat_ip_block * 10 + h->flat_ip_vec;

@@ -113,8 +113,8 @@ def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
         args = [a.strip() for a in k[k.index("<") + 1:-1].split(",")]
         name = k[:k.index("<")]
         assert "s80" not in name and "nocap" not in name, k
-        if name == "advance_flat_inplace_kernel":
-            assert args == ["512", "2", args[2], "0"] and args[2] in ("0", "1"), k   # 512 x 2, no SKIP bits
+        if name == "advance_flat_inplace_kernel":                                   # 512 x 2 / 256 x 2, no SKIP bits
+            assert args in (["512", "2", "0", "0"], ["512", "2", "1", "0"], ["256", "2", "0", "0"]), k
         if name == "step_env_kernel":
             assert args[0] == "4" and args[3] == "0", k                             # V = 4, ABL = 0
         if name == "advance_rows_kernel":
