@@ -26,13 +26,14 @@ def _t(x, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
 
 
-def replay_gpu(g, mode, host=False):
+def replay_gpu(g, mode, host=False, impl="auto"):
     """host=True: the reference's own call shape with CPU tensors (train/on_policy.py:59-67
-    hands the env host tensors); the env stages them through the GPU."""
+    hands the env host tensors); the env stages them through the GPU. impl: the advance
+    step's implementation (TradingEnv.set_step_impl)."""
     from pmenv import TradingEnv
     m = g["meta"]
     N, W, F, T = m["N"], m["W"], m["F"], m["T"]
-    env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True)
+    env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True, step_impl=impl)
     _t = (lambda x, dtype=torch.float32: torch.as_tensor(np.ascontiguousarray(x), dtype=dtype)) if host else \
         globals()["_t"]
     out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
@@ -63,6 +64,23 @@ def replay_gpu(g, mode, host=False):
 def test_gpu_matches_reference_goldens(name, mode):
     g = gu.load(name)
     out = replay_gpu(g, mode)
+    assert out["market_ok"]
+    compare(g, out)
+
+
+@pytest.mark.parametrize("name", gu.cases())
+@pytest.mark.parametrize("impl", ["flat", "one_launch", "two_launch"])
+def test_gpu_every_step_path_matches_reference_goldens(name, impl):
+    """The reference's recorded outputs replayed through each advance-step implementation
+    forced (AUTO takes one_launch at one env); shapes a path does not fit are skipped."""
+    from pmenv import TradingEnv
+    m = gu.load(name)["meta"]
+    try:
+        TradingEnv(num_envs=1, num_assets=m["N"], window=m["W"], features=m["F"], device=DEV, step_impl=impl)
+    except ValueError:
+        pytest.skip(f"{impl} does not fit N={m['N']} W={m['W']} F={m['F']}")
+    g = gu.load(name)
+    out = replay_gpu(g, "advance", impl=impl)
     assert out["market_ok"]
     compare(g, out)
 
