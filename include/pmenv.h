@@ -197,8 +197,11 @@ const char* pmenv_step_path(const pmenv* h);
  * halo of its tiles, both produced by the previous step: a caller that writes the state
  * blob (pmenv_create_in) or an in-place window outside this API must go through
  * pmenv_set_state / pmenv_reset before the next step (both re-prime them; so does every
- * other step path). A step enqueued while `stream` is being captured into a hipGraph
- * takes the two-launch path instead (the parity is a launch argument). */
+ * other step path). From the first FLAT step enqueued while `stream` is being captured
+ * into a hipGraph on, the handle sequences its FLAT steps on the device (a small
+ * flat_seq_kernel before each step_flat_kernel reads the parity and the snapshot's
+ * validity from device memory, so graph replays and eager calls interleave freely;
+ * pmenv_step_path then says "device-sequenced"). */
 typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,

@@ -80,6 +80,12 @@ struct StepParams {
     const float* halo_in;
     float* halo_out;
     uint32_t per4;         // 16-B chunks per env window
+    // device-sequenced flat step (hipGraph-safe; step_flat.h): null = the host chose the
+    // parity. Else seq = {D, C, V, pad, HOBS lo, HOBS hi}: D the parity the next step
+    // reads, C the parity of the step in flight, V = 1 when snapshot D mirrors the state,
+    // HOBS the window whose halo halo[D] holds; *_in / halo_in are parity 0, *_out /
+    // halo_out parity 1, swapped by the kernel when C == 1
+    int32_t* seq;
     FastDiv div_wf, div_f, div_w, div_units;
 };
 

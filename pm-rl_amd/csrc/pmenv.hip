@@ -100,6 +100,12 @@ struct pmenv {
     int par;              // parity of the snapshot / halo the next step reads
     bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
     const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
+    // device-sequenced form (hipGraph-safe): from the first flat step enqueued under
+    // stream capture on, every flat step is flat_seq_kernel + step_flat_kernel reading
+    // the parity and the validity from seq (device words) instead of the host fields above
+    bool device_seq;
+    int32_t* seq;         // {D, C, V, pad, HOBS lo, HOBS hi} (step_flat.h)
+    uint64_t snap_stride; // bytes between the two parities of the snapshot / halo
     int path;             // pmenv_step_path_kind
     // tools build only
     int fused;            // PMENV_FUSE_* bits: advance_rows_kernel<fused> (PMENV_FUSED)
@@ -520,7 +526,24 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
     const bool need_halo = !out && h->halo1_obs != p.obs;
-    if (!h->snap_ok || need_halo) {
+    if (h->device_seq) {
+        // parity 0 in *_in / halo_in, parity 1 in *_out / halo_out; the sequencer primes
+        // parity D if needed and publishes it, the kernel swaps when it is 1
+        p.sv_in = h->sv[0]; p.sk_in = h->sk[0]; p.sw_in = h->sw[0]; p.slc_in = h->slc[0];
+        p.sv_out = h->sv[1]; p.sk_out = h->sk[1]; p.sw_out = h->sw[1]; p.slc_out = h->slc[1];
+        p.halo_in = h->halo1[0];
+        p.halo_out = h->halo1[1];
+        p.seq = h->seq;
+        StepParams pp = p;
+        pp.sv_out = h->sv[0]; pp.sk_out = h->sk[0]; pp.sw_out = h->sw[0]; pp.slc_out = h->slc[0];
+        pp.halo = h->halo1[0];
+        pp.halo_wgs = h->halo1_wgs;
+        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
+        pp.halo_qtot = h->flat_qtot;
+        const int64_t work = (int64_t)h->cfg.num_envs * h->cfg.num_assets;
+        const unsigned g = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
+        flat_seq_kernel<<<g, 256, 0, stream>>>(pp, out ? 1 : 0, h->snap_stride);
+    } else if (!h->snap_ok || need_halo) {
         StepParams pp = p;
         pp.sv_out = h->sv[q]; pp.sk_out = h->sk[q]; pp.sw_out = h->sw[q]; pp.slc_out = h->slc[q];
         pp.halo = need_halo ? h->halo1[q] : nullptr;
@@ -531,10 +554,12 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
         const unsigned g = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
         flat_prime_kernel<<<g, 256, 0, stream>>>(pp);
     }
-    p.sv_in = h->sv[q]; p.sk_in = h->sk[q]; p.sw_in = h->sw[q]; p.slc_in = h->slc[q];
-    p.sv_out = h->sv[1 - q]; p.sk_out = h->sk[1 - q]; p.sw_out = h->sw[1 - q]; p.slc_out = h->slc[1 - q];
-    p.halo_in = h->halo1[q];
-    p.halo_out = h->halo1[1 - q];
+    if (!h->device_seq) {
+        p.sv_in = h->sv[q]; p.sk_in = h->sk[q]; p.sw_in = h->sw[q]; p.slc_in = h->slc[q];
+        p.sv_out = h->sv[1 - q]; p.sk_out = h->sk[1 - q]; p.sw_out = h->sw[1 - q]; p.slc_out = h->slc[1 - q];
+        p.halo_in = h->halo1[q];
+        p.halo_out = h->halo1[1 - q];
+    }
     const int pol = out ? h->flat_pol : h->flat_ip_pol;
     const unsigned grid = (h->flat_qtot + (uint32_t)(h->flat1_block * h->flat1_vec) - 1) /
                           (uint32_t)(h->flat1_block * h->flat1_vec);
@@ -570,13 +595,14 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
 
 // anything but step_flat_kernel that writes the state or a window leaves the snapshot
 // and the halo stale
-inline void flat1_invalidate(pmenv* h) {
+inline void flat1_invalidate(pmenv* h, hipStream_t stream) {
     h->snap_ok = false;
     h->halo1_obs = nullptr;
+    if (h->device_seq) (void)hipMemsetAsync(h->seq + 2, 0, 4, stream);   // V = 0 (a graph node under capture)
 }
 
-// the stream is being captured into a hipGraph: step_flat_kernel's parity is a launch
-// argument (frozen under replay), so a captured step takes another path
+// the stream is being captured into a hipGraph: step_flat_kernel's host-chosen parity
+// would be frozen under replay, so the handle switches to the device-sequenced form
 bool capturing(hipStream_t stream) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
@@ -939,7 +965,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const uint32_t wgs = (h->flat_qtot + cpw - 1) / cpw;
         h->halo1_wgs = wgs > 0 ? wgs - 1 : 0;
         const size_t hal = up16(((size_t)h->halo1_wgs + 1) * 32);
-        hipError_t ae = hipMalloc(&h->snap, 2 * (one + hal));
+        hipError_t ae = hipMalloc(&h->snap, 2 * (one + hal) + 64);
         if (ae != hipSuccess) {
             set_err(h, "hipMalloc(snapshot) failed: %s", hipGetErrorString(ae));
             h->snap = nullptr;
@@ -953,8 +979,14 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             h->slc[q] = (float*)(sb + up16(B * 8) + up16(B * 4) + up16(BN * 4));
             h->halo1[q] = (float*)(sb + one);
         }
+        h->snap_stride = one + hal;
+        h->seq = (int32_t*)((char*)h->snap + 2 * (one + hal));
+        if (hipMemset(h->seq, 0, 64) != hipSuccess) {
+            set_err(h, "hipMemset(seq) failed");
+            return fail(PMENV_ERR_HIP);
+        }
     }
-    flat1_invalidate(h);
+    flat1_invalidate(h, nullptr);
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
     h->sa = (double*)(base + off[1]);
@@ -1024,7 +1056,7 @@ int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
     if (obs && !aligned4(obs)) { set_err(h, "obs not 4-byte aligned"); return PMENV_ERR_ALIGN; }
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
-    flat1_invalidate(h);
+    flat1_invalidate(h, stream);
     reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, obs, mask);
     return check_launch(h, "reset_kernel");
 }
@@ -1061,14 +1093,17 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     const int B = h->cfg.num_envs;
     const bool obs16 = (((uintptr_t)a->obs | (uintptr_t)p.obs_out) & 15u) == 0;
     const int fuse_bit = p.obs_out == p.obs ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-    if (a->bar && h->streaming && obs16 && (h->flat1 & fuse_bit) && !capturing(stream)) {
+    if (a->bar && h->streaming && obs16 && (h->flat1 & fuse_bit)) {
         // one launch over the flat stream: the whole step runs in the scalar phase
         const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
         if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
+        // a step captured into a hipGraph replays with frozen arguments: from then on this
+        // handle sequences its flat steps on the device (flat_seq_kernel + the kernel)
+        if (!h->device_seq && capturing(stream)) h->device_seq = true;
         launch_flat1(h, p, stream);
         return check_launch(h, "step_flat_kernel");
     }
-    flat1_invalidate(h);             // every other path writes the state without the snapshot
+    flat1_invalidate(h, stream);     // every other path writes the state without the snapshot
     if (!a->bar) {
         if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
         step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
@@ -1127,7 +1162,7 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* db2 = h->flat ? (h->flat_db_wg ? "advance_flat_wg_kernel" : "advance_flat_kernel")
                     : "advance_rows_kernel";
     const char* ip2 = h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
-    static thread_local char buf[2][128], out[288];
+    static thread_local char buf[2][128], out[320];
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
@@ -1139,7 +1174,8 @@ const char* pmenv_step_path(const pmenv* h) {
             part[m] = buf[m];
         }
     }
-    snprintf(out, sizeof out, "%s (obs_out) | %s (in place)", part[0], part[1]);
+    snprintf(out, sizeof out, "%s (obs_out) | %s (in place)%s", part[0], part[1],
+             h->device_seq && h->flat1 ? " [flat steps device-sequenced]" : "");
     return out;
 }
 
@@ -1154,7 +1190,7 @@ int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
 int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
     if (!h || !src) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
-    flat1_invalidate(h);
+    flat1_invalidate(h, stream);
     hipError_t e = hipMemcpyAsync(h->state, src, h->state_bytes, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) { set_err(h, "set_state: %s", hipGetErrorString(e)); return PMENV_ERR_HIP; }
     return PMENV_OK;

@@ -32,8 +32,10 @@
 // stored into the halo buffer of parity 1 - p. After anything else touched the state or
 // the window (reset, set_state, another step path, a different obs), the host primes
 // the snapshot and the halo from the canonical state and the window (flat_prime_kernel)
-// before the step. Under hipGraph capture the host takes another path (the parity is a
-// launch argument, frozen under replay).
+// before the step. Under hipGraph capture the host-chosen parity would be frozen: from the
+// first captured step on, the handle runs flat_seq_kernel before each step, which reads
+// the parity and the snapshot's validity from device words and primes on the device; the
+// kernel then reads the parity from memory (below).
 #pragma once
 #include "env_step.h"
 
@@ -169,9 +171,69 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void st
         const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = tile & 7, i = tile >> 3;
         tile = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
     }
+    if (p.seq) {
+        // device-sequenced step: the parity C that flat_seq_kernel published (nothing
+        // writes C during this launch); workgroup 0 publishes the next step's D, V and
+        // HOBS (nothing reads them during this launch)
+        const int c = __builtin_amdgcn_readfirstlane(p.seq[1]);
+        if (c) {
+            const double* v = p.sv_in; p.sv_in = p.sv_out; p.sv_out = const_cast<double*>(v);
+            const int32_t* k = p.sk_in; p.sk_in = p.sk_out; p.sk_out = const_cast<int32_t*>(k);
+            const float* w = p.sw_in; p.sw_in = p.sw_out; p.sw_out = const_cast<float*>(w);
+            const float* l = p.slc_in; p.slc_in = p.slc_out; p.slc_out = const_cast<float*>(l);
+            const float* h = p.halo_in; p.halo_in = p.halo_out; p.halo_out = const_cast<float*>(h);
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint64_t hobs = OUT ? 0ull : (uint64_t)(uintptr_t)p.obs;
+            p.seq[0] = 1 - c;
+            p.seq[2] = 1;
+            p.seq[4] = (int32_t)(uint32_t)hobs;
+            p.seq[5] = (int32_t)(uint32_t)(hobs >> 32);
+        }
+    }
     FlatTile<V> t;
     flat1_load<BLOCK, V, POL, OUT>(p, qtot, tile, t);
     flat1_process<BLOCK, V, POL, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
+}
+
+// The device-sequenced form's first node (hipGraph-safe: every decision is read from
+// device memory, none is a launch argument): reads D, V and HOBS (nothing writes them
+// during this launch), re-primes the snapshot of parity D from the canonical state when
+// V == 0 and — in place — the halo of parity D from the window when HOBS is not this
+// step's window, and publishes C = D for the flat kernel (which reads nothing else of
+// seq). *_out / halo point at parity 0, the kernel adds parity D's offset (`stride`
+// bytes between the parities).
+__global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, uint64_t stride) {
+    const int d = __builtin_amdgcn_readfirstlane(p.seq[0]);
+    const int valid = __builtin_amdgcn_readfirstlane(p.seq[2]);
+    const uint64_t hobs = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(p.seq[4]) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(p.seq[5]) << 32);
+    const bool snap = !valid;
+    const bool halo = !out && (!valid || hobs != (uint64_t)(uintptr_t)p.obs);
+    if (snap || halo) {
+        const uint64_t off = d ? stride : 0ull;
+        StepParams q = p;
+        q.sv_out = (double*)((char*)p.sv_out + off);
+        q.sk_out = (int32_t*)((char*)p.sk_out + off);
+        q.sw_out = (float*)((char*)p.sw_out + off);
+        q.slc_out = (float*)((char*)p.slc_out + off);
+        q.halo = halo ? (float*)((char*)p.halo + off) : nullptr;
+        copy_halo(q);
+        if (snap) {
+            const uint32_t nthr = gridDim.x * blockDim.x;
+            const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+            const size_t BN = (size_t)p.B * p.N;
+            for (size_t i = tid; i < (size_t)p.B; i += nthr) {
+                q.sv_out[i] = p.value[i];
+                q.sk_out[i] = p.k[i];
+            }
+            for (size_t i = tid; i < BN; i += nthr) {
+                q.sw_out[i] = p.w_new[i];
+                q.slc_out[i] = p.last_close[i];
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.seq[1] = d;
 }
 
 // Prime the snapshot (parity p) from the canonical state and, in place, the halo of

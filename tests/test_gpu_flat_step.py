@@ -138,40 +138,83 @@ def test_gpu_flat_masked_reset_same_mask():
         _same(_state(envs[0]), _state(envs[1]), f"step {t}")
 
 
-def test_gpu_flat_graph_capture_takes_another_path():
-    """A step captured into a hipGraph cannot carry the flat step's per-step parity; the
-    captured step takes the two-launch path, and replays equal the eager flat step."""
+def test_gpu_flat_graph_capture_and_replay():
+    """Flat steps captured into a hipGraph (an odd count, so a host-chosen parity would
+    go wrong on the second replay): the handle switches to the device-sequenced form and
+    graph replays interleave with eager steps, a full reset, a masked reset and a
+    checkpoint restore — every reward, value and window equal to an eager two-launch env
+    on the same inputs, bit for bit."""
     import ctypes
     from pmenv import TradingEnv, synth, _abi
-    B, N, W, T = 2048, 30, 50, 6
-    ser = synth.series(W + T, B, N, device=DEV)
-    act = synth.actions(T, B, N, device=DEV)
+    B, N, W, T, D = 2048, 30, 50, 5, 48
+    ser = synth.series(W + D, B, N, seed=7, device=DEV)
+    act = synth.actions(D, B, N, seed=8, device=DEV)
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
     obs_a = synth.window_from_series(ser, W)
     obs_b = obs_a.clone()
-    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
-    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
     ea.reset(obs_a)
     eb.reset(obs_b)
-    torch.cuda.synchronize()
+    day = 0
+
+    def eager(n):
+        nonlocal day
+        for _ in range(n):
+            ra, _ = ea.step(act[day], obs_a, bar=ser[W + day])
+            rb, _ = eb.step(act[day], obs_b, bar=ser[W + day])
+            assert torch.equal(ra, rb) and torch.equal(obs_a, obs_b), f"eager day {day}"
+            day += 1
+
+    eager(3)                                               # host-sequenced flat steps first
     lib = _abi.load()
-    rew = torch.empty(T, B, device=DEV)
+    act_buf = torch.empty(T, B, N, device=DEV)
+    bar_buf = torch.empty(T, B, N, 4, device=DEV)
+    rew_b = torch.empty(T, B, device=DEV)
+    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         for t in range(T):
-            _abi.check(lib.pmenv_step(eb._h, ctypes.c_void_p(act[t].data_ptr()), None,
-                                      ctypes.c_void_p(ser[W + t].data_ptr()), ctypes.c_void_p(obs_b.data_ptr()),
-                                      ctypes.c_void_p(rew[t].data_ptr()), s), eb._h)
-    obs_b.copy_(synth.window_from_series(ser, W))
-    eb.reset(obs_b)
-    g.replay()
-    ref = torch.stack([ea.step(act[t], obs_a, bar=ser[W + t])[0] for t in range(T)])
-    torch.cuda.synchronize()
-    assert torch.equal(ref, rew) and torch.equal(obs_a, obs_b)
-    # and the eager flat step after the replay re-primes from the graph's state
-    ra, _ = ea.step(act[0], obs_a, bar=ser[W])
-    rb, _ = eb.step(act[0], obs_b, bar=ser[W])
-    assert torch.equal(ra, rb) and torch.equal(obs_a, obs_b)
+            _abi.check(lib.pmenv_step(eb._h, ctypes.c_void_p(act_buf[t].data_ptr()), None,
+                                      ctypes.c_void_p(bar_buf[t].data_ptr()), ctypes.c_void_p(obs_b.data_ptr()),
+                                      ctypes.c_void_p(rew_b[t].data_ptr()), s), eb._h)
+    assert "device-sequenced" in eb.step_path
+
+    def replay():
+        nonlocal day
+        act_buf.copy_(act[day:day + T])
+        bar_buf.copy_(ser[W + day:W + day + T])
+        g.replay()
+        ref = torch.stack([ea.step(act[day + t], obs_a, bar=ser[W + day + t])[0] for t in range(T)])
+        torch.cuda.synchronize()
+        assert torch.equal(ref, rew_b), f"replay from day {day}: rewards"
+        assert torch.equal(obs_a, obs_b) and torch.equal(ea.value, eb.value), f"replay from day {day}"
+        day += T
+
+    replay()
+    replay()                                               # the same graph: parity from the device
+    eager(2)                                               # eager, device-sequenced
+    replay()
+    fresh = synth.window_from_series(ser[day:day + W + 1].contiguous(), W)
+    obs_a.copy_(fresh)
+    obs_b.copy_(fresh)
+    ea.reset(obs_a)
+    eb.reset(obs_b)                                        # invalidates on the device
+    replay()
+    mask = torch.rand(B, device=DEV, generator=torch.Generator(DEV).manual_seed(1)) < 0.3
+    ea.reset(obs_a, mask=mask)
+    eb.reset(obs_b, mask=mask)
+    eager(1)
+    ck_a, ck_b, ck_obs = ea.state_dict(), eb.state_dict(), obs_a.clone()
+    replay()
+    ea.load_state_dict(ck_a)
+    eb.load_state_dict(ck_b)
+    obs_a.copy_(ck_obs)
+    obs_b.copy_(ck_obs)
+    day -= T
+    replay()                                               # from the restored checkpoint
+    eager(2)
+    assert day <= D
 
 
 def test_gpu_flat_path_rules():
