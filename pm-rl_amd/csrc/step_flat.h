@@ -196,6 +196,24 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void st
     flat1_process<BLOCK, V, POL, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
 }
 
+// The snapshot copy (sv_out .. slc_out <- the canonical state, when `snap`) and the halo
+// copy (copy_halo, when p.halo is set), grid-stride over the launch.
+__device__ __forceinline__ void flat_prime(const StepParams& p, bool snap) {
+    copy_halo(p);
+    if (!snap) return;
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t BN = (size_t)p.B * p.N;
+    for (size_t i = tid; i < (size_t)p.B; i += nthr) {
+        p.sv_out[i] = p.value[i];
+        p.sk_out[i] = p.k[i];
+    }
+    for (size_t i = tid; i < BN; i += nthr) {
+        p.sw_out[i] = p.w_new[i];
+        p.slc_out[i] = p.last_close[i];
+    }
+}
+
 // The device-sequenced form's first node (hipGraph-safe: every decision is read from
 // device memory, none is a launch argument): reads D, V and HOBS (nothing writes them
 // during this launch), re-primes the snapshot of parity D from the canonical state when
@@ -218,39 +236,13 @@ __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, ui
         q.sw_out = (float*)((char*)p.sw_out + off);
         q.slc_out = (float*)((char*)p.slc_out + off);
         q.halo = halo ? (float*)((char*)p.halo + off) : nullptr;
-        copy_halo(q);
-        if (snap) {
-            const uint32_t nthr = gridDim.x * blockDim.x;
-            const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-            const size_t BN = (size_t)p.B * p.N;
-            for (size_t i = tid; i < (size_t)p.B; i += nthr) {
-                q.sv_out[i] = p.value[i];
-                q.sk_out[i] = p.k[i];
-            }
-            for (size_t i = tid; i < BN; i += nthr) {
-                q.sw_out[i] = p.w_new[i];
-                q.slc_out[i] = p.last_close[i];
-            }
-        }
+        flat_prime(q, snap);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) p.seq[1] = d;
 }
 
 // Prime the snapshot (parity p) from the canonical state and, in place, the halo of
 // parity p from the window: halo[i] = chunks (i+1)*CPW and (i+1)*CPW + 1 (copy_halo).
-__global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) {
-    copy_halo(p);
-    const uint32_t nthr = gridDim.x * blockDim.x;
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t BN = (size_t)p.B * p.N;
-    for (size_t i = tid; i < (size_t)p.B; i += nthr) {
-        p.sv_out[i] = p.value[i];
-        p.sk_out[i] = p.k[i];
-    }
-    for (size_t i = tid; i < BN; i += nthr) {
-        p.sw_out[i] = p.w_new[i];
-        p.slc_out[i] = p.last_close[i];
-    }
-}
+__global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) { flat_prime(p, true); }
 
 }  // namespace pmenv_dev
