@@ -273,3 +273,51 @@ def test_gpu_flat_full_size_properties():
     np.testing.assert_allclose(env.value[:S].cpu().numpy(), cenv.value, rtol=1e-12)
     assert np.array_equal(obs[:S, ..., :4].cpu().numpy(), cobs[..., :4])
     np.testing.assert_allclose(obs[:S, ..., 4].cpu().numpy(), cobs[..., 4], rtol=2e-7, atol=1e-12)
+
+
+def test_gpu_flat_long_run_bitwise_at_baseline_size():
+    """400 steps at the BASELINE shape (65,536 envs x 30 x 50) on a resident series, the
+    flat one-launch step against the two-launch path: in place with a double-buffered
+    step every 7th day and masked resets (a fifth of the envs, fresh windows) every 50
+    days; windows, rewards, values and counters compared bit for bit every 20 steps and
+    at the end. A rare ordering fault in the snapshot / halo sequencing would surface
+    here."""
+    from pmenv import TradingEnv, MarketSeries
+    B, N, W, T = 65536, 30, 50, 400
+    rng = np.random.default_rng(11)
+    days = W + T + 64
+    closes = 100 * np.exp(np.cumsum(0.01 * rng.standard_normal((days, N)), axis=0))
+    bars = np.stack([closes * np.exp(0.002 * rng.standard_normal((days, N))) for _ in range(3)] + [closes], -1)
+    m = MarketSeries(bars.astype(np.float32), device=DEV)
+    g = torch.Generator().manual_seed(5)
+    start = m.random_starts(B, W, T, generator=g)
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
+    obs = [m.initial_window(start, W) for _ in envs]
+    spare = [torch.empty_like(obs[0]) for _ in envs]
+    for e, o in zip(envs, obs):
+        e.reset(o)
+    day = start.clone()
+    gd = torch.Generator(DEV).manual_seed(6)
+    for t in range(T):
+        a = torch.softmax(torch.randn(B, N, device=DEV, generator=gd), -1)
+        d = day + W + t
+        if t and t % 50 == 0:
+            mask = torch.rand(B, device=DEV, generator=gd) < 0.2
+            fresh = m.initial_window(torch.where(mask, start, d - W).to(torch.int32), W)
+            for i, e in enumerate(envs):
+                obs[i][mask] = fresh[mask]
+                e.reset(obs[i], mask=mask)
+        rs = []
+        for i, e in enumerate(envs):
+            if t % 7 == 3:
+                r, nxt = e.step(a, obs[i], series=m, day=d, out=spare[i])
+                obs[i], spare[i] = nxt, obs[i]
+            else:
+                r, _ = e.step(a, obs[i], series=m, day=d)
+            rs.append(r)
+        assert torch.equal(rs[0], rs[1]), f"step {t}: rewards"
+        if t % 20 == 19 or t == T - 1:
+            assert torch.equal(obs[0], obs[1]), f"step {t}: windows"
+            assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
+            assert torch.equal(envs[0]._counter, envs[1]._counter), f"step {t}: counters"
+    assert envs[0].nonfinite_count() == 0
