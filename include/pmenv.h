@@ -155,7 +155,10 @@ typedef struct pmenv_step_args {
     uint32_t phases;       /* 0 = whole step; PMENV_PHASE_SCALAR / PMENV_PHASE_ADVANCE run
                               one launch of the two-launch advance path (the advance
                               phase must follow the scalar phase of the same step;
-                              used to time the streaming kernel on its own)          */
+                              used to time the streaming kernel on its own). Where the
+                              step is one launch (step_flat_kernel, step_env_kernel)
+                              the scalar phase runs all of it, the advance phase
+                              nothing                                                 */
 } pmenv_step_args;
 
 #define PMENV_PHASE_SCALAR 1u
