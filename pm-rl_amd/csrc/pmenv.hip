@@ -595,10 +595,17 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
 
 // anything but step_flat_kernel that writes the state or a window leaves the snapshot
 // and the halo stale
-inline void flat1_invalidate(pmenv* h, hipStream_t stream) {
+int flat1_invalidate(pmenv* h, hipStream_t stream) {
     h->snap_ok = false;
     h->halo1_obs = nullptr;
-    if (h->device_seq) (void)hipMemsetAsync(h->seq + 2, 0, 4, stream);   // V = 0 (a graph node under capture)
+    if (h->device_seq) {                       // V = 0 (a graph node under capture)
+        const hipError_t e = hipMemsetAsync(h->seq + 2, 0, 4, stream);
+        if (e != hipSuccess) {
+            set_err(h, "invalidating the flat step's snapshot: %s", hipGetErrorString(e));
+            return PMENV_ERR_HIP;
+        }
+    }
+    return PMENV_OK;
 }
 
 // the stream is being captured into a hipGraph: step_flat_kernel's host-chosen parity
@@ -986,7 +993,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             return fail(PMENV_ERR_HIP);
         }
     }
-    flat1_invalidate(h, nullptr);
+    (void)flat1_invalidate(h, nullptr);      // host flags only: no device sequencing yet
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
     h->sa = (double*)(base + off[1]);
@@ -1056,7 +1063,7 @@ int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
     if (obs && !aligned4(obs)) { set_err(h, "obs not 4-byte aligned"); return PMENV_ERR_ALIGN; }
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
-    flat1_invalidate(h, stream);
+    if (const int rc = flat1_invalidate(h, stream)) return rc;
     reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, obs, mask);
     return check_launch(h, "reset_kernel");
 }
@@ -1103,7 +1110,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         launch_flat1(h, p, stream);
         return check_launch(h, "step_flat_kernel");
     }
-    flat1_invalidate(h, stream);     // every other path writes the state without the snapshot
+    if (const int rc = flat1_invalidate(h, stream)) return rc;   // every other path skips the snapshot
     if (!a->bar) {
         if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
         step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
@@ -1190,7 +1197,7 @@ int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
 int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
     if (!h || !src) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
-    flat1_invalidate(h, stream);
+    if (const int rc = flat1_invalidate(h, stream)) return rc;
     hipError_t e = hipMemcpyAsync(h->state, src, h->state_bytes, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) { set_err(h, "set_state: %s", hipGetErrorString(e)); return PMENV_ERR_HIP; }
     return PMENV_OK;

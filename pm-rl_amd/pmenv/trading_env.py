@@ -316,8 +316,8 @@ class TradingEnv:
 
     def load_state_dict(self, sd):
         st = sd["state"]
-        if st.numel() != self._state.numel():
-            raise ValueError("state blob size mismatch (different env shape)")
+        if st.dtype != torch.uint8 or st.numel() != self._state.numel():
+            raise ValueError("state blob mismatch (a uint8 blob of this env shape's size expected)")
         # through pmenv_set_state: the handle re-primes what it derives from the state
         src = st.to(device=self.device, dtype=torch.uint8).contiguous()
         _abi.check(self._lib.pmenv_set_state(self._h, _ptr(src), self._stream()), self._h, "pmenv_set_state")
