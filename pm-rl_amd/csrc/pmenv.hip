@@ -97,6 +97,7 @@ struct pmenv {
     uint32_t halo1_wgs;
     int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread (tools: PMENV_FLAT1_GEOM)
     bool flat1_xcd;               // tools: XCD-contiguous tile ranges (PMENV_FLAT1_XCD)
+    int flat1_pol;                // tools: 3 = nt loads only, 4 = nt stores only (PMENV_FLAT1_POL)
     int par;              // parity of the snapshot / halo the next step reads
     bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
     const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
@@ -573,7 +574,16 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     }
     const int key = h->flat1_block * 100 + h->flat1_vec;
 #ifdef PMENV_AB
-    if (key == 25604 && h->flat1_xcd) {
+    if (key == 25604 && (h->flat1_pol == 3 || h->flat1_pol == 4)) {   // split load / store policies
+        if (h->flat1_pol == 3) {
+            if (out) step_flat_kernel<256, 4, 3, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+            else step_flat_kernel<256, 4, 3, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        } else {
+            if (out) step_flat_kernel<256, 4, 4, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+            else step_flat_kernel<256, 4, 4, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        }
+    }
+    else if (key == 25604 && h->flat1_xcd) {
         if (out) step_flat_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
         else step_flat_kernel<256, 4, 1, false, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
     }
@@ -903,6 +913,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->one_auto = h->flat1_auto ? 0 : one_auto_base;
     }
     h->flat1_xcd = ab_int("PMENV_FLAT1_XCD", 0) != 0;
+    h->flat1_pol = ab_int("PMENV_FLAT1_POL", 0);
     if (const char* knob = ab_knob("PMENV_FLAT1_GEOM")) {   // "512x2" | "512x4" | "1024x2" | "256x8" | ...
         int bk = 0, vv = 0;
         if (sscanf(knob, "%dx%d", &bk, &vv) == 2) {

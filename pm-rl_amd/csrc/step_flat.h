@@ -76,7 +76,7 @@ struct FlatTile {
 
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, uint32_t tile, FlatTile<V>& t) {
-    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int kAux = (POL == 1 || POL == 3) ? 2 : 0;          // window loads: nt for POL 1, 3
     constexpr int CPW = BLOCK * V;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     t.c0 = tile * (uint32_t)CPW;
@@ -99,7 +99,7 @@ __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, u
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot, uint32_t tile, const FlatTile<V>& t,
                                               f4* sh4, f4 (*sh_bar)[64], float (*sh_wp)[64], int32_t* sh_k) {
-    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int kAux = (POL == 1 || POL == 4) ? 2 : 0;          // window stores: nt for POL 1, 4
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t per4 = p.per4;
@@ -154,7 +154,8 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
     }
 }
 
-// POL: cache policy of the window stream (0 default, 1 nt); OUT: double-buffered (the
+// POL: cache policy of the window stream (0 default, 1 nt; tools A/B: 3 nt loads only,
+// 4 nt stores only); OUT: double-buffered (the
 // two chunks past a tile are read straight from obs, no halo). BLOCK x V: 256 x 4 (env
 // windows of >= 511 chunks) or 512 x 2 (148 .. 510), host-chosen. Held to 80 SGPRs where
 // the compiler can (512 x 2: 8 waves per SIMD instead of 7).
