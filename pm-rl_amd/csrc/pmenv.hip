@@ -97,7 +97,7 @@ struct pmenv {
     uint32_t halo1_wgs;
     int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread (tools: PMENV_FLAT1_GEOM)
     bool flat1_xcd;               // tools: XCD-contiguous tile ranges (PMENV_FLAT1_XCD)
-    int flat1_pol;                // tools: 3 = nt loads only, 4 = nt stores only (PMENV_FLAT1_POL)
+    int flat1_pol;                // tools: 3 nt loads only, 4 nt stores only, 5 sc0 nt, 6 sc1 nt, 7 nt loads + sc1 nt stores
     int par;              // parity of the snapshot / halo the next step reads
     bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
     const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
@@ -574,14 +574,14 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     }
     const int key = h->flat1_block * 100 + h->flat1_vec;
 #ifdef PMENV_AB
-    if (key == 25604 && (h->flat1_pol == 3 || h->flat1_pol == 4)) {   // split load / store policies
-        if (h->flat1_pol == 3) {
-            if (out) step_flat_kernel<256, 4, 3, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-            else step_flat_kernel<256, 4, 3, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-        } else {
-            if (out) step_flat_kernel<256, 4, 4, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-            else step_flat_kernel<256, 4, 4, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+    if (key == 25604 && h->flat1_pol >= 3 && h->flat1_pol <= 7) {   // other cache policies
+#define PMENV_FLAT1_POLV(PV)                                                                      \
+        if (h->flat1_pol == PV) {                                                                 \
+            if (out) step_flat_kernel<256, 4, PV, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);  \
+            else step_flat_kernel<256, 4, PV, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);     \
         }
+        PMENV_FLAT1_POLV(3) PMENV_FLAT1_POLV(4) PMENV_FLAT1_POLV(5) PMENV_FLAT1_POLV(6) PMENV_FLAT1_POLV(7)
+#undef PMENV_FLAT1_POLV
     }
     else if (key == 25604 && h->flat1_xcd) {
         if (out) step_flat_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);

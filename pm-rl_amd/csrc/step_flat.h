@@ -76,7 +76,8 @@ struct FlatTile {
 
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, uint32_t tile, FlatTile<V>& t) {
-    constexpr int kAux = (POL == 1 || POL == 3) ? 2 : 0;          // window loads: nt for POL 1, 3
+    // window loads: nt for POL 1, 3 (tools A/B: 5 sc0 nt, 6 sc1 nt, 7 nt)
+    constexpr int kAux = (POL == 1 || POL == 3 || POL == 7) ? 2 : POL == 5 ? 3 : POL == 6 ? 18 : 0;
     constexpr int CPW = BLOCK * V;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     t.c0 = tile * (uint32_t)CPW;
@@ -99,7 +100,8 @@ __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, u
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot, uint32_t tile, const FlatTile<V>& t,
                                               f4* sh4, f4 (*sh_bar)[64], float (*sh_wp)[64], int32_t* sh_k) {
-    constexpr int kAux = (POL == 1 || POL == 4) ? 2 : 0;          // window stores: nt for POL 1, 4
+    // window stores: nt for POL 1, 4 (tools A/B: 5 sc0 nt, 6 and 7 sc1 nt)
+    constexpr int kAux = (POL == 1 || POL == 4) ? 2 : POL == 5 ? 3 : (POL == 6 || POL == 7) ? 18 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t per4 = p.per4;
