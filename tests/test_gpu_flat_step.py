@@ -321,3 +321,20 @@ def test_gpu_flat_long_run_bitwise_at_baseline_size():
             assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
             assert torch.equal(envs[0]._counter, envs[1]._counter), f"step {t}: counters"
     assert envs[0].nonfinite_count() == 0
+
+
+def test_gpu_flat_counts_a_nonfinite_env_once():
+    """An env whose tiles straddle several workgroups is still counted once when its reward
+    turns non-finite (only the owner writes the env's outputs), and its NaN stays in it."""
+    from pmenv import TradingEnv, synth
+    B, N, W = 37, 30, 50                                    # 1,875 chunks per env: 2-3 tiles each
+    ser = synth.series(W + 2, B, N, seed=3, device=DEV)
+    obs = synth.window_from_series(ser, W)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
+    env.reset(obs)
+    a = torch.full((B, N), 1.0 / N, device=DEV)
+    a[5, 7] = float("nan")
+    r, _ = env.step(a, obs, bar=ser[W])
+    assert env.nonfinite_count() == 1
+    assert torch.isnan(r[5]) and torch.isfinite(r[torch.arange(B, device=DEV) != 5]).all()
+    assert torch.isfinite(obs[torch.arange(B, device=DEV) != 5]).all()
