@@ -591,11 +591,11 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     else if (key == 102402) { PMENV_FLAT1_LAUNCH(1024, 2) }
     else if (key == 25608) { PMENV_FLAT1_LAUNCH(256, 8) }
     else if (key == 25602) { PMENV_FLAT1_LAUNCH(256, 2) }
-    else if (key == 12808) { PMENV_FLAT1_LAUNCH(128, 8) }
     else if (key == 12804) { PMENV_FLAT1_LAUNCH(128, 4) }
     else
 #endif
     if (key == 25604) { PMENV_FLAT1_LAUNCH(256, 4) }
+    else if (key == 12808) { PMENV_FLAT1_LAUNCH(128, 8) }
     else { PMENV_FLAT1_LAUNCH(512, 2) }
 #undef PMENV_FLAT1_LAUNCH
     h->par = 1 - q;
@@ -886,8 +886,16 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const uint32_t ne_max = h->per4 ? (cpw + h->per4 - 2u) / h->per4 + 1u : 0u;
         return flat_ok && c.num_assets <= 64 && ne_max <= (uint32_t)(block / 64);
     };
-    h->flat1_block = flat1_fits(256, 4) ? 256 : 512;
-    h->flat1_vec = h->flat1_block == 256 ? 4 : 2;
+    // 128 x 8 (2 waves, 8 chunks per lane, the same 16 KiB tiles) where every tile holds at
+    // most two envs (1,023 .. 1,999 chunks per env: N = 20 .. 39 at W = 50) and the window
+    // streams through HBM: 0.5-1.1 % ahead of 256 x 4 from 49,152 envs at N = 30 (65,536:
+    // 625.7 vs 629.4 and 628.8 vs 631.6 us; 98,304: 941.1 vs 951.6), N = 20 / 24 / 28 by
+    // 1.0 / 0.7 / 0.5 %; behind it at 16,384 envs (162.9 vs 161.4) and at N = 16 / 64
+    // (profiles/ab_r02/r02w_flat1k_*, r02w_flat1l_*, r02w_flat1c_*)
+    const bool band128 = h->per4 >= 1023u && h->per4 < 2000u && win > (1ll << 30);
+    if (band128 && flat1_fits(128, 8)) { h->flat1_block = 128; h->flat1_vec = 8; }
+    else if (flat1_fits(256, 4)) { h->flat1_block = 256; h->flat1_vec = 4; }
+    else { h->flat1_block = 512; h->flat1_vec = 2; }
     h->flat1_ok = flat1_fits(h->flat1_block, h->flat1_vec);
     // AUTO: above the one-launch-per-env windows (48 MiB) the flat step beats the two-launch
     // stream by 1-3.5 % for env windows of >= 1,000 chunks (N >= 16 at W = 50): 65,536 x 30
@@ -902,7 +910,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->flat1_auto = 0;
     const int one_auto_base = h->one_auto;   // tools: PMENV_FLAT1=0 restores it
     (void)one_auto_base;
-    if (h->flat1_ok && h->flat1_block == 256 && h->per4 >= 1000u && !(c.commission > 0.0)) {
+    if (h->flat1_ok && h->flat1_block <= 256 && h->per4 >= 1000u && !(c.commission > 0.0)) {
         if (win > (48ll << 20)) h->flat1_auto |= PMENV_FUSE_DB;
         if (win > (256ll << 20)) h->flat1_auto |= PMENV_FUSE_INPLACE;
         h->one_auto &= ~h->flat1_auto;
