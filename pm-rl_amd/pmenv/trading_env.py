@@ -27,6 +27,8 @@ import torch
 from . import _abi
 from .config import EnvConfig
 
+_CPU = torch.device("cpu")
+
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -121,6 +123,8 @@ class TradingEnv:
         self._last_close = s[off[6]:off[6] + 4 * B * N].view(torch.float32).view(B, N)
         self._w_new = s[off[7]:off[7] + 4 * B * N].view(torch.float32).view(B, N)
         self.weights = RingView(self)
+        self._obs_shape = (B, N, W, self.cfg.features)
+        self._args = _abi.PmenvStepArgs()          # reused: every field is set on every step
         self.track_info = track_info
         self._unbatched = False
         self._host_io = False               # the last reset/step came with CPU tensors
@@ -145,9 +149,9 @@ class TradingEnv:
 
     def _obs_check(self, features, name="features"):
         cfg = self.cfg
-        shape = (cfg.num_envs, cfg.num_assets, cfg.window, cfg.features)
+        shape = self._obs_shape
         if features.dtype != torch.float32 or not features.is_contiguous() or \
-                features.device not in (self.device, torch.device("cpu")):
+                features.device not in (self.device, _CPU):
             raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device} or the host "
                              "(written in place)")
         if tuple(features.shape) == shape:
@@ -162,6 +166,8 @@ class TradingEnv:
         B = self.cfg.num_envs
         if not torch.is_tensor(x):
             x = torch.as_tensor(x)
+        elif x.dtype == torch.float32 and x.device == self.device and x.is_contiguous() and x.numel() == B * per_env:
+            return x if x.dim() == 2 and x.shape[0] == B else x.view(B, per_env)   # the common case: as is
         if x.numel() != B * per_env:
             # weight_buffer.py:18-19 raises ValueError on a mis-shaped action
             raise ValueError(f"{name} must have {B} x {per_env} elements, got shape {tuple(x.shape)}")
@@ -268,7 +274,8 @@ class TradingEnv:
         elif p is None:
             raise ValueError("step needs prices (reference contract) or bar (fused window advance)")
         r = torch.empty(B, dtype=torch.float32, device=self.device)
-        args = _abi.PmenvStepArgs()
+        args = self._args
+        args.day, args.series_days, args.obs_out, args.ret, args.weights, args.phases = None, 0, None, None, None, 0
         args.action = a.data_ptr()
         args.prices = p.data_ptr() if p is not None else None
         args.bar = br.data_ptr() if br is not None else None
