@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 # (N, W, B): envs of 150 .. 3,760 chunks, i.e. 1 .. 8 envs per 1,024-chunk tile, rows
 # straddling chunks, envs at every offset in a tile, a partial last tile
 SHAPES = [(30, 50, 37), (4, 50, 600), (4, 30, 301), (12, 10, 97), (64, 47, 3), (8, 50, 11), (64, 16, 5),
-          (33, 20, 5), (2, 60, 130), (1, 600, 9)]
+          (33, 20, 5), (2, 60, 130), (1, 600, 9), (64, 2, 50), (40, 3, 21)]   # W = 2, 3: most days are last days
 
 
 def _mode_id(k):
