@@ -1514,6 +1514,39 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         reward_kind != PMENV_REWARD_SHARPE)
         return PMENV_ERR_ARG;
     if (norm < PMENV_BNORM_GLOBAL_OR || norm > PMENV_BNORM_NONE) return PMENV_ERR_ARG;
+    // one launch: the row blocks' partials and, in the block that finishes last, the
+    // final fold (batch_reward_fwd_*_kernel; the ticket it counts on is zeroed first)
+#ifdef PMENV_AB
+    // tools: the forward in one launch (batch_reward_fwd_*_kernel: the block that draws
+    // the last ticket folds the partials). Measured slower than the two launches below at
+    // every shape, so the product keeps the two.
+    if (ab_knob("PMENV_BR_ONE")) {
+        if (hipMemsetAsync(work + 6 * (size_t)B + 6, 0, sizeof(uint32_t), stream) != hipSuccess) return PMENV_ERR_HIP;
+        const bool quad = N <= kQuadMaxN;
+        const int nblk = quad ? (B + kQuadRows - 1) / kQuadRows : (int)batch_reward_blocks(B);
+        int grid = nblk, fence = 1;
+        if (const char* knob = ab_knob("PMENV_BR_GRID")) grid = std::max(1, std::min(nblk, atoi(knob)));
+        if (const char* knob = ab_knob("PMENV_BR_FENCE")) fence = atoi(knob);
+        const unsigned g = (unsigned)grid;
+#define PMENV_FWD_ARGS a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, nblk
+        if (quad) {
+            if (fence == 0) {
+                if (N <= 32) batch_reward_fwd_quad_kernel<8, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+                else batch_reward_fwd_quad_kernel<16, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+            } else if (N <= 32) batch_reward_fwd_quad_kernel<8, 1><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+            else batch_reward_fwd_quad_kernel<16, 1><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+        } else {
+            if (N <= 128) batch_reward_fwd_rows_kernel<2, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+            else if (N <= 256) batch_reward_fwd_rows_kernel<4, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+            else if (N <= 512) batch_reward_fwd_rows_kernel<8, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+            else batch_reward_fwd_rows_kernel<0, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
+        }
+#undef PMENV_FWD_ARGS
+        if (ret_out || N > kQuadMaxN)
+            batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+#endif
     int nparts;
     if (N <= kQuadMaxN) {         // a quad of lanes per row
         nparts = (B + kQuadRows - 1) / kQuadRows;

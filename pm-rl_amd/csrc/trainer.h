@@ -17,7 +17,8 @@ namespace pmenv_dev {
 
 // work layout (f64): [0,B) ret chosen, [B,2B) row sum, [2B,3B) row min, [3B,4B) ret raw,
 // [4B,5B) ret softmax, [5B,6B) row normalised flag, [6B..6B+8) globals:
-// +0 normalised (global), +1 mean, +2 std, +3 reward, +4 norm mode; then the partial
+// +0 normalised (global), +1 mean, +2 std, +3 reward, +4 norm mode, +6 the tools build's
+// one-launch forward's ticket (a u32, zeroed by the host before the launch); then the partial
 // records of the row blocks (kRowsPerBlock or kQuadRows rows each), field-major:
 // field i of block k at [6B+8 + i*nblocks + k].
 constexpr int kTrainBlock = 256;
@@ -53,10 +54,9 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
 // count, mean, M2 (two-pass inside the block) and the sum of f(ret) (log for the
 // log-return reward).
 template <int EPL>
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const float* a, const float* v_prev,
-                                                                        const float* p, int B, int N, int kind,
-                                                                        double* work) {
-    __shared__ double sh[4][kRowsPerBlock];       // row sum, row min, raw, softmax
+__device__ __forceinline__ void rows_wave_partial(const float* a, const float* v_prev, const float* p, int B, int N,
+                                                  int kind, double* work, double (*sh)[kRowsPerBlock], int blk,
+                                                  int nblk) {
     constexpr int RPW = kRowsPerBlock / 4;        // rows per wave
     constexpr int E = EPL > 0 ? EPL : 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
         const auto rsa = make_rsrc(a, bytes), rsp = make_rsrc(p, bytes);
 #pragma unroll
         for (int j = 0; j < RPW; ++j) {
-            const int b = blockIdx.x * kRowsPerBlock + wave * RPW + j;
+            const int b = blk * kRowsPerBlock + wave * RPW + j;
 #pragma unroll
             for (int k = 0; k < E; ++k) {
                 const int n = lane + 64 * k;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
     }
     for (int j = 0; j < RPW; ++j) {
         const int rl = wave * RPW + j;
-        const int b = blockIdx.x * kRowsPerBlock + rl;
+        const int b = blk * kRowsPerBlock + rl;
         if (b >= B) break;
         const double v = (double)v_prev[b];
         double s = 0.0, mn = INFINITY, mx = -INFINITY, raw = 0.0;
@@ -144,11 +144,11 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
         }
     }
     __syncthreads();
-    if (wave != 0) return;
-    const int b = blockIdx.x * kRowsPerBlock + lane;
+    if (wave != 0) return;                                          // (no barrier follows in this function)
+    const int b = blk * kRowsPerBlock + lane;
     const bool ok = lane < kRowsPerBlock && b < B;
-    const double cnt = (double)min(kRowsPerBlock, B - (int)blockIdx.x * kRowsPerBlock);
-    double* part = work + (size_t)6 * B + 8 + blockIdx.x;
+    const double cnt = (double)min(kRowsPerBlock, B - blk * kRowsPerBlock);
+    double* part = work + (size_t)6 * B + 8 + blk;
     const int li = ok ? lane : 0;
     const double rs = ok ? sh[0][li] : 0.0, rm = ok ? sh[1][li] : INFINITY;
     const double s_all = wave_sum(rs);
@@ -178,8 +178,16 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const fl
         double val = rec[0];
 #pragma unroll
         for (int i = 1; i < kPartStride; ++i) val = lane == i ? rec[i] : val;
-        part[(size_t)lane * gridDim.x] = val;                      // field-major: coalesced final fold
+        part[(size_t)lane * nblk] = val;                      // field-major: coalesced final fold
     }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const float* a, const float* v_prev,
+                                                                        const float* p, int B, int N, int kind,
+                                                                        double* work) {
+    __shared__ double sh[4][kRowsPerBlock];       // row sum, row min, raw, softmax
+    rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------- N <= 64: a quad per row
@@ -214,12 +222,11 @@ __device__ __forceinline__ RowQuad<EPL> load_row_quad(const float* a, const floa
 }
 
 template <int EPL>
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_quad_kernel(const float* a, const float* v_prev,
-                                                                             const float* p, int B, int N, int kind,
-                                                                             double* work) {
-    __shared__ double rec_w[4][kPartStride];
+__device__ __forceinline__ void rows_quad_partial(const float* a, const float* v_prev, const float* p, int B, int N,
+                                                  int kind, double* work, double (*rec_w)[kPartStride], int blk,
+                                                  int nblk) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid & 3;
-    const int r0 = blockIdx.x * kQuadRows;
+    const int r0 = blk * kQuadRows;
     const int nrows = min(kQuadRows, B - r0);
     const bool ok = (tid >> 2) < nrows;
     const int b = r0 + (ok ? tid >> 2 : 0);
@@ -305,8 +312,16 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_quad_kernel(con
             acc[6 + 4 * c] += r[6 + 4 * c];
         }
     }
-    double* part = work + (size_t)6 * B + 8 + blockIdx.x;        // field-major: coalesced final fold
-    for (int i = 0; i < kPartStride; ++i) part[(size_t)i * gridDim.x] = acc[i];
+    double* part = work + (size_t)6 * B + 8 + blk;        // field-major: coalesced final fold
+    for (int i = 0; i < kPartStride; ++i) part[(size_t)i * nblk] = acc[i];
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_quad_kernel(const float* a, const float* v_prev,
+                                                                             const float* p, int B, int N, int kind,
+                                                                             double* work) {
+    __shared__ double rec_w[4][kPartStride];
+    rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // backward, N <= 64, a quad per row: dR/da through the (optional) softmax. The
@@ -385,9 +400,8 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_grad_quad_kernel(con
 // single workgroup over the `nparts` block partials: the normalisation decision, the reward
 // and the chosen candidate's mean / std. Thread t folds partials t, t + 256, ... in
 // order, then a fixed-shape LDS tree folds the 256 threads: deterministic.
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, int kind, int norm, double scale,
-                                                                         double* work, float* reward_out,
-                                                                         int nparts) {
+__device__ __forceinline__ void final_fold(int B, int kind, int norm, double scale, double* work, float* reward_out,
+                                           int nparts) {
     __shared__ double sh[4][kPartStride];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t nblk = (size_t)nparts;
@@ -455,6 +469,75 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, 
     work[6 * (size_t)B + 4] = (double)norm;
     *reward_out = (float)R;
 }
+
+// the second launch of the forward: one workgroup folds the row blocks' partials
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, int kind, int norm, double scale,
+                                                                         double* work, float* reward_out,
+                                                                         int nparts) {
+    final_fold(B, kind, norm, scale, work, reward_out, nparts);
+}
+
+#ifdef PMENV_AB
+// ---------------------------------------------------------------- tools: the forward in one launch
+// The row blocks write their partials as above; then every block takes a ticket from a
+// device-scope counter (work[6B + 6], zeroed by the host before the launch), and the block
+// that draws the last ticket folds all partials with final_fold — the same code and
+// order as batch_reward_final_kernel, so both forms give the same bits. Release: the
+// partials' writers fence before the block barrier and the ticket; acquire: the last
+// block fences before reading the other blocks' partials (they live in other XCDs' L2).
+// No block waits for another: blocks that are not last simply exit. Measured: the
+// agent-scope fences (an L2 write-back per block) cost more than the second launch they
+// save, at every shape and grid tried — kept here as that evidence.
+__device__ __forceinline__ uint32_t* batch_reward_ticket(double* work, int B) {
+    return reinterpret_cast<uint32_t*>(work + 6 * (size_t)B + 6);
+}
+
+// FENCE 0: every thread fences its own stores; 1: only thread 0 (after the barrier that
+// orders the block's stores, all of which thread 0 made in the quad form)
+template <int FENCE>
+__device__ __forceinline__ bool drew_last_ticket(uint32_t* ticket) {
+    __shared__ uint32_t last;
+    if (FENCE == 0) __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (FENCE == 1) __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return false;
+    __threadfence();
+    return true;
+}
+
+// nblk row blocks over the grid (grid-stride: a block may produce several partials)
+template <int EPL, int FENCE>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(const float* a, const float* v_prev,
+                                                                            const float* p, int B, int N, int kind,
+                                                                            int norm, double scale, double* work,
+                                                                            float* reward_out, int nblk) {
+    __shared__ double rec_w[4][kPartStride];
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, blk, nblk);
+        __syncthreads();                                          // rec_w is reused
+    }
+    if (drew_last_ticket<FENCE>(batch_reward_ticket(work, B)))
+        final_fold(B, kind, norm, scale, work, reward_out, nblk);
+}
+
+template <int EPL, int FENCE>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(const float* a, const float* v_prev,
+                                                                            const float* p, int B, int N, int kind,
+                                                                            int norm, double scale, double* work,
+                                                                            float* reward_out, int nblk) {
+    __shared__ double sh[4][kRowsPerBlock];
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, blk, nblk);
+        __syncthreads();
+    }
+    if (drew_last_ticket<FENCE == 1 ? 0 : FENCE>(batch_reward_ticket(work, B)))   // several writer lanes
+        final_fold(B, kind, norm, scale, work, reward_out, nblk);
+}
+#endif
 
 // elementwise: each row's chosen return and normalisation flag (for the backward)
 __global__ __launch_bounds__(256) void batch_reward_select_kernel(int B, int norm, double* work, float* ret_out) {

@@ -88,3 +88,34 @@ def test_gpu_batch_reward_trains_like_reference_update():
     ref_loss.backward()
     opt.step()
     assert abs(float(loss) - float(ref_loss)) < 1e-6 and not torch.equal(w0, lin.weight)
+
+
+@pytest.mark.parametrize("B,N", [(65536, 30), (8192, 500), (3, 20)])
+def test_gpu_batch_reward_forward_is_deterministic(B, N):
+    """The forward folds per-block partials in a fixed order: repeated calls on one
+    workspace pre-filled with garbage give the same bits, and match the oracle."""
+    import ctypes
+    from pmenv import _abi
+    lib = _abi.load()
+    g = torch.Generator(device=DEV).manual_seed(B + N)
+    a = torch.randn(B, N, device=DEV, generator=g)
+    v = torch.rand(B, device=DEV, generator=g) + 1.0
+    p = 1.0 + 0.01 * torch.randn(B, N, device=DEV, generator=g)
+    work = torch.full((lib.pmenv_batch_reward_workspace(B) // 8,), float("nan"), dtype=torch.float64, device=DEV)
+    work.view(torch.int32)[::3] = 0x7ffffff3                  # garbage
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for kind in (0, 2):
+        for _ in range(5):
+            r = torch.empty((), device=DEV)
+            assert lib.pmenv_batch_reward_forward(P(a), P(v), P(p), B, N, kind, 0, 1.0, P(work), P(r), None, s) == 0
+            outs.append((kind, r.clone(), work[6 * B:6 * B + 5].clone()))
+    torch.cuda.synchronize()
+    for kind in (0, 2):
+        ref = [o for o in outs if o[0] == kind]
+        for o in ref[1:]:
+            assert torch.equal(o[1], ref[0][1]) and torch.equal(o[2], ref[0][2]), kind
+        R, _, _ = or_batch_reward(a.cpu().numpy(), v.cpu().numpy(), p.cpu().numpy(),
+                                  reward="log_returns" if kind == 0 else "sharpe_ratio", norm="global_or")
+        assert np.isclose(float(ref[0][1]), np.float32(R), rtol=1e-6, atol=1e-12), (kind, float(ref[0][1]), R)

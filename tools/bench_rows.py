@@ -110,7 +110,8 @@ def main():
             res.append(row("moments", us, n * 4, n=n))
 
     if "f2" in only:
-        # differentiable batched PG reward: forward (reward only) and backward
+        # differentiable batched PG reward: forward (reward only; the product's two launches
+        # and the tools build's one-launch forms under PMENV_BR_ONE, interleaved) and backward
         for B, N in ((65536, 30), (16384, 30), (4096, 30), (8192, 500)):
             act = torch.randn(B, N, device=dev, generator=g)
             vp = torch.rand(B, device=dev, generator=g) + 1.0
@@ -123,9 +124,32 @@ def main():
                                                             P(rout), None, st), "fwd")
             bwd = lambda: ck(lib.pmenv_batch_reward_backward(P(act), P(vp), P(p), B, N, 0, 1.0, P(work), P(go),  # noqa: E731
                                                              P(ga), st), "bwd")
-            fwd()
             f_bytes = B * N * 4 * 2 + B * 4
-            res.append(row("batch_reward_fwd", timeit(fwd, a.reps), f_bytes, B=B, N=N))
+            forms = {"two": {}, "one": {"PMENV_BR_ONE": "1"}, "one_fence_all": {"PMENV_BR_ONE": "1", "PMENV_BR_FENCE": "0"},
+                     "one_grid256": {"PMENV_BR_ONE": "1", "PMENV_BR_GRID": "256"},
+                     "one_grid512": {"PMENV_BR_ONE": "1", "PMENV_BR_GRID": "512"}}
+            knobs = ("PMENV_BR_ONE", "PMENV_BR_FENCE", "PMENV_BR_GRID")
+
+            def use(form):
+                for k in knobs:
+                    os.environ.pop(k, None)
+                os.environ.update(forms[form])
+            outs = {}
+            for form in forms:                          # the same bits every way
+                use(form)
+                fwd()
+                outs[form] = (rout.clone(), work[6 * B:6 * B + 5].clone())
+            same = all(torch.equal(outs[f][0], outs["two"][0]) and torch.equal(outs[f][1], outs["two"][1])
+                       for f in forms)
+            ts = {f: [] for f in forms}
+            for _ in range(3):
+                for form in forms:
+                    use(form)
+                    ts[form].append(timeit(fwd, a.reps))
+            use("two")
+            for form in forms:
+                res.append(row(f"batch_reward_fwd_{form}", statistics.median(ts[form]), f_bytes, B=B, N=N,
+                               same_bits=same))
             res.append(row("batch_reward_bwd", timeit(bwd, a.reps), f_bytes + B * N * 4, B=B, N=N))
 
     if "f3" in only or "f4" in only:
