@@ -1284,6 +1284,20 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     int E = ab_int("PMENV_GAE_E", 0);
     if (E != 1 && E != 2 && E != 4) E = 0;
     if (E && B % E) E = 0;
+    if (knob && !strcmp(knob, "tile8") && fits) {   // tools: the tile held to 64 VGPRs (8 waves per SIMD)
+        gae_tile_kernel<8, 8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+    if (knob && !strcmp(knob, "stream") && fits) {   // PMENV_GAE_P: days per block (16 or 32)
+        const unsigned g = (unsigned)((B + 63) / 64);
+        if (ab_int("PMENV_GAE_P", 16) == 32)
+            gae_stream_kernel<32><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+        else if (ab_int("PMENV_GAE_P", 16) == 8)
+            gae_stream_kernel<8><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+        else
+            gae_stream_kernel<16><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
     if (tile && E) {
         const unsigned g = (unsigned)((B + 64 * E - 1) / (64 * E));
 #define PMENV_GAEV(U_, E_) \
@@ -1297,7 +1311,14 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
     }
 #endif
-    if (tile && U == 16)
+    // many envs and at least four 64-day segments: the tile held to 64 VGPRs (8 waves per
+    // SIMD, so a 65,536-env rollout's 1,024 workgroups are resident at once; the same bits):
+    // 56.7 vs 58.5 us at 256 x 65,536, 110.1 vs 114.7 at 512 x 65,536; slower below 65,536
+    // envs or 256 days (profiles/ab_r02/gae_occ8_r02zl.json)
+    if (tile && U == 8 && B >= 65536 && T >= 256)
+        gae_tile_kernel<8, 8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                   lam);
+    else if (tile && U == 16)
         gae_tile_kernel<8, 16><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
                                                                  lam);
     else if (tile)

@@ -83,10 +83,10 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const flo
 // Loads are buffer loads with the lane's env as the (only) VGPR offset and the
 // wave-uniform row as the SGPR offset, so U rows in flight cost no address VGPRs.
 // Needs every array below 2 GiB (the host checks).
-template <int NW, int U>
-__global__ __launch_bounds__(64 * NW) void gae_tile_kernel(const float* r, const float* v, const uint8_t* dones,
-                                                          float* adv, float* ret, int T, int B, float gamma,
-                                                          float lam) {
+template <int NW, int U, int OCC = 1>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) void gae_tile_kernel(
+    const float* r, const float* v, const uint8_t* dones, float* adv, float* ret, int T, int B, float gamma,
+    float lam) {
     __shared__ double shC[NW][64], shD[NW][64];
     constexpr int S = NW * U;
     const int lane = threadIdx.x & 63;
@@ -121,20 +121,30 @@ __global__ __launch_bounds__(64 * NW) void gae_tile_kernel(const float* r, const
             const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
             alive |= (dn ? 0u : 1u) << u;
         }
-        double dl[U];                             // delta_t, kept for the second walk
+        // delta_t, kept for the second walk (OCC >= 8: recomputed there, the same bits, so
+        // the kernel fits 64 VGPRs)
+        constexpr bool RECOMP = OCC >= 8;
+        double dl[RECOMP ? 1 : U];
         double C = 1.0, D = 0.0;
 #pragma unroll
         for (int u = U - 1; u >= 0; --u) {
             const double n = (alive >> u) & 1u ? 1.0 : 0.0;
-            dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
+            const double d = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
+            if (!RECOMP) dl[u] = d;
             if (t0 + u < seg_end) {
-                D = dl[u] + gl * n * D;
+                D = d + gl * n * D;
                 C = gl * n * C;
             }
         }
         shC[w][lane] = C;
         shD[w][lane] = D;
         __syncthreads();
+        if (RECOMP) {                             // opaque to the optimiser: no delta stays live
+#pragma unroll
+            for (int u = 0; u < U; ++u) asm volatile("" : "+v"(rr[u]));
+#pragma unroll
+            for (int u = 0; u <= U; ++u) asm volatile("" : "+v"(vv[u]));
+        }
         double a = carry;
         for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
 #pragma unroll
@@ -142,7 +152,8 @@ __global__ __launch_bounds__(64 * NW) void gae_tile_kernel(const float* r, const
             const int t = t0 + u;
             if (t < seg_end) {
                 const double n = (alive >> u) & 1u ? 1.0 : 0.0;
-                a = dl[u] + gl * n * a;
+                const double d = RECOMP ? (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u] : dl[RECOMP ? 0 : u];
+                a = d + gl * n * a;
                 // lanes past B: voff is out of range for the store descriptors -> dropped
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret, voff_st,
@@ -151,6 +162,76 @@ __global__ __launch_bounds__(64 * NW) void gae_tile_kernel(const float* r, const
         }
         for (int j = NW - 1; j >= 0; --j) carry = shD[j][lane] + shC[j][lane] * carry;
         __syncthreads();                          // the LDS maps are rewritten next segment
+    }
+}
+
+// GAE as a pipelined per-env walk for many envs (B / 64 waves fill the SIMDs): one lane
+// per env, so a wave's rows are coalesced 256-B runs of the time-major rollout; the
+// horizon walked backwards in blocks of P days whose loads are issued one block ahead
+// (P rows of r, v and done in flight per wave while the previous block is consumed), no
+// LDS, no barrier, no second pass. The recursion is gae_kernel's, in f64.
+template <int P>
+__device__ __forceinline__ void gae_stream_load(__amdgpu_buffer_rsrc_t rs_r, __amdgpu_buffer_rsrc_t rs_v,
+                                                __amdgpu_buffer_rsrc_t rs_d, uint32_t voff, uint32_t row, int B,
+                                                int tb, float* rr, float* vv, uint32_t& alive) {
+    alive = 0;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+        const uint32_t t = (uint32_t)max(tb - P + u, 0);          // days before 0: row 0 again, unused
+        rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
+        vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
+        const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
+        alive |= (dn ? 0u : 1u) << u;
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void gae_stream_block(__amdgpu_buffer_rsrc_t rs_adv, __amdgpu_buffer_rsrc_t rs_ret,
+                                                 uint32_t voff_st, uint32_t row, int tb, const float* rr,
+                                                 const float* vv, uint32_t alive, double g, double gl, double& a,
+                                                 float& vnext) {
+#pragma unroll
+    for (int u = P - 1; u >= 0; --u) {
+        const int t = tb - P + u;
+        if (t >= 0) {
+            const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+            const double vt = (double)vv[u];
+            const double delta = (double)rr[u] + g * n * (double)vnext - vt;
+            a = delta + gl * n * a;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + vt)), rs_ret, voff_st, (uint32_t)t * row,
+                                                  0);
+            vnext = vv[u];
+        }
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const float* v, const uint8_t* dones,
+                                                       float* adv, float* ret, int T, int B, float gamma, float lam) {
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x * 64 + lane;
+    const bool ok = b < B;
+    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
+    const uint32_t row = (uint32_t)B * 4u;
+    const auto rs_r = make_rsrc(r, (uint32_t)T * row);
+    const auto rs_v = make_rsrc(v, (uint32_t)(T + 1) * row);
+    const auto rs_d = make_rsrc(dones ? (const void*)dones : (const void*)r, dones ? (uint32_t)T * (uint32_t)B : 0u);
+    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
+    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
+    const uint32_t voff_st = ok ? voff : 0x80000000u;
+    const double g = (double)gamma, gl = (double)gamma * (double)lam;
+    float cr[P], cv[P], nr[P], nv[P];
+    uint32_t ca, na;
+    float vnext = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, (uint32_t)T * row, 0));
+    double a = 0.0;
+    gae_stream_load<P>(rs_r, rs_v, rs_d, voff, row, B, T, cr, cv, ca);
+    for (int tb = T; tb > 0; tb -= 2 * P) {
+        if (tb - P > 0) gae_stream_load<P>(rs_r, rs_v, rs_d, voff, row, B, tb - P, nr, nv, na);
+        gae_stream_block<P>(rs_adv, rs_ret, voff_st, row, tb, cr, cv, ca, g, gl, a, vnext);
+        if (tb - P <= 0) break;
+        if (tb - 2 * P > 0) gae_stream_load<P>(rs_r, rs_v, rs_d, voff, row, B, tb - 2 * P, cr, cv, ca);
+        gae_stream_block<P>(rs_adv, rs_ret, voff_st, row, tb - P, nr, nv, na, g, gl, a, vnext);
     }
 }
 

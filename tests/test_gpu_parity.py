@@ -517,7 +517,9 @@ def test_gpu_synth_matches_oracle():
 @pytest.mark.parametrize("T,B,kernel", [(300, 10, "scan"), (257, 63, "scan"), (1, 5, "tile16"), (63, 2, "tile16"),
                                         # tiled: T below / across / not a multiple of the segment, ragged B
                                         (37, 100, "tile16"), (64, 64, "tile16"), (129, 4099, "tile16"),
-                                        (300, 130, "tile16"), (256, 65536, "tile8"), (37, 16385, "tile8")])
+                                        (300, 130, "tile16"), (256, 65536, "tile8"), (37, 16385, "tile8"),
+                                        # the 64-VGPR tile (B >= 65,536, T >= 256): ragged B, T past a segment
+                                        (300, 70001, "tile8_occ8"), (256, 65600, "tile8_occ8")])
 def test_gpu_gae_kernels_match_oracle(T, B, kernel):
     """GAE(gamma, lambda) over a [T, B] rollout through the kernel each shape takes
     (chunked wave scan for a handful of envs with long horizons, the tiled scan with

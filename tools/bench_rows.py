@@ -85,20 +85,36 @@ def main():
             d = (torch.rand(T, B, device=dev, generator=g) < 0.01).to(torch.uint8) if dn else None
             adv, ret = torch.empty_like(r), torch.empty_like(r)
             alg = T * B * (4 + 4 + 4 + 4 + (1 if dn else 0)) + B * 4
-            modes = ("loop", "scan", "tile", "tile16", "auto") if T * B <= (1 << 24) else ("tile", "tile16", "auto")
+            big = T * B <= (1 << 24)
+            modes = {"loop": {"PMENV_GAE": "loop"}, "scan": {"PMENV_GAE": "scan"}} if big else {}
+            modes.update({"tile": {"PMENV_GAE": "tile", "PMENV_GAE_U": "8"},
+                          "tile16": {"PMENV_GAE": "tile", "PMENV_GAE_U": "16"},
+                          "tile_occ8": {"PMENV_GAE": "tile8"},
+                          "stream8": {"PMENV_GAE": "stream", "PMENV_GAE_P": "8"},
+                          "stream16": {"PMENV_GAE": "stream", "PMENV_GAE_P": "16"},
+                          "stream32": {"PMENV_GAE": "stream", "PMENV_GAE_P": "32"},
+                          "auto": {}})
             nbytes = lib.pmenv_gae_workspace(T, B)
             work = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=dev)
-            for mode in modes:
-                for k in ("PMENV_GAE", "PMENV_GAE_U"):
+            gk = ("PMENV_GAE", "PMENV_GAE_U", "PMENV_GAE_P")
+            outs = {}
+            for mode, env in modes.items():
+                for k in gk:
                     os.environ.pop(k, None)
-                if mode != "auto":
-                    os.environ["PMENV_GAE"] = mode.rstrip("16")
-                    os.environ["PMENV_GAE_U"] = "16" if mode.endswith("16") else "8"
+                os.environ.update(env)
                 # auto = what rollout.gae runs: pmenv_gae_ex with its workspace (horizon split)
-                us = timeit(lambda: ck(lib.pmenv_gae_ex(P(r), P(v), P(d), P(adv), P(ret), T, B, 0.99, 0.95, P(work),
-                                                        nbytes, st), "gae"), a.reps)
-                res.append(row(f"gae_{mode}", us, alg, T=T, B=B, dones=dn, split=bool(nbytes) and mode == "auto"))
-            for k in ("PMENV_GAE", "PMENV_GAE_U"):
+                call = lambda: ck(lib.pmenv_gae_ex(P(r), P(v), P(d), P(adv), P(ret), T, B, 0.99, 0.95,  # noqa: E731
+                                                   P(work), nbytes, st), "gae")
+                call()
+                outs[mode] = (adv.clone(), ret.clone())
+                us = timeit(call, a.reps)
+                same_tile = bool(torch.equal(outs[mode][0], outs["tile"][0])) if "tile" in outs else None
+                same_loop = bool(torch.equal(outs[mode][0], outs["loop"][0])) if "loop" in outs else None
+                err = float((outs[mode][0] - outs["tile"][0]).abs().max()) if "tile" in outs else None
+                res.append(row(f"gae_{mode}", us, alg, T=T, B=B, dones=dn, split=bool(nbytes) and mode == "auto",
+                               same_bits_tile=same_tile, same_bits_loop=same_loop, max_abs_vs_tile=err))
+            del outs
+            for k in gk:
                 os.environ.pop(k, None)
             del r, v, d, adv, ret
         # advantage moments (the 24-byte all-reduce's input)
