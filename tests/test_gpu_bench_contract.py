@@ -51,3 +51,30 @@ def test_bench_refuses_a_knob():
     env = dict(os.environ, PMENV_ONE="all")
     p = _run(env=env)
     assert p.returncode != 0 and "PMENV_" in (p.stderr + p.stdout)
+
+
+def test_bench_two_ranks_rehearsal():
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank) with both
+    ranks on the one GPU over gloo (RCCL refuses two ranks on a device): weak scaling,
+    value = both ranks' env-steps over the max-over-ranks time, the moments all-reduce
+    recorded, parity on every rank."""
+    import socket
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--dist-backend", "gloo", "--envs-per-gpu", "2048", "--steps", "8", "--warmup", "2", "--alt-steps", "0"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert abs(d["value"] - 2 * 2048 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    assert d["collective"]["backend"] == "gloo" and d["collective"]["count_all_ranks"] > 0
+    assert d["parity_sample"]["obs_bit_exact_all_ranks"] is True
+    assert d["cpu_baseline"] is None                     # rank 0 at N = 1 only
