@@ -1491,9 +1491,28 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     if (!series || !start || (!weights && T_rec > 0) || !t_idx || !env || !s || T < 1 || N < 1 || F < 2 || W < 1 ||
         T_rec < 0 || B < 1 || S < 1 || ring_mode < 0 || ring_mode > 1)
         return PMENV_ERR_ARG;
-    const int64_t threads = (int64_t)S * N * W * F;
-    rollout_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(series, T, N, F, W, start, weights,
-                                                                                T_rec, B, ring_mode, t_idx, env, S, s);
+#ifdef PMENV_AB
+    if (ab_knob("PMENV_RGATHER_ELEM")) {          // tools: one thread per output float
+        const int64_t threads = (int64_t)S * N * W * F;
+        rollout_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
+            series, T, N, F, W, start, weights, T_rec, B, ring_mode, t_idx, env, S, s);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+#endif
+    const size_t lds = (size_t)W * N * F * sizeof(float);
+    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && (int64_t)(T + W) * N * 4 < (1ll << 31);
+#ifdef PMENV_AB
+    if (ab_knob("PMENV_RGATHER_ROWS")) tile = false;      // tools: the wave-per-row form
+#endif
+    if (tile) {                                            // one workgroup per sample, staged in LDS
+        rollout_gather_tile_kernel<<<(unsigned)S, 256, lds, stream>>>(
+            series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N * 4),
+            make_fastdiv((uint32_t)N), make_fastdiv((uint32_t)(W * F)), make_fastdiv((uint32_t)F));
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
+    const int64_t rows = (int64_t)S * N;                 // one wave per (sample, asset) row
+    rollout_gather_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(
+        series, T, N, F, W, start, weights, B, ring_mode, t_idx, env, S, s, make_fastdiv((uint32_t)F));
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

@@ -63,8 +63,8 @@ __global__ void replay_gather_kernel(const float* series, int T, int N, int F, i
 // Chronological position c of the window after u = t updates reads row t + c; once the
 // ring is full (u >= W-1) the reference returns it in storage order (:38-39): position
 // p holds update j with j % W == p, i.e. chronological c = (p - u - 1) mod W.
-// One thread per output float ([S, N, W, F], coalesced stores). Days outside the series
-// read NaN.
+// Days outside the series read NaN.
+#ifdef PMENV_AB   // tools build: one thread per output float ([S, N, W, F], coalesced stores)
 __global__ void rollout_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* start,
                                       const float* weights, int T_rec, int B, int ring_mode, const int32_t* t_idx,
                                       const int32_t* env, int S, float* s) {
@@ -91,6 +91,114 @@ __global__ void rollout_gather_kernel(const float* series, int T, int N, int F, 
         else v = weights[((size_t)(r - W) * B + b) * N + n];
     }
     s[i] = v;
+}
+#endif
+
+constexpr int kRowGatherUnroll = 8;   // rows of W*F <= 512 floats: all loads first
+
+// The map above, one wave per (sample, asset) row of W*F floats: a lane writes floats
+// lane, lane + 64, ... of the row (each store one contiguous 256-B run), the day and
+// channel from the row offset by one multiply-shift, the sample's env / step / start
+// wave-uniform. The float-per-thread form (tools build) spends its time in 64-bit divisions.
+__global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const float* series, int T, int N, int F, int W,
+                                                                  const int32_t* start, const float* weights,
+                                                                  int B, int ring_mode, const int32_t* t_idx,
+                                                                  const int32_t* env, int S, float* s, FastDiv div_f) {
+    const int64_t rowi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (rowi >= (int64_t)S * N) return;
+    const int lane = threadIdx.x & 63;
+    const int j = __builtin_amdgcn_readfirstlane((int)(rowi / N));
+    const int n = __builtin_amdgcn_readfirstlane((int)(rowi - (int64_t)j * N));
+    const int b = env[j], t = t_idx[j];
+    const int d0 = start[b] + t;
+    const int Fm = F - 1, WF = W * F;
+    const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
+    float* out = s + rowi * WF;
+    // the value of row float i: a series or a weight-history float, or a constant
+    auto fetch = [&](int i) -> float {
+        const int p = (int)fdiv((uint32_t)i, div_f), f = i - p * F;
+        if (f < Fm) {
+            const int d = d0 + p;
+            return (d >= 0 && d < T) ? series[((size_t)d * N + n) * Fm + f] : NAN;
+        }
+        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
+        const int r = t + c;                       // history row
+        if (r < W - 1) return 0.0f;
+        if (r == W - 1) return n == 0 ? 1.0f : 0.0f;
+        return weights[((size_t)(r - W) * B + b) * N + n];
+    };
+    if (WF <= 64 * kRowGatherUnroll) {             // every load of the row in flight before the stores
+        float v[kRowGatherUnroll];
+#pragma unroll
+        for (int k = 0; k < kRowGatherUnroll; ++k) v[k] = lane + 64 * k < WF ? fetch(lane + 64 * k) : 0.0f;
+#pragma unroll
+        for (int k = 0; k < kRowGatherUnroll; ++k)
+            if (lane + 64 * k < WF) out[lane + 64 * k] = v[k];
+        return;
+    }
+    for (int i = lane; i < WF; i += 64) out[i] = fetch(i);
+}
+
+// One workgroup per sample (F = 5, the sample's [W, N] weight block and [W, N, 4] market
+// block fit LDS): both blocks are staged with coalesced reads — the market block is W
+// consecutive series days, contiguous in [T, N, 4]; each history row's N weights are one
+// contiguous run of [T_rec, B, N] — and the [N, W, 5] window is written as 16-B chunks
+// from LDS (a lane's four floats walk (asset, day, channel) incrementally). Every weight
+// line is fetched once per sample, where the per-row form fetches it per asset row.
+__global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
+                                                                  const int32_t* start, const float* weights, int B,
+                                                                  int ring_mode, const int32_t* t_idx,
+                                                                  const int32_t* env, float* s, FastDiv div_n4,
+                                                                  FastDiv div_n, FastDiv div_wf, FastDiv div_f) {
+    constexpr int F = 5;
+    extern __shared__ float sh[];                  // market [W][N][4], then weights [W][N]
+    float* sh_m = sh;
+    float* sh_w = sh + (size_t)W * N * 4;
+    const int tid = threadIdx.x;
+    const int j = blockIdx.x;
+    const int b = env[j], t = t_idx[j];
+    const int d0 = start[b] + t;
+    const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
+    const int nm = W * N * 4, nw = W * N;
+    const float* src = series + (size_t)d0 * N * 4;
+    for (int i = tid; i < nm; i += 256) {
+        const int d = d0 + (int)fdiv((uint32_t)i, div_n4);
+        sh_m[i] = (d >= 0 && d < T) ? src[i] : NAN;   // days outside the series read NaN
+    }
+    for (int i = tid; i < nw; i += 256) {
+        const int p = (int)fdiv((uint32_t)i, div_n), n = i - p * N;
+        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
+        const int r = t + c;                       // history row
+        float v;
+        if (r < W - 1) v = 0.0f;
+        else if (r == W - 1) v = n == 0 ? 1.0f : 0.0f;
+        else v = weights[((size_t)(r - W) * B + b) * N + n];
+        sh_w[i] = v;
+    }
+    __syncthreads();
+    const int WF = W * F;
+    const int nq = N * WF / 4;
+    f4* out = reinterpret_cast<f4*>(s + (size_t)j * N * WF);
+    for (int q = tid; q < nq; q += 256) {
+        const int e = 4 * q;
+        int n = (int)fdiv((uint32_t)e, div_wf);
+        int rem = e - n * WF;
+        int p = (int)fdiv((uint32_t)rem, div_f);
+        int f = rem - p * F;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = f < F - 1 ? sh_m[(p * N + n) * 4 + f] : sh_w[p * N + n];
+            if (++f == F) {
+                f = 0;
+                if (++p == W) {
+                    p = 0;
+                    ++n;
+                }
+            }
+        }
+        out[q] = f4{v[0], v[1], v[2], v[3]};
+    }
 }
 
 #ifdef PMENV_AB   // tools build: the thread-per-env walk (the fused kernel replaced it)

@@ -117,6 +117,34 @@ def main():
             for k in gk:
                 os.environ.pop(k, None)
             del r, v, d, adv, ret
+        # compact on-policy rollout: minibatch windows re-materialised from the resident
+        # series + recorded w' (pmenv_rollout_gather), config 2's shape (4,096 envs x 32 steps)
+        for Bc, Tr, S in ((4096, 32, 4096), (4096, 32, 32768), (65536, 64, 8192)):
+            N_, W_ = 30, 50
+            Ts = Tr + W_ + 8
+            ser_c = torch.rand(Ts, N_, 4, device=dev, generator=g)
+            start = torch.randint(0, 8, (Bc,), device=dev, generator=g).to(torch.int32)
+            wts = torch.rand(Tr, Bc, N_, device=dev, generator=g)
+            tix = torch.randint(0, Tr + 1, (S,), device=dev, generator=g).to(torch.int32)
+            eix = torch.randint(0, Bc, (S,), device=dev, generator=g).to(torch.int32)
+            out_c = torch.empty(S, N_, W_, 5, device=dev)
+            call = lambda: ck(lib.pmenv_rollout_gather(P(ser_c), Ts, N_, 5, W_, P(start), P(wts), Tr, Bc, 0,  # noqa: E731
+                                                       P(tix), P(eix), S, P(out_c), st), "rollout_gather")
+            outs = {}
+            # the product's LDS-staged tile, the wave-per-row and float-per-thread forms (tools)
+            for form, knob in (("tile", None), ("rows", "PMENV_RGATHER_ROWS"), ("elem", "PMENV_RGATHER_ELEM")):
+                os.environ.pop("PMENV_RGATHER_ELEM", None)
+                os.environ.pop("PMENV_RGATHER_ROWS", None)
+                if knob:
+                    os.environ[knob] = "1"
+                call()
+                outs[form] = out_c.clone()
+                res.append(row(f"rollout_gather_{form}", timeit(call, a.reps), S * N_ * W_ * 5 * 4, B=Bc, T=Tr, S=S,
+                               N=N_, W=W_, same_bits=bool(torch.equal(outs[form], outs["tile"]))))
+            os.environ.pop("PMENV_RGATHER_ELEM", None)
+            os.environ.pop("PMENV_RGATHER_ROWS", None)
+            del outs
+            del ser_c, wts, out_c
         # advantage moments (the 24-byte all-reduce's input)
         for n in (256 * 65536, 256 * 4096):
             x = torch.randn(n, device=dev, generator=g)
