@@ -61,7 +61,8 @@ def test_gpu_on_policy_rollout_and_update(B, N, W, T):
 
 
 @pytest.mark.parametrize("ring", ["storage", "chrono"])
-@pytest.mark.parametrize("B,N,W,T", [(33, 7, 6, 20), (5, 30, 50, 60), (64, 1, 2, 9)])
+# (the LDS-staged gather: 16-B granular windows of <= 64 KiB; the per-row gather: the rest)
+@pytest.mark.parametrize("B,N,W,T", [(33, 7, 6, 20), (5, 30, 50, 60), (64, 1, 2, 9), (3, 80, 50, 8)])
 def test_gpu_compact_rollout_rematerialises_the_env_windows(ring, B, N, W, T):
     """The compact rollout (resident series, O(T*B*N) storage) re-materialises, for
     every step t and env, exactly the window the env held after t steps — market
