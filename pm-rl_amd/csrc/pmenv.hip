@@ -1500,7 +1500,7 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     }
 #endif
     const size_t lds = (size_t)W * N * F * sizeof(float);
-    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && (int64_t)(T + W) * N * 4 < (1ll << 31);
+    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024;     // market [W][N][4] + weights [W][N]
 #ifdef PMENV_AB
     if (ab_knob("PMENV_RGATHER_ROWS")) tile = false;      // tools: the wave-per-row form
 #endif
