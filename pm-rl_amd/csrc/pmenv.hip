@@ -113,6 +113,7 @@ struct pmenv {
     int fused_vec;
     int ablate;           // PMENV_ABLATE timing-only variants
     bool one_nocap, flat_s80;
+    int flat1_lds_pad;
     size_t lds_scalar, lds_stream;
     char err[512];
 };
@@ -564,13 +565,17 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     const int pol = out ? h->flat_pol : h->flat_ip_pol;
     const unsigned grid = (h->flat_qtot + (uint32_t)(h->flat1_block * h->flat1_vec) - 1) /
                           (uint32_t)(h->flat1_block * h->flat1_vec);
+    size_t pad = 0;                               // tools: extra LDS per workgroup (occupancy study)
+#ifdef PMENV_AB
+    pad = (size_t)h->flat1_lds_pad;
+#endif
 #define PMENV_FLAT1_LAUNCH(BK, VV)                                                                           \
     if (out) {                                                                                              \
-        if (pol == 1) step_flat_kernel<BK, VV, 1, true><<<grid, BK, 0, stream>>>(p, h->flat_qtot);          \
-        else step_flat_kernel<BK, VV, 0, true><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                   \
+        if (pol == 1) step_flat_kernel<BK, VV, 1, true><<<grid, BK, pad, stream>>>(p, h->flat_qtot);        \
+        else step_flat_kernel<BK, VV, 0, true><<<grid, BK, pad, stream>>>(p, h->flat_qtot);                 \
     } else {                                                                                                \
-        if (pol == 1) step_flat_kernel<BK, VV, 1, false><<<grid, BK, 0, stream>>>(p, h->flat_qtot);         \
-        else step_flat_kernel<BK, VV, 0, false><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                  \
+        if (pol == 1) step_flat_kernel<BK, VV, 1, false><<<grid, BK, pad, stream>>>(p, h->flat_qtot);       \
+        else step_flat_kernel<BK, VV, 0, false><<<grid, BK, pad, stream>>>(p, h->flat_qtot);                \
     }
     const int key = h->flat1_block * 100 + h->flat1_vec;
 #ifdef PMENV_AB
@@ -819,6 +824,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         if (!strcmp(knob, "lds")) h->streaming = h->flat = h->flat_inplace = false;
     h->ablate = ab_int("PMENV_ABLATE", 0);
     h->one_nocap = ab_int("PMENV_ONE_NOCAP", 0) != 0;
+    h->flat1_lds_pad = ab_int("PMENV_FLAT1_LDS_PAD", 0);
     h->flat_s80 = ab_int("PMENV_FLAT_S80", 0) != 0;
 #endif
     h->k1_groups = ab_int("PMENV_K1_GROUPS", 1);

@@ -39,7 +39,7 @@ days = [day0 + t for t in range(a.H)]
 KNOBS = ("PMENV_ADVANCE", "PMENV_UNIT_ROWS", "PMENV_ABLATE", "PMENV_FUSED", "PMENV_K1_GROUPS",
          "PMENV_STREAM_BLOCK", "PMENV_STREAM_POL", "PMENV_FLAT", "PMENV_FLAT_BLOCK",
          "PMENV_FLAT_INPLACE", "PMENV_FLAT_IP_BLOCK", "PMENV_FLAT_IP_VEC", "PMENV_FLAT_DB_WG", "PMENV_K1",
-         "PMENV_ONE", "PMENV_ONE_V", "PMENV_ONE_NOCAP", "PMENV_FLAT_S80", "PMENV_ONE_LDS_PAD", "PMENV_FLAT1", "PMENV_FLAT1_GEOM", "PMENV_FLAT1_XCD", "PMENV_FLAT1_POL")
+         "PMENV_ONE", "PMENV_ONE_V", "PMENV_ONE_NOCAP", "PMENV_FLAT_S80", "PMENV_ONE_LDS_PAD", "PMENV_FLAT1", "PMENV_FLAT1_GEOM", "PMENV_FLAT1_XCD", "PMENV_FLAT1_POL", "PMENV_FLAT1_LDS_PAD")
 for v in a.variants.split(","):
     # "base+KNOB=val+...": extra env knobs at creation (e.g. "o+PMENV_FUSED=0")
     base, *extra = v.split("+")
