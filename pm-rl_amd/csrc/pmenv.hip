@@ -1512,8 +1512,8 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
 #endif
     if (tile) {                                            // one workgroup per sample, staged in LDS
         rollout_gather_tile_kernel<<<(unsigned)S, 256, lds, stream>>>(
-            series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N * 4),
-            make_fastdiv((uint32_t)N), make_fastdiv((uint32_t)(W * F)), make_fastdiv((uint32_t)F));
+            series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N),
+            make_fastdiv((uint32_t)(W * F)), make_fastdiv((uint32_t)F));
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
     }
     const int64_t rows = (int64_t)S * N;                 // one wave per (sample, asset) row

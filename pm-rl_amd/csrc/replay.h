@@ -148,8 +148,8 @@ __global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const float* s
 __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
                                                                   const int32_t* start, const float* weights, int B,
                                                                   int ring_mode, const int32_t* t_idx,
-                                                                  const int32_t* env, float* s, FastDiv div_n4,
-                                                                  FastDiv div_n, FastDiv div_wf, FastDiv div_f) {
+                                                                  const int32_t* env, float* s, FastDiv div_n,
+                                                                  FastDiv div_wf, FastDiv div_f) {
     constexpr int F = 5;
     extern __shared__ float sh[];                  // market [W][N][4], then weights [W][N]
     float* sh_m = sh;
@@ -159,21 +159,36 @@ __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* s
     const int b = env[j], t = t_idx[j];
     const int d0 = start[b] + t;
     const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
-    const int nm = W * N * 4, nw = W * N;
-    const float* src = series + (size_t)d0 * N * 4;
-    for (int i = tid; i < nm; i += 256) {
-        const int d = d0 + (int)fdiv((uint32_t)i, div_n4);
-        sh_m[i] = (d >= 0 && d < T) ? src[i] : NAN;   // days outside the series read NaN
-    }
-    for (int i = tid; i < nw; i += 256) {
-        const int p = (int)fdiv((uint32_t)i, div_n), n = i - p * N;
-        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
-        const int r = t + c;                       // history row
-        float v;
-        if (r < W - 1) v = 0.0f;
-        else if (r == W - 1) v = n == 0 ? 1.0f : 0.0f;
-        else v = weights[((size_t)(r - W) * B + b) * N + n];
-        sh_w[i] = v;
+    const int nd = W * N;                          // market: one f4 per (day, asset); weights: one float
+    const f4* src = reinterpret_cast<const f4*>(series) + (size_t)d0 * N;
+    f4* sh_m4 = reinterpret_cast<f4*>(sh_m);
+    // every load of a round in flight before its LDS writes (4 per thread and array)
+    for (int i0 = 0; i0 < nd; i0 += 4 * 256) {
+        f4 m[4];
+        float w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * 256 + tid;
+            m[k] = f4{NAN, NAN, NAN, NAN};
+            w[k] = 0.0f;
+            if (i < nd) {
+                const int p = (int)fdiv((uint32_t)i, div_n), n = i - p * N;
+                const int d = d0 + p;
+                if (d >= 0 && d < T) m[k] = src[i];        // days outside the series read NaN
+                const int c = storage ? (((p - t - 1) % W) + W) % W : p;
+                const int r = t + c;                       // history row
+                if (r == W - 1) w[k] = n == 0 ? 1.0f : 0.0f;
+                else if (r > W - 1) w[k] = weights[((size_t)(r - W) * B + b) * N + n];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = i0 + k * 256 + tid;
+            if (i < nd) {
+                sh_m4[i] = m[k];
+                sh_w[i] = w[k];
+            }
+        }
     }
     __syncthreads();
     const int WF = W * F;
