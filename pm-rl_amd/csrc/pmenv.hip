@@ -1588,8 +1588,7 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
             else batch_reward_fwd_rows_kernel<0, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
         }
 #undef PMENV_FWD_ARGS
-        if (ret_out || N > kQuadMaxN)
-            batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+        if (ret_out) batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
     }
 #endif
@@ -1611,9 +1610,8 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         else batch_reward_rows_kernel<0><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
     }
     batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out, nparts);
-    // the chosen per-row return (and the row flags of the N > 64 backward)
-    if (ret_out || N > kQuadMaxN)
-        batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+    // the chosen per-row return, when asked for (the backward takes each row's choice itself)
+    if (ret_out) batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

@@ -15,8 +15,9 @@
 
 namespace pmenv_dev {
 
-// work layout (f64): [0,B) ret chosen, [B,2B) row sum, [2B,3B) row min, [3B,4B) ret raw,
-// [4B,5B) ret softmax, [5B,6B) row normalised flag, [6B..6B+8) globals:
+// work layout (f64): [0,B) ret chosen and [5B,6B) row normalised flag (the select pass,
+// run when the caller asks for the per-row returns), [B,2B) row sum, [2B,3B) row min,
+// [3B,4B) ret raw, [4B,5B) ret softmax, [6B..6B+8) globals:
 // +0 normalised (global), +1 mean, +2 std, +3 reward, +4 norm mode, +6 the tools build's
 // one-launch forward's ticket (a u32, zeroed by the host before the launch); then the partial
 // records of the row blocks (kRowsPerBlock or kQuadRows rows each), field-major:
@@ -578,7 +579,14 @@ __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, 
         }
     }
     const double go = (double)*grad_out;
-    const double r = work[b];
+    // the per-row choice from the forward's workspace (its norm mode at work[6B+4]), as
+    // the quad backward does: the forward needs no select pass for this kernel
+    const int norm = (int)work[6 * (size_t)B + 4];
+    bool nb;
+    if (norm == PMENV_BNORM_GLOBAL_OR) nb = work[6 * (size_t)B] != 0.0;
+    else if (norm == PMENV_BNORM_ROW_OR) nb = row_normalises(work[(size_t)B + b], work[2 * (size_t)B + b]);
+    else nb = false;
+    const double r = nb ? work[4 * (size_t)B + b] : work[3 * (size_t)B + b];
     double dr;
     if (kind == PMENV_REWARD_LOG_RETURN) dr = scale / ((double)B * r);
     else if (kind == PMENV_REWARD_RETURN) dr = scale / (double)B;
@@ -588,7 +596,6 @@ __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, 
     }
     dr *= go;
     const double v = (double)v_prev[b];
-    const bool nb = work[5 * (size_t)B + b] != 0.0;
     if (EPL > 0) {
         float out[E];
         if (!nb) {

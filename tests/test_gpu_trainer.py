@@ -119,3 +119,24 @@ def test_gpu_batch_reward_forward_is_deterministic(B, N):
         R, _, _ = or_batch_reward(a.cpu().numpy(), v.cpu().numpy(), p.cpu().numpy(),
                                   reward="log_returns" if kind == 0 else "sharpe_ratio", norm="global_or")
         assert np.isclose(float(ref[0][1]), np.float32(R), rtol=1e-6, atol=1e-12), (kind, float(ref[0][1]), R)
+
+
+@pytest.mark.parametrize("B,N,norm", [(300, 129, "global_or"), (64, 500, "row_or"), (33, 65, "none")])
+def test_gpu_batch_reward_backward_without_per_row_returns(B, N, norm):
+    """The backward takes each row's normalisation choice from the forward's workspace
+    itself: with or without the per-row returns requested, the gradients are the same."""
+    from pmenv.trainer import batch_reward
+    rng = np.random.default_rng(B * N)
+    a_np = rng.standard_normal((B, N)).astype(np.float32)
+    a_np[::3] = np.abs(a_np[::3]) / np.abs(a_np[::3]).sum(1, keepdims=True)
+    v = torch.tensor((25000.0 * np.exp(0.1 * rng.standard_normal(B))).astype(np.float32), device=DEV)
+    p = torch.tensor((1.0 + 0.01 * rng.standard_normal((B, N))).astype(np.float32), device=DEV).reshape(B, N, 1)
+    grads = []
+    for want in (False, True):
+        a = torch.tensor(a_np, device=DEV).reshape(B, N, 1).requires_grad_(True)
+        out = batch_reward(a, v, p, reward="sharpe_ratio", norm=norm, return_ret=want)
+        (out[0] if want else out).backward()
+        grads.append(a.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    _, _, og = or_batch_reward(a_np, v.cpu().numpy(), p.reshape(B, N).cpu().numpy(), reward="sharpe_ratio", norm=norm)
+    np.testing.assert_allclose(grads[0].reshape(B, N).cpu().numpy(), og, rtol=1e-5, atol=1e-6 * (np.abs(og).max() + 1e-30))
