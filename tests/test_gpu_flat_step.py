@@ -338,3 +338,39 @@ def test_gpu_flat_counts_a_nonfinite_env_once():
     assert env.nonfinite_count() == 1
     assert torch.isnan(r[5]) and torch.isfinite(r[torch.arange(B, device=DEV) != 5]).all()
     assert torch.isfinite(obs[torch.arange(B, device=DEV) != 5]).all()
+
+
+def test_gpu_flat_two_handles_on_two_streams():
+    """One handle per stream: two envs stepped on two HIP streams with their launches
+    interleaved (each handle's snapshot / halo parities are its own) give the bits of
+    each env stepped alone."""
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 4096, 30, 50, 12
+    ser = [synth.series(W + T, B, N, env_offset=k * B, seed=5, device=DEV) for k in range(2)]
+    act = [synth.actions(T, B, N, env_offset=k * B, seed=6, device=DEV) for k in range(2)]
+
+    def run(streams):
+        envs, obs, rews = [], [], []
+        for k in range(2):
+            with torch.cuda.stream(streams[k]):
+                e = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
+                o = synth.window_from_series(ser[k], W)
+                e.reset(o)
+                envs.append(e)
+                obs.append(o)
+                rews.append([])
+        for t in range(T):
+            for k in range(2):
+                with torch.cuda.stream(streams[k]):
+                    r, _ = envs[k].step(act[k][t], obs[k], bar=ser[k][W + t])
+                    rews[k].append(r.clone())
+        torch.cuda.synchronize()
+        return [(obs[k], torch.stack(rews[k]), envs[k].value.clone()) for k in range(2)]
+
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    both = run([s1, s2])
+    alone = run([s1, s1])
+    for k in range(2):
+        for x, y in zip(both[k], alone[k]):
+            assert torch.equal(x, y), k
