@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* s
                                                                   const int32_t* env, float* s, FastDiv div_n,
                                                                   FastDiv div_wf, FastDiv div_f) {
     constexpr int F = 5;
-    extern __shared__ float sh[];                  // market [W][N][4], then weights [W][N]
+    extern __shared__ __attribute__((aligned(16))) float sh[];   // market [W][N][4], then weights [W][N]
     float* sh_m = sh;
     float* sh_w = sh + (size_t)W * N * 4;
     const int tid = threadIdx.x;
