@@ -72,13 +72,23 @@ def test_gpu_matches_reference_goldens(name, mode):
 @pytest.mark.parametrize("impl", ["flat", "one_launch", "two_launch"])
 def test_gpu_every_step_path_matches_reference_goldens(name, impl):
     """The reference's recorded outputs replayed through each advance-step implementation
-    forced (AUTO takes one_launch at one env); shapes a path does not fit are skipped."""
+    forced (AUTO takes one_launch at one env). A path refuses exactly the shapes its
+    contract excludes (include/pmenv.h: the one-launch forms need N <= 64 and 16-B
+    granular env windows); those cases check the refusal instead."""
     from pmenv import TradingEnv
     m = gu.load(name)["meta"]
+    N, W, F = m["N"], m["W"], m["F"]
+    # the shape rules of pmenv_set_step_path (include/pmenv.h)
+    granular = F == 5 and (N * W * F) % 4 == 0
+    misfit = {"two_launch": not granular,
+              "one_launch": not (granular and W >= 2 and N <= 64 and N * W * F * 4 <= 64 * 1024),
+              "flat": not (granular and W >= 2 and N <= 64 and N * W * F // 4 >= 148)}[impl]
     try:
-        TradingEnv(num_envs=1, num_assets=m["N"], window=m["W"], features=m["F"], device=DEV, step_impl=impl)
+        TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
     except ValueError:
-        pytest.skip(f"{impl} does not fit N={m['N']} W={m['W']} F={m['F']}")
+        assert misfit, f"{impl} refused N={N} W={W} F={F}"
+        return
+    assert not misfit, f"{impl} accepted N={N} W={W} F={F}"
     g = gu.load(name)
     out = replay_gpu(g, "advance", impl=impl)
     assert out["market_ok"]
