@@ -67,10 +67,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs-per-gpu", type=int, default=65536)
-    ap.add_argument("--global-envs", type=int, default=0,
-                    help="strong scaling: this many envs in total, sharded over the ranks "
-                         "(BASELINE config 4: 65536 over 8 GPUs); 0 = weak scaling, --envs-per-gpu per rank")
+    ap.add_argument("--global-envs", type=int, default=None,
+                    help="strong scaling (the default): this many envs in total, sharded over the ranks "
+                         "(north star / BASELINE config 4: 65,536 over 1/2/4/8 GPUs); default 65536")
+    ap.add_argument("--envs-per-gpu", type=int, default=None,
+                    help="weak scaling: this many envs per rank (implies --weak)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: --envs-per-gpu (default 65536) envs per rank instead of a fixed total")
+    ap.add_argument("--alt-weak-steps", type=int, default=0,
+                    help="N > 1, strong run: also time this many steps of the weak-scaled workload "
+                         "(65,536 envs per rank), reported under alt_weak (0: skip)")
     ap.add_argument("--assets", type=int, default=30)
     ap.add_argument("--window", type=int, default=50)
     ap.add_argument("--features", type=int, default=5)
@@ -89,7 +95,15 @@ def parse():
                     help="extra timed steps of the other window mode (0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo lets several ranks share one GPU (functional rehearsal)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.envs_per_gpu is not None or args.weak:
+        if args.global_envs is not None:
+            ap.error("--global-envs (strong scaling) and --envs-per-gpu / --weak (weak scaling) exclude each other")
+        args.weak = True
+        args.envs_per_gpu = args.envs_per_gpu or 65536
+    elif args.global_envs is None:
+        args.global_envs = 65536
+    return args
 
 
 def cpu_model():
@@ -219,6 +233,57 @@ def reference_golden_mae(dev, torch, TradingEnv):
     return {"case": "simplex_n30_w50_t256 (reference env outputs recorded in tests/golden)", **out}
 
 
+def weak_leg(args, rank, world, dev, lib, _abi, synth, TradingEnv, torch, dist):
+    """The weak-scaled workload beside a strong-scaled run: 65,536 envs per rank (global ids
+    rank * 65,536 ..), in place, `--alt-weak-steps` steps between barriers, max over ranks."""
+    N, W, F, B = args.assets, args.window, args.features, 65536
+    steps = args.alt_weak_steps
+    H = max(1, min(args.horizon, steps + 4))
+    series = synth.series(H + W, B, N, env_offset=rank * B, seed=args.seed, device=dev)
+    actions = synth.actions(H, B, N, env_offset=rank * B, seed=args.seed + 1, device=dev)
+    obs = synth.window_from_series(series, W, F)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=dev,
+                     reward=args.reward, commission=args.commission)
+    env.reset(obs)
+    reward = torch.empty(B, dtype=torch.float32, device=dev)
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    blocks = []
+    for t in range(H):
+        a = _abi.PmenvStepArgs()
+        a.action, a.bar, a.obs, a.reward = actions[t].data_ptr(), series[W + t].data_ptr(), obs.data_ptr(), \
+            reward.data_ptr()
+        blocks.append((a, ctypes.byref(a)))
+    for i in range(4):
+        _abi.check(lib.pmenv_step_ex(env._h, blocks[i % H][1], sp), env._h, "pmenv_step_ex")
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        _abi.check(lib.pmenv_step_ex(env._h, blocks[(4 + i) % H][1], sp), env._h, "pmenv_step_ex")
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el[0])
+    out = {"scaling": "weak", "envs_per_gpu": B, "global_envs": world * B, "steps": steps,
+           "value": world * B * steps / el, "unit": "env-steps/s", "ms_per_step": el / steps * 1e3,
+           "step_path": env.step_path.split(" | ")[-1], "nonfinite_envs": env.nonfinite_count()}
+    env.close()
+    return out
+
+
+def sha256_file(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def spread(us):
     """min / median / max of the sampled kernel times, and which sample was the slowest
     (sample i brackets timed step EVENT_EVERY * i)."""
@@ -256,7 +321,7 @@ def main():
     lib = _abi.load()
 
     N, W, F = args.assets, args.window, args.features
-    if args.global_envs:                             # strong scaling: a shard of a fixed total
+    if not args.weak:                                # strong scaling: a shard of a fixed total
         from pmenv.parallel import shard_range
         lo, hi = shard_range(args.global_envs, rank, world)
         B = hi - lo
@@ -391,6 +456,9 @@ def main():
         n_all, _, _ = parallel.allreduce_moments(parallel.local_moments_cpu(adv).to(adv.device))
         collective = {"op": "all_reduce(sum) of 24-byte advantage moments + normalise", "backend": dist.get_backend(),
                       "us_per_update": c_us, "count_all_ranks": n_all, "normalised_finite": bool(torch.isfinite(normed).all())}
+    alt_weak = None
+    if world > 1 and not args.weak and args.alt_weak_steps > 0:
+        alt_weak = weak_leg(args, rank, world, dev, lib, _abi, synth, TradingEnv, torch, dist)
     nonfinite = env.nonfinite_count()
 
     # ---- 3. checks and baselines (after the timed region)
@@ -411,23 +479,31 @@ def main():
         ref_gold = reference_golden_mae(dev, torch, TradingEnv)
 
     kernel = paths[0 if double else -1].split(" (")[0].split("+")[-1]
-    total_env_steps = (args.global_envs or world * B) * args.steps
+    total_env_steps = (world * B if args.weak else args.global_envs) * args.steps
     value = total_env_steps / elapsed
     bstep = step_bytes(N, W, F)
     achieved = bstep * B / kern_avg_s / 1e9
     achieved_step = bstep * B / (elapsed / args.steps) / 1e9
     window_bytes = B * N * W * F * 4
-    traffic = None
+    traffic, traffic_src = None, None
+    lib_sha = sha256_file(_abi.LIB_PATH)
     try:
         pmc = json.load(open(args.pmc_file))
-        # PMC passes of the same kernel at the same workload only
-        if pmc.get("workload") == [B, N, W, F] and f"::{kernel}<" in pmc.get("dominant_kernel", ""):
+        # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py) of the same kernel at
+        # the same workload, measured on THIS library build (its sha256 recorded on the box):
+        # anything else reports null rather than a stale figure
+        same = pmc.get("workload") == [B, N, W, F] and f"::{kernel}<" in pmc.get("dominant_kernel", "")
+        traffic_src = {"file": os.path.relpath(args.pmc_file, ROOT), "tag": pmc.get("tag"),
+                       "lib_sha256": pmc.get("lib_sha256"), "running_lib_sha256": lib_sha,
+                       "same_workload_and_kernel": same,
+                       "same_library": pmc.get("lib_sha256") == lib_sha}
+        if same and traffic_src["same_library"]:
             traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 
+    l3 = window_bytes * (2 if double else 1) <= L3_BYTES
     if rank == 0:
-        l3 = window_bytes * (2 if double else 1) <= L3_BYTES
         line = {
             "metric": "env-steps/sec (whole node) at 65k envs x 30 assets; reward MAE vs CPU ref",
             "value": value,
@@ -437,21 +513,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.global_envs else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Philox OHLC random walk + softmax actions, resident in HBM)",
             "config": {
-                "workload": f"fused env step, {B} envs/GPU x {N} assets x {W}-day window x {F} channels"
-                            + (f" ({args.global_envs} envs in total, sharded)" if args.global_envs else ""),
-                "envs_per_gpu": B, "global_envs": args.global_envs or world * B, "assets": N, "window": W, "features": F,
+                "workload": (f"fused env step, {world * B if args.weak else args.global_envs} envs in total "
+                             f"({B} envs/GPU) x {N} assets x {W}-day window x {F} channels"),
+                "envs_per_gpu": B, "global_envs": world * B if args.weak else args.global_envs,
+                "assets": N, "window": W, "features": F,
                 "reward": args.reward, "commission": args.commission, "obs_dtype": "f32", "accumulate": "f64",
                 "windows": args.windows,
                 "parallelism": f"env-sharded x{world} (no collective in the step)",
+                # what one rank's share runs as (rank 0): at N = 8 the 65,536-env job is 8,192
+                # envs per GPU, an Infinity-Cache-resident window on its own step path
+                "per_rank": {"envs": B, "window_bytes": window_bytes, "l3_resident": l3,
+                             "step_path": paths[0 if double else -1]},
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kernel, "kernel_avg_us": kern_avg_s * 1e6, "kernel_us": spread(k_us),
                 "bytes_per_env_step": bstep,
                 "achieved_step": achieved_step, "frac_step": achieved_step / HBM_PEAK_GBS,
@@ -468,6 +549,7 @@ def main():
             "knobs": knobs,
             "alt": alt,
             "collective": collective,
+            "alt_weak": alt_weak,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

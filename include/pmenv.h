@@ -72,13 +72,17 @@ typedef enum pmenv_ring_mode {
 
 /* Which value the return uses (trading_env.py:75,88). The reference has two answers:
  * step() takes log(value / (mu * V_prev)) (trading_env.py:75,88,99 — the commission is
- * excluded), while env/reward.py:20-31 forms its returns / sharpe_ratio from
- * info["values"], i.e. V_t / V_{t-1} (trading_env.py:80 — commission included). AUTO,
- * the default, follows each: gross for the log-return reward, net for the others. */
+ * excluded) and records that ratio as info["returns"] (:90), while env/reward.py:20-31
+ * forms returns / log_returns / sharpe_ratio from info["values"], i.e. V_t / V_{t-1}
+ * (trading_env.py:80 — commission included). GROSS, the default, is step()'s answer for
+ * every reward kind, so info["returns"] and every reward match trading_env.py whatever
+ * the commission. NET and AUTO are opt-in; with commission 0 all three agree. */
 typedef enum pmenv_ret_mode {
-    PMENV_RET_GROSS = 0, /* ret = value / (mu * V_prev): excludes commission (trading_env.py:88) */
+    PMENV_RET_GROSS = 0, /* ret = value / (mu * V_prev): excludes commission (trading_env.py:88) — default */
     PMENV_RET_NET = 1,   /* ret = value / V_prev: includes commission (reward.py:20-31 over info["values"]) */
-    PMENV_RET_AUTO = 2   /* GROSS for PMENV_REWARD_LOG_RETURN, NET for every other kind (resolved at create) */
+    PMENV_RET_AUTO = 2   /* opt-in: GROSS for PMENV_REWARD_LOG_RETURN (step()'s hard-coded reward,
+                            trading_env.py:99), NET for the kinds only reward.py defines (returns,
+                            sharpe_ratio) and for diff_sharpe (resolved at create) */
 } pmenv_ret_mode;
 
 typedef struct pmenv_cfg {
@@ -90,7 +94,7 @@ typedef struct pmenv_cfg {
     int32_t reward_kind;    /* pmenv_reward_kind */
     int32_t norm_mode;      /* pmenv_norm_mode */
     int32_t ring_mode;      /* pmenv_ring_mode */
-    int32_t ret_mode;       /* pmenv_ret_mode (AUTO is resolved at create; pmenv_get_cfg returns the result) */
+    int32_t ret_mode;       /* pmenv_ret_mode, default GROSS (AUTO is resolved at create; pmenv_get_cfg returns the result) */
     int32_t mu_max_iter;    /* cap on the commission fixed point (trading_env.py:70 has none) */
     double init_cash;       /* config/base.py:47 INITIAL_CASH = 25000 */
     double commission;      /* config/base.py:48 COMISSION = 0.0 */
@@ -198,9 +202,12 @@ const char* pmenv_step_path(const pmenv* h);
  *
  * FLAT keeps a per-step snapshot of the state its scalar step reads and, in place, the
  * halo of its tiles, both produced by the previous step: a caller that writes the state
- * blob (pmenv_create_in) or an in-place window outside this API must go through
- * pmenv_set_state / pmenv_reset before the next step (both re-prime them; so does every
- * other step path). From the first FLAT step enqueued while `stream` is being captured
+ * blob (pmenv_create_in, e.g. the value) or an in-place window outside this API — or that
+ * hands in a different window at the address of the last one — must say so before the
+ * next step: pmenv_state_written / pmenv_window_written (pmenv_set_state and pmenv_reset
+ * do it themselves; so does every other step path). The reference keeps no copy of the
+ * caller's features (trading_env.py:102-105), so every such edit is honoured.
+ * From the first FLAT step, reset or invalidation enqueued while `stream` is being captured
  * into a hipGraph on, the handle sequences its FLAT steps on the device (a small
  * flat_seq_kernel before each step_flat_kernel reads the parity and the snapshot's
  * validity from device memory, so graph replays and eager calls interleave freely;
@@ -212,6 +219,16 @@ typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_FLAT = 3
 } pmenv_step_path_kind;
 int pmenv_set_step_path(pmenv* h, int32_t path);
+
+/* The caller wrote the in-place window `obs` between steps (features it owns and may
+ * edit, trading_env.py:102-105), or hands in a new window at a previous one's address:
+ * the next FLAT step re-reads the tile halo from the window (enqueued on `stream`; a
+ * no-op for the other step paths, which keep nothing of the window). */
+int pmenv_window_written(pmenv* h, const float* obs, hipStream_t stream);
+/* The caller wrote the state blob (pmenv_value, pmenv_counter, pmenv_ring or any field of
+ * pmenv_state_layout) outside pmenv_set_state: the next FLAT step re-primes its snapshot
+ * from the state (and its halo from the window). */
+int pmenv_state_written(pmenv* h, hipStream_t stream);
 
 /* Device pointer to the env-owned portfolio values [B] f64 (TradingEnv.value). */
 double* pmenv_value(pmenv* h);

@@ -608,21 +608,6 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     h->halo1_obs = out ? nullptr : p.obs;
 }
 
-// anything but step_flat_kernel that writes the state or a window leaves the snapshot
-// and the halo stale
-int flat1_invalidate(pmenv* h, hipStream_t stream) {
-    h->snap_ok = false;
-    h->halo1_obs = nullptr;
-    if (h->device_seq) {                       // V = 0 (a graph node under capture)
-        const hipError_t e = hipMemsetAsync(h->seq + 2, 0, 4, stream);
-        if (e != hipSuccess) {
-            set_err(h, "invalidating the flat step's snapshot: %s", hipGetErrorString(e));
-            return PMENV_ERR_HIP;
-        }
-    }
-    return PMENV_OK;
-}
-
 // the stream is being captured into a hipGraph: step_flat_kernel's host-chosen parity
 // would be frozen under replay, so the handle switches to the device-sequenced form
 bool capturing(hipStream_t stream) {
@@ -632,6 +617,31 @@ bool capturing(hipStream_t stream) {
         return true;
     }
     return st != hipStreamCaptureStatusNone;
+}
+
+// Anything but step_flat_kernel that writes the state or a window leaves the snapshot and
+// the halo stale (`what` = the device words to clear: V, the snapshot-valid word, or HOBS,
+// the window the halo belongs to). The host flags cover eager steps; device-sequenced
+// handles also clear the device word on the stream. An invalidation enqueued while the
+// stream is being captured switches the handle to the device-sequenced form first: a
+// graph of [reset, flat steps] replays the reset's clear before every replay's steps,
+// where host flags set once at capture time would let replay 2 on read the snapshot the
+// previous replay left (flat_seq_kernel then re-primes from the reset state).
+enum { kInvalSnap = 1, kInvalHalo = 2 };
+int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInvalHalo, bool host_only = false) {
+    if (what & kInvalSnap) h->snap_ok = false;
+    h->halo1_obs = nullptr;
+    if (host_only || !h->flat1_ok) return PMENV_OK;
+    if (!h->device_seq && h->flat1 && capturing(stream)) h->device_seq = true;
+    if (!h->device_seq) return PMENV_OK;
+    // V = 0 clears both (a stale V re-primes the halo too); HOBS = 0 only the halo
+    const hipError_t e = (what & kInvalSnap) ? hipMemsetAsync(h->seq + 2, 0, 4, stream)
+                                             : hipMemsetAsync(h->seq + 4, 0, 8, stream);
+    if (e != hipSuccess) {
+        set_err(h, "invalidating the flat step's snapshot: %s", hipGetErrorString(e));
+        return PMENV_ERR_HIP;
+    }
+    return PMENV_OK;
 }
 
 // which windows take the one-launch steps under `path`
@@ -664,7 +674,7 @@ void pmenv_cfg_default(pmenv_cfg* cfg, int32_t num_envs, int32_t num_assets, int
     cfg->reward_kind = PMENV_REWARD_LOG_RETURN;
     cfg->norm_mode = PMENV_NORM_AND;
     cfg->ring_mode = PMENV_RING_STORAGE;
-    cfg->ret_mode = PMENV_RET_AUTO;
+    cfg->ret_mode = PMENV_RET_GROSS;
     cfg->mu_max_iter = 100;
     cfg->init_cash = 25000.0;
     cfg->commission = 0.0;
@@ -1018,7 +1028,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             return fail(PMENV_ERR_HIP);
         }
     }
-    (void)flat1_invalidate(h, nullptr);      // host flags only: no device sequencing yet
+    (void)flat1_invalidate(h, nullptr, kInvalSnap | kInvalHalo, true);   // no device sequencing yet
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
     h->sa = (double*)(base + off[1]);
@@ -1226,6 +1236,19 @@ int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
     hipError_t e = hipMemcpyAsync(h->state, src, h->state_bytes, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) { set_err(h, "set_state: %s", hipGetErrorString(e)); return PMENV_ERR_HIP; }
     return PMENV_OK;
+}
+
+int pmenv_window_written(pmenv* h, const float* obs, hipStream_t stream) {
+    if (!h) return PMENV_ERR_ARG;
+    (void)obs;                                 // any window: the halo is dropped whichever it was
+    DeviceGuard g(h->device);
+    return flat1_invalidate(h, stream, kInvalHalo);
+}
+
+int pmenv_state_written(pmenv* h, hipStream_t stream) {
+    if (!h) return PMENV_ERR_ARG;
+    DeviceGuard g(h->device);
+    return flat1_invalidate(h, stream, kInvalSnap | kInvalHalo);
 }
 
 int pmenv_nonfinite_count(pmenv* h, uint64_t* out, hipStream_t stream) {
@@ -1506,7 +1529,10 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     }
 #endif
     const size_t lds = (size_t)W * N * F * sizeof(float);
-    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024;     // market [W][N][4] + weights [W][N]
+    // market [W][N][4] + weights [W][N]; the tile's 16-B series loads and window stores need
+    // 16-B aligned series / s (C callers may pass sliced views: those take the row form)
+    const bool al16 = (((uintptr_t)series | (uintptr_t)s) & 15u) == 0;
+    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && al16;
 #ifdef PMENV_AB
     if (ab_knob("PMENV_RGATHER_ROWS")) tile = false;      // tools: the wave-per-row form
 #endif

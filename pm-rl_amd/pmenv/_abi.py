@@ -72,6 +72,8 @@ SIGNATURES = [
     ("pmenv_state_bytes", _SZ, [_P]),
     ("pmenv_step_path", ctypes.c_char_p, [_P]),
     ("pmenv_set_step_path", ctypes.c_int, [_P, _I32]),
+    ("pmenv_window_written", ctypes.c_int, [_P, _P, _P]),
+    ("pmenv_state_written", ctypes.c_int, [_P, _P]),
     ("pmenv_get_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_set_state", ctypes.c_int, [_P, _P, _P]),
     ("pmenv_nonfinite_count", ctypes.c_int, [_P, ctypes.POINTER(_U64), _P]),

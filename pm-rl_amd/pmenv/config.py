@@ -30,8 +30,9 @@ class EnvConfig:
     reward: str = REWARD              # log_returns | returns | sharpe_ratio | diff_sharpe
     norm: str = "and"                 # and (trading_env.py:58) | or (pg.py:52)
     ring: str = "storage"             # storage (weight_buffer.py:38-39) | chrono
-    ret: str = "auto"                 # auto: gross (trading_env.py:88) for log_returns, net (reward.py:20-31,
-                                      # info["values"]) for returns / sharpe_ratio / diff_sharpe | gross | net
+    ret: str = "gross"                # gross: trading_env.py:88 for every reward kind (info["returns"] as
+                                      # the reference records it) | net: reward.py:20-31 over info["values"]
+                                      # (commission included) | auto: gross for log_returns, net otherwise
     init_cash: float = float(INITIAL_CASH)
     commission: float = COMISSION
     reward_scale: float = float(REWARD_SCALE)

@@ -10,6 +10,7 @@ drawdown, average turnover) per env on device.
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _abi
@@ -25,9 +26,14 @@ def valid_starts(row_episode, oldest, count, W, H):
     one episode — the reference samples a window inside one epoch of its [epoch, step]
     layout (buffer.py:17-21, :47-51). Episode ids only grow along the ring, so the
     first and the last row of a window decide. st < count - W - 1, as buffer.py:50
-    draws starts below epoch_len - WINDOW_SIZE - 1."""
-    return [st for st in range(max(count - W - 1, 0))
-            if row_episode[(oldest + st) % H] == row_episode[(oldest + st + W) % H]]
+    draws starts below epoch_len - WINDOW_SIZE - 1. Returns a range when every start is
+    valid (the oldest and the newest row share one episode: no scan), else an int64 array."""
+    span = max(count - W - 1, 0)
+    ep = np.asarray(row_episode)
+    if span == 0 or ep[oldest] == ep[(oldest + count - 1) % H]:
+        return range(span)
+    chrono = np.roll(ep, -oldest)[:count]                 # rows oldest .. newest
+    return np.flatnonzero(chrono[:span] == chrono[W:W + span])
 
 
 class DeviceReplay:
@@ -44,7 +50,7 @@ class DeviceReplay:
         self.count = 0
         # episode id of every ring row (all envs record in lockstep, so one id per row)
         self.episode = 0
-        self._row_ep = [0] * capacity
+        self._row_ep = np.zeros(capacity, dtype=np.int64)
         self._starts = None           # device tensor of valid starts when some windows straddle episodes
         self._starts_key = None
 
@@ -77,13 +83,16 @@ class DeviceReplay:
         dev = self.days.device
         gdev = generator.device if generator is not None else dev
         oldest = (self.head - self.count) % self.H
-        key = (oldest, self.count, self._row_ep[oldest], self._row_ep[(oldest + self.count - 1) % self.H])
-        if self._starts_key != key:
+        first, last = int(self._row_ep[oldest]), int(self._row_ep[(oldest + self.count - 1) % self.H])
+        key = None if first == last else (oldest, self.count, first, last)
+        if key is None:                    # one episode in the ring: every start (no scan, no upload)
+            self._starts_key, self._starts = None, None
+        elif self._starts_key != key:
             self._starts_key = key
             ok = valid_starts(self._row_ep, oldest, self.count, self.W, self.H)
-            if not ok:
+            if len(ok) == 0:
                 raise ValueError("no episode holds W + 1 recorded steps")
-            self._starts = None if len(ok) == span else torch.tensor(ok, dtype=torch.int64, device=gdev)
+            self._starts = None if len(ok) == span else torch.as_tensor(ok, dtype=torch.int64).to(gdev)
         if self._starts is None:
             st = torch.randint(0, span, (batch_size,), generator=generator, device=gdev)
         else:

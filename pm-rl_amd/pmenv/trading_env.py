@@ -21,6 +21,7 @@ round trip per call — the slow path; keep tensors on the GPU for throughput), 
 the reward and `.value` come back on the host as the reference returns them.
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -32,6 +33,15 @@ _CPU = torch.device("cpu")
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _version(t):
+    """t's in-place write counter; None for inference-mode tensors, which keep none
+    (their edits are then assumed on every step)."""
+    try:
+        return t._version
+    except RuntimeError:
+        return None
 
 
 class RingView:
@@ -106,7 +116,8 @@ class TradingEnv:
             raise ValueError("invalid env shape")
         off = (ctypes.c_size_t * _abi.STATE_FIELDS)()
         _abi.check(self._lib.pmenv_state_layout(ctypes.byref(self._c), off), None, "pmenv_state_layout")
-        self._state = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        with torch.inference_mode(False):      # a normal tensor: its views count in-place writes
+            self._state = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
         h = ctypes.c_void_p()
         torch.cuda.synchronize(self.device)
         _abi.check(self._lib.pmenv_create_in(ctypes.byref(self._c), self.device.index, _ptr(self._state),
@@ -114,20 +125,28 @@ class TradingEnv:
         self._h = h
         B, N, W = self.cfg.num_envs, self.cfg.num_assets, self.cfg.window
         s = self._state
-        self._value = s[off[0]:off[0] + 8 * B].view(torch.float64)
-        self._stat_a = s[off[1]:off[1] + 8 * B].view(torch.float64)
-        self._stat_b = s[off[2]:off[2] + 8 * B].view(torch.float64)
-        self._counter = s[off[3]:off[3] + 4 * B].view(torch.int32)
-        self._ring = s[off[4]:off[4] + 4 * B * W * N].view(torch.float32).view(B, W, N)
-        self._nonfinite = s[off[5]:off[5] + 8].view(torch.int64)
-        self._last_close = s[off[6]:off[6] + 4 * B * N].view(torch.float32).view(B, N)
-        self._w_new = s[off[7]:off[7] + 4 * B * N].view(torch.float32).view(B, N)
+        with torch.inference_mode(False):
+            self._value = s[off[0]:off[0] + 8 * B].view(torch.float64)
+            self._stat_a = s[off[1]:off[1] + 8 * B].view(torch.float64)
+            self._stat_b = s[off[2]:off[2] + 8 * B].view(torch.float64)
+            self._counter = s[off[3]:off[3] + 4 * B].view(torch.int32)
+            self._ring = s[off[4]:off[4] + 4 * B * W * N].view(torch.float32).view(B, W, N)
+            self._nonfinite = s[off[5]:off[5] + 8].view(torch.int64)
+            self._last_close = s[off[6]:off[6] + 4 * B * N].view(torch.float32).view(B, N)
+            self._w_new = s[off[7]:off[7] + 4 * B * N].view(torch.float32).view(B, N)
         self.weights = RingView(self)
         self._obs_shape = (B, N, W, self.cfg.features)
         self._args = _abi.PmenvStepArgs()          # reused: every field is set on every step
         self.track_info = track_info
         self._unbatched = False
         self._host_io = False               # the last reset/step came with CPU tensors
+        # caller edits between steps (trading_env.py:102-105: the features are the caller's):
+        # the version counters of the state blob (shared by .value and every other view)
+        # and of the last in-place window, as this wrapper left them; a change tells the
+        # handle to re-read what its one-launch step keeps from the previous step
+        self._state_ver = _version(self._state)
+        self._win = None
+        self._win_ver = -1
         self.set_step_impl(step_impl)
         self.info = None
         self._reset_info()
@@ -214,6 +233,9 @@ class TradingEnv:
                    "pmenv_reset")
         if dev_features is not features:
             features.copy_(dev_features)
+        self._state_ver = _version(self._state)
+        if dev_features is not None:
+            self._watch(dev_features)
         if mask is None:
             self._reset_info()
         return features
@@ -290,6 +312,8 @@ class TradingEnv:
                 raise ValueError("out must have the same shape as features")
             args.obs_out = out.data_ptr()
         args.reward = r.data_ptr()
+        stream = self._stream()
+        self._edits(features if (br is not None and out is None) else None, stream)
         ret = w = None
         if weights_out is not None:
             if weights_out.dtype != torch.float32 or not weights_out.is_contiguous() or \
@@ -302,7 +326,9 @@ class TradingEnv:
             if weights_out is None:
                 w = torch.empty(B, N, dtype=torch.float32, device=self.device)
                 args.weights = w.data_ptr()
-        _abi.check(self._lib.pmenv_step_ex(self._h, ctypes.byref(args), self._stream()), self._h, "pmenv_step")
+        _abi.check(self._lib.pmenv_step_ex(self._h, ctypes.byref(args), stream), self._h, "pmenv_step")
+        if out is None and br is not None:
+            self._watch(features)
         if self.track_info:
             # trading_env.py:80,85,90,100
             self.info["values"].append(self._value.clone())
@@ -311,6 +337,24 @@ class TradingEnv:
             self.info["rewards"].append(r)
         self._unbatched = unb
         return (r[0] if unb else r), (features if out is None else out)
+
+    def _watch(self, window):
+        """Remember the window as the handle left it (it is stepped in place next)."""
+        self._win = weakref.ref(window)
+        self._win_ver = _version(window)
+
+    def _edits(self, window, stream):
+        """Tell the handle what the caller wrote since the last call: the state blob
+        (e.g. `env.value[:] = ...`) -> pmenv_state_written; the in-place window (an edit,
+        or a different tensor, possibly at the same address) -> pmenv_window_written."""
+        sv = _version(self._state)
+        if sv is None or sv != self._state_ver:
+            _abi.check(self._lib.pmenv_state_written(self._h, stream), self._h, "pmenv_state_written")
+            self._state_ver = sv
+        elif window is not None and (self._win is None or self._win() is not window or
+                                     self._win_ver is None or _version(window) != self._win_ver):
+            _abi.check(self._lib.pmenv_window_written(self._h, _ptr(window), stream), self._h,
+                       "pmenv_window_written")
 
     def advance(self, action, features, bar, prices=None, out=None):
         """Fused step: window advance + bar append (see step)."""

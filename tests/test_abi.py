@@ -47,7 +47,7 @@ def test_abi_version_and_cfg_defaults_match_reference_config():
     # config/base.py:47-53
     assert c.init_cash == 25000 and c.commission == 0.0 and c.reward_scale == 1.0
     assert c.risk_free_rate == 0.04 and c.reward_kind == 0
-    assert c.norm_mode == 0 and c.ring_mode == 0 and c.ret_mode == 2 and c.mu_tol == 1e-10   # ret: AUTO
+    assert c.norm_mode == 0 and c.ring_mode == 0 and c.ret_mode == 0 and c.mu_tol == 1e-10   # ret: GROSS
     assert ctypes.sizeof(_abi.PmenvCfg) == 88
 
 

@@ -53,28 +53,50 @@ def test_bench_refuses_a_knob():
     assert p.returncode != 0 and "PMENV_" in (p.stderr + p.stdout)
 
 
-def test_bench_two_ranks_rehearsal():
-    """The driver's N > 1 launch (torch.distributed.run, one process per rank) with both
-    ranks on the one GPU over gloo (RCCL refuses two ranks on a device): weak scaling,
-    value = both ranks' env-steps over the max-over-ranks time, the moments all-reduce
-    recorded, parity on every rank."""
+def _two_ranks(*extra):
     import socket
-    import torch
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--dist-backend", "gloo", "--envs-per-gpu", "2048", "--steps", "8", "--warmup", "2", "--alt-steps", "0"]
+           "--dist-backend", "gloo", "--steps", "8", "--warmup", "2", "--alt-steps", "0", *extra]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    assert abs(d["value"] - 2 * 2048 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_rehearsal():
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank) with both
+    ranks on the one GPU over gloo (RCCL refuses two ranks on a device), by default: the
+    north star's strong-scaled workload, 65,536 envs in total sharded 32,768 per rank,
+    value = all envs' steps over the max-over-ranks time, the moments all-reduce
+    recorded, parity on every rank, the weak-scaled workload beside it under alt_weak."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _two_ranks("--alt-weak-steps", "4")
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_envs"] == 65536 and d["config"]["envs_per_gpu"] == 32768
+    assert d["config"]["per_rank"]["envs"] == 32768 and "step_path" in d["config"]["per_rank"]
+    assert abs(d["value"] - 65536 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
     assert d["collective"]["backend"] == "gloo" and d["collective"]["count_all_ranks"] > 0
     assert d["parity_sample"]["obs_bit_exact_all_ranks"] is True
+    assert d["parity_sample"]["reward_max_rel_all_ranks"] <= 1e-6
     assert d["cpu_baseline"] is None                     # rank 0 at N = 1 only
+    w = d["alt_weak"]
+    assert w["scaling"] == "weak" and w["envs_per_gpu"] == 65536 and w["global_envs"] == 131072
+    assert w["value"] > 0 and w["nonfinite_envs"] == 0
+
+
+def test_bench_two_ranks_weak():
+    """--envs-per-gpu keeps the weak-scaled form: per-rank work fixed as N grows."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _two_ranks("--envs-per-gpu", "2048")
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["global_envs"] == 4096
+    assert abs(d["value"] - 2 * 2048 * 1e3 / d["ms_per_step"]) <= 1e-6 * d["value"]
+    assert d["parity_sample"]["obs_bit_exact_all_ranks"] is True

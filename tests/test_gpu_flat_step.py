@@ -217,6 +217,110 @@ def test_gpu_flat_graph_capture_and_replay():
     assert day <= D
 
 
+def test_gpu_flat_graph_captures_a_reset_before_its_steps():
+    """A hipGraph whose first node is a reset (masked) followed by flat steps, captured on a
+    handle that was host-sequenced until then: the captured reset clears the snapshot's
+    valid word, so every replay re-primes from the reset state — replays 2, 3, ... included,
+    where a validity left at 1 by the previous replay would compose straddling envs from
+    the pre-reset snapshot. Equal to an eager two-launch env doing the same, bit for bit."""
+    import ctypes
+    from pmenv import TradingEnv, synth, _abi
+    B, N, W, T, D = 2048, 30, 50, 3, 40
+    ser = synth.series(W + D, B, N, seed=17, device=DEV)
+    act = synth.actions(D, B, N, seed=18, device=DEV)
+    ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
+    obs_a = synth.window_from_series(ser, W)
+    obs_b = obs_a.clone()
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    for day in range(2):                                   # host-sequenced flat steps first
+        ea.step(act[day], obs_a, bar=ser[W + day])
+        eb.step(act[day], obs_b, bar=ser[W + day])
+    assert torch.equal(obs_a, obs_b)
+    lib = _abi.load()
+    mask = (torch.rand(B, device=DEV, generator=torch.Generator(DEV).manual_seed(2)) < 0.5).to(torch.uint8)
+    act_buf = torch.empty(T, B, N, device=DEV)
+    bar_buf = torch.empty(T, B, N, 4, device=DEV)
+    rew_b = torch.empty(T, B, device=DEV)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    with torch.cuda.graph(g):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _abi.check(lib.pmenv_reset(eb._h, p(obs_b), p(mask), s), eb._h)
+        for t in range(T):
+            _abi.check(lib.pmenv_step(eb._h, p(act_buf[t]), None, p(bar_buf[t]), p(obs_b), p(rew_b[t]), s), eb._h)
+    assert "device-sequenced" in eb.step_path
+    day = 2
+    for rep in range(4):
+        act_buf.copy_(act[day:day + T])
+        bar_buf.copy_(ser[W + day:W + day + T])
+        g.replay()
+        ea.reset(obs_a, mask=mask)
+        ref = torch.stack([ea.step(act[day + t], obs_a, bar=ser[W + day + t])[0] for t in range(T)])
+        torch.cuda.synchronize()
+        assert torch.equal(ref, rew_b), f"replay {rep}: rewards"
+        assert torch.equal(obs_a, obs_b) and torch.equal(ea.value, eb.value), f"replay {rep}: windows / values"
+        assert torch.equal(ea._counter, eb._counter), f"replay {rep}: counters"
+        day += T
+    ra, _ = ea.step(act[day], obs_a, bar=ser[W + day])     # eager after the replays
+    rb, _ = eb.step(act[day], obs_b, bar=ser[W + day])
+    assert torch.equal(ra, rb) and torch.equal(obs_a, obs_b)
+
+
+def test_gpu_flat_caller_edits_between_steps():
+    """The features are the caller's (trading_env.py:102-105: the reference keeps no copy
+    and honours every edit). At the BASELINE shape the caller, between steps and without a
+    reset, rescales the market channels of the in-place window, writes env.value, and hands
+    in the window as a new tensor at the old one's address: the flat one-launch step (tile
+    halo and state snapshot from the previous step) equals the two-launch path (which
+    keeps nothing) bit for bit, because TradingEnv tells the handle what changed
+    (pmenv_window_written / pmenv_state_written). The wrapper's check costs well under a
+    microsecond of host time per step."""
+    import time
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 65536, 30, 50, 12
+    ser = synth.series(W + T, B, N, seed=31, device=DEV)
+    act = synth.actions(T, B, N, seed=32, device=DEV)
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
+    assert envs[0].step_path.endswith("step_flat_kernel (in place)")
+    obs = [synth.window_from_series(ser, W) for _ in envs]
+    for e, o in zip(envs, obs):
+        e.reset(o)
+    reused = 0
+    for t in range(T):
+        for i, e in enumerate(envs):
+            if t in (2, 7):                                # edit the window in place (every tile seam)
+                obs[i][..., :4].mul_(1.0009765625)
+            if t in (3, 9):                                # write the state through .value
+                e.value.mul_(0.75)
+            if t == 5:                                     # a new tensor, likely at the same address
+                keep = obs[i].clone()
+                keep[..., 3].mul_(0.998046875)
+                old = obs[i].data_ptr()
+                obs[i] = None
+                obs[i] = torch.empty_like(keep)
+                obs[i].copy_(keep)
+                del keep
+                reused += obs[i].data_ptr() == old
+        rs = [e.step(act[t], o, bar=ser[W + t])[0] for e, o in zip(envs, obs)]
+        assert torch.equal(rs[0], rs[1]), f"step {t}: rewards"
+        assert torch.equal(obs[0], obs[1]), f"step {t}: windows"
+        assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
+    print(f"new window at the old address: {reused} of 2")
+    e, o = envs[0], obs[0]
+    st = e._stream()
+    n = 20000
+    t0 = time.perf_counter()
+    for _ in range(n):
+        e._edits(o, st)
+        e._watch(o)
+    per = (time.perf_counter() - t0) / n
+    print(f"edit check + watch: {per * 1e6:.3f} us per step")
+    assert per < 2e-6
+
+
 def test_gpu_flat_path_rules():
     """FLAT takes F = 5, W >= 2, N <= 64 windows of >= 148 chunks (at most one env per
     wave of a tile: 256 x 4 from 511 chunks, 512 x 2 below); a forced FLAT that does not

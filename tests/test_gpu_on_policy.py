@@ -93,6 +93,21 @@ def test_gpu_compact_rollout_rematerialises_the_env_windows(ring, B, N, W, T):
                                                                                                     device=DEV))
     assert s.shape == (3, N, W, 5) and p.shape == (3, N, 1) and v_prev.shape == (3, 1, 1)
     assert buf.nbytes() < 4 * (T + 1) * B * N * 4 + 64 * B      # O(T * B * N): no windows kept
+    # a C caller's misaligned output view (4 B past a 16-B boundary) takes the dword row
+    # form instead of the tile's 16-B stores: the same windows
+    import ctypes
+    from pmenv import _abi
+    ti = torch.tensor([T, 1, T // 2], dtype=torch.int32, device=DEV)
+    ei = torch.tensor([0, B - 1, B // 2], dtype=torch.int32, device=DEV)
+    raw = torch.full((3 * N * W * 5 + 4,), -1.0, device=DEV)
+    mis = raw[1:1 + 3 * N * W * 5]
+    assert mis.data_ptr() % 16 == 4
+    st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    pp = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    _abi.check(_abi.load().pmenv_rollout_gather(pp(m.bars), m.bars.shape[0], N, 5, W, pp(buf.start), pp(buf.w), T, B,
+                                                _abi.RING_MODES[ring], pp(ti), pp(ei), 3, pp(mis), st))
+    assert torch.equal(mis.view(3, N, W, 5), buf.windows(ti, ei))
+    assert bool((raw[0] == -1.0) & (raw[-3:] == -1.0).all())         # nothing written outside the view
 
 
 def test_gpu_on_policy_compact_loop():

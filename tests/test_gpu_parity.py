@@ -187,6 +187,8 @@ MODES = [
     dict(reward="diff_sharpe", sharpe_eta=0.05),
     dict(commission=0.0025),
     dict(commission=0.01, ret="net", reward="diff_sharpe"),
+    dict(commission=0.0025, reward="returns"),                  # default GROSS: info["returns"] as :88
+    dict(commission=0.0025, ret="auto", reward="sharpe_ratio"),  # opt-in AUTO: net for reward.py kinds
     dict(norm="or"),
     dict(reward_scale=100.0, init_cash=1e6),
 ]

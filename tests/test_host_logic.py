@@ -1,5 +1,6 @@
 """Host-side logic that needs no GPU: config validation, sharding, the wrapper's
 shape checks, and the bench's algorithmic byte model."""
+import numpy as np
 import pytest
 
 from pmenv.config import EnvConfig
@@ -142,12 +143,24 @@ def test_replay_valid_starts_stay_inside_one_episode():
     W, H = 3, 10
     # rows 0..9 written in order; episodes 0 (rows 0-5) then 1 (rows 6-9), oldest = 0
     ep = [0] * 6 + [1] * 4
-    assert valid_starts(ep, 0, 10, W, H) == [0, 1, 2]
+    assert list(valid_starts(ep, 0, 10, W, H)) == [0, 1, 2]
     # the same ring after 4 more adds of episode 2 (rows 0-3 overwritten, oldest = 4)
     ep = [2] * 4 + [0, 0, 1, 1, 1, 1]
-    got = valid_starts(ep, 4, 10, W, H)                  # st counts from the oldest row (row 4)
+    got = list(valid_starts(ep, 4, 10, W, H))            # st counts from the oldest row (row 4)
     for st in got:
         rows = [(4 + st + i) % H for i in range(W + 1)]
         assert len({ep[r] for r in rows}) == 1
     assert got == [2]                                      # rows 6..9 are the only whole window
-    assert valid_starts([5] * H, 0, H, W, H) == list(range(H - W - 1))
+    one = valid_starts([5] * H, 0, H, W, H)               # one episode: every start, no scan
+    assert isinstance(one, range) and list(one) == list(range(H - W - 1))
+    # the vectorised scan against the per-start definition on random rings
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        H = int(rng.integers(W + 2, 40))
+        count = int(rng.integers(0, H + 1))
+        oldest = int(rng.integers(0, H))
+        chrono = np.sort(rng.integers(0, 4, count))        # ids grow along the ring
+        ring = np.zeros(H, dtype=np.int64)
+        ring[(oldest + np.arange(count)) % H] = chrono
+        want = [st for st in range(max(count - W - 1, 0)) if ring[(oldest + st) % H] == ring[(oldest + st + W) % H]]
+        assert list(valid_starts(ring, oldest, count, W, H)) == want
