@@ -186,6 +186,7 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
 /* Which kernels the advance path launches for this handle's shape (diagnostics):
  * "<obs_out path> (obs_out) | <in-place path> (in place)", each either
  * "step_flat_kernel" (the whole step in one launch over 16 KiB window tiles),
+ * "step_flat_vec_kernel" (the same for 64 < N <= 512),
  * "step_env_kernel" (the whole step in one launch, one workgroup per env) or
  * "<scalar step>+<window stream>"
  * (two launches); or "step_advance_lds_kernel" (single-launch fallback, any F). */
@@ -196,7 +197,8 @@ const char* pmenv_step_path(const pmenv* h);
  * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
  * kernel followed by the window stream (F = 5, 16-B granular env windows); FLAT forces
  * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:
- * F = 5, W >= 2, N <= 64, env windows of >= 148 16-B chunks). Returns PMENV_ERR_ARG
+ * F = 5, W >= 2, env windows of >= 148 16-B chunks, N <= 64 — or, as step_flat_vec_kernel,
+ * 64 < N <= 512 with W >= 14). Returns PMENV_ERR_ARG
  * (handle unchanged) when the shape does not fit the requested path. For N <= 64 every
  * path gives the same bits; the N > 64 scalar-step forms reduce in another order.
  *

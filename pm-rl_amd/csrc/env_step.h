@@ -334,17 +334,23 @@ __device__ __forceinline__ ScalarIn scalar_load_row(const StepParams& p, int b, 
     return in;
 }
 
-// SNAP (step_flat_kernel): only the env's owner workgroup (`owner`) writes the state,
-// reward and ring slot, and it also writes the next step's snapshot (sv_out .. slc_out)
-template <int L, bool ROW = false, bool SNAP = false>
-__device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int lane, const ScalarIn& in,
-                                               int32_t& k_before, bool owner = true) {
+// The scalar step in two halves. scalar_core computes what the window's compose needs
+// — the normalised weights, the commission factor, the portfolio value and w' — and
+// nothing else; scalar_tail does every state write and the return / reward (lane 0's
+// f64 division, log and statistics). The one-launch steps run the tail after the
+// window's barrier and stores, so the barrier waits for the core only.
+struct ScalarMid {
+    double value, V;   // portfolio value after the step, mu-scaled value before it
+    float wp, cn;      // the lane's w' (0 past N) and today's close
+    int32_t k;         // the counter before the step
+};
+
+template <int L, bool ROW = false>
+__device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int lane, const ScalarIn& in) {
     const int n = lane % L;
-    const int N = p.N, W = p.W;
+    const int N = p.N;
     const bool env_ok = b < p.B;
     const bool act = env_ok && n < N;
-    const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
-    const int32_t k = in.k;
     const double v_prev = in.v_prev;
     const double a = (double)in.a;
     const float wlf = in.wlf;
@@ -366,16 +372,21 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
         }
     }
 
-    // :58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min(action) < 0
+    // :58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min(action) < 0.
+    // AND mode with every group's sum close to 1 (simplex actions) cannot normalise:
+    // the min reduction is skipped (wave-uniform), the result is the same
     const double sum = group_sum<L>(act ? a : 0.0, lane);
-    double mn = group_min<L>(act ? a : INFINITY, lane);
-    const bool nan_here = act && isnan(a);
-    const uint64_t nan_mask = __ballot(nan_here);
-    const uint64_t gmask = L == 64 ? ~0ull : (lane < 32 ? 0xFFFFFFFFull : 0xFFFFFFFF00000000ull);
-    if (nan_mask & gmask) mn = NAN;               // torch.min propagates NaN
     const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
-    const bool negative = mn < 0.0;
-    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    bool norm = false;
+    if (p.norm_mode != PMENV_NORM_AND || __any(not_close)) {
+        double mn = group_min<L>(act ? a : INFINITY, lane);
+        const bool nan_here = act && isnan(a);
+        const uint64_t nan_mask = __ballot(nan_here);
+        const uint64_t gmask = L == 64 ? ~0ull : (lane < 32 ? 0xFFFFFFFFull : 0xFFFFFFFF00000000ull);
+        if (nan_mask & gmask) mn = NAN;           // torch.min propagates NaN
+        const bool negative = mn < 0.0;
+        norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    }
     double w = a;
     if (__any(norm)) {
         double shift = 0.0;
@@ -407,39 +418,60 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
         V = mu * V;
     }
 
-    // :78-79 portfolio value; :83-84 w' = portfolio / value -> ring slot (1 + k) % W
+    // :78-79 portfolio value; :83-84 w' = portfolio / value
     const double pv = act ? V * (w * y) : 0.0;
-    const double value = group_sum<L>(pv, lane);
+    ScalarMid m;
+    m.value = group_sum<L>(pv, lane);
+    m.V = V;
+    m.wp = act ? (float)(pv / m.value) : 0.0f;
+    m.cn = cn;
+    m.k = in.k;
+    return m;
+}
+
+// SNAP (step_flat_kernel): only the env's owner workgroup (`owner`) writes the state,
+// reward and ring slot, and it also writes the next step's snapshot (sv_out .. slc_out)
+template <int L, bool SNAP = false>
+__device__ __forceinline__ void scalar_tail(const StepParams& p, int b, int lane, const ScalarIn& in,
+                                            const ScalarMid& m, bool owner = true) {
+    const int n = lane % L;
+    const int N = p.N, W = p.W;
+    const bool env_ok = b < p.B;
+    const bool act = env_ok && n < N;
+    const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
+    const int32_t k = m.k;
+    const double value = m.value, V = m.V;
+    // :83-84 ring.update(w') at slot idx = (1 + k) % W
     const int slot = (int)((1 + (int64_t)k) % W);
     const bool wr = !SNAP || owner;
     if (act && wr) {
-        const float wp = (float)(pv / value);     // the value returned below
+        const float wp = m.wp;
         p.ring[(size_t)b * W * N + (size_t)slot * N + n] = wp;
         p.w_new[i] = wp;
         if (p.weights) p.weights[i] = wp;
-        if (p.bar) p.last_close[i] = cn;
+        if (p.bar) p.last_close[i] = m.cn;
         if (SNAP) {
             if (p.commission > 0.0) p.sw_out[i] = wp;      // get_last() feeds only the fixed point
-            p.slc_out[i] = cn;
+            p.slc_out[i] = m.cn;
         }
     }
     if (env_ok && n == 0 && wr) {
         // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
-        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
+        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / in.v_prev;
         double r;
         switch (p.reward_kind) {
         case PMENV_REWARD_RETURN:
             r = ret * p.scale;
             break;
         case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
-            double m = (double)(k + 1);
+            double mm = (double)(k + 1);
             double mean = in.sa, m2 = in.sb;
             double d = ret - mean;
-            mean += d / m;
+            mean += d / mm;
             m2 += d * (ret - mean);
             p.sa[b] = mean;
             p.sb[b] = m2;
-            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
+            r = mm < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (mm - 1.0)) * p.scale;
             break;
         }
         case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
@@ -463,8 +495,17 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
         if (p.ret) p.ret[b] = ret;
         if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
     }
-    k_before = k;
-    return act ? (float)(pv / value) : 0.0f;
+}
+
+// the whole scalar step: core, then tail; returns the lane's w' (0 past N) and the
+// counter before the step
+template <int L, bool ROW = false, bool SNAP = false>
+__device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int lane, const ScalarIn& in,
+                                               int32_t& k_before, bool owner = true) {
+    const ScalarMid m = scalar_core<L, ROW>(p, b, lane, in);
+    scalar_tail<L, SNAP>(p, b, lane, in, m, owner);
+    k_before = m.k;
+    return m.wp;
 }
 
 // P env groups per wave in sequence, all their loads issued first: P times the

@@ -520,6 +520,34 @@ void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
 }
 #endif
 
+// step_flat_vec_kernel (64 < N <= 512): A strided assets per lane, as pick_k1_vec's
+// packed two-launch scalar step, so the two paths give the same bits
+template <int A, int BK, int VV>
+void launch_flat1_vec_g(const StepParams& p, uint32_t qtot, unsigned grid, bool out, int pol, hipStream_t stream) {
+    if (out) {
+        if (pol == 1) step_flat_vec_kernel<A, BK, VV, 1, true><<<grid, BK, 0, stream>>>(p, qtot);
+        else step_flat_vec_kernel<A, BK, VV, 0, true><<<grid, BK, 0, stream>>>(p, qtot);
+    } else {
+        if (pol == 1) step_flat_vec_kernel<A, BK, VV, 1, false><<<grid, BK, 0, stream>>>(p, qtot);
+        else step_flat_vec_kernel<A, BK, VV, 0, false><<<grid, BK, 0, stream>>>(p, qtot);
+    }
+}
+
+template <int A>
+void launch_flat1_vec_a(const pmenv* h, const StepParams& p, unsigned grid, bool out, int pol, hipStream_t stream) {
+#ifdef PMENV_AB
+    if (h->flat1_block == 128) { launch_flat1_vec_g<A, 128, 8>(p, h->flat_qtot, grid, out, pol, stream); return; }
+#endif
+    launch_flat1_vec_g<A, 256, 4>(p, h->flat_qtot, grid, out, pol, stream);
+}
+
+void launch_flat1_vec(const pmenv* h, const StepParams& p, unsigned grid, bool out, int pol, hipStream_t stream) {
+    const int N = h->cfg.num_assets;
+    if (N <= 128) launch_flat1_vec_a<2>(h, p, grid, out, pol, stream);
+    else if (N <= 256) launch_flat1_vec_a<4>(h, p, grid, out, pol, stream);
+    else launch_flat1_vec_a<8>(h, p, grid, out, pol, stream);
+}
+
 // the whole step in one launch over the flat stream (step_flat.h): prime the snapshot
 // and the halo when something other than this kernel touched them, then one launch
 void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
@@ -565,6 +593,13 @@ void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     const int pol = out ? h->flat_pol : h->flat_ip_pol;
     const unsigned grid = (h->flat_qtot + (uint32_t)(h->flat1_block * h->flat1_vec) - 1) /
                           (uint32_t)(h->flat1_block * h->flat1_vec);
+    if (h->cfg.num_assets > 64) {                 // wide envs: the packed scalar step per tile
+        launch_flat1_vec(h, p, grid, out, pol, stream);
+        h->par = 1 - q;
+        h->snap_ok = true;
+        h->halo1_obs = out ? nullptr : p.obs;
+        return;
+    }
     size_t pad = 0;                               // tools: extra LDS per workgroup (occupancy study)
 #ifdef PMENV_AB
     pad = (size_t)h->flat1_lds_pad;
@@ -656,6 +691,7 @@ int flat1_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_AUTO) return h->flat1_auto;
     return 0;
 }
+
 
 }  // namespace
 
@@ -897,10 +933,14 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // 714 / 678 / 790 / 695 / 675 / 624 / 641 us; 128 x 8 loses 15 % at N = 16 and 64 where
     // 256 x 4 wins (profiles/ab_r02/r02w_flat1b_*, r02w_flat1c_*). A persistent form that
     // keeps the next tile's loads in flight needs 160 VGPRs (3 waves per SIMD): 2x slower.
+    // Wide envs (64 < N <= 512, step_flat_vec_kernel) also need the rows a tile touches
+    // per env to fit one wave's 64 staged bar rows (W >= 14 at F = 5 for 16 KiB tiles).
     auto flat1_fits = [&](int block, int vec) {
         const uint32_t cpw = (uint32_t)(block * vec);
         const uint32_t ne_max = h->per4 ? (cpw + h->per4 - 2u) / h->per4 + 1u : 0u;
-        return flat_ok && c.num_assets <= 64 && ne_max <= (uint32_t)(block / 64);
+        const int64_t span_rows = (4ll * cpw - 1) / (WF > 0 ? WF : 1) + 2;
+        const bool wide_ok = c.num_assets <= kWideMaxAssets && span_rows <= 64;
+        return flat_ok && (c.num_assets <= 64 || wide_ok) && ne_max <= (uint32_t)(block / 64);
     };
     // 128 x 8 (2 waves, 8 chunks per lane, the same 16 KiB tiles) where every tile holds at
     // most two envs (1,023 .. 1,999 chunks per env: N = 20 .. 39 at W = 50) and the window
@@ -926,11 +966,19 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->flat1_auto = 0;
     const int one_auto_base = h->one_auto;   // tools: PMENV_FLAT1=0 restores it
     (void)one_auto_base;
-    if (h->flat1_ok && h->flat1_block <= 256 && h->per4 >= 1000u && !(c.commission > 0.0)) {
+    if (h->flat1_ok && c.num_assets <= 64 && h->flat1_block <= 256 && h->per4 >= 1000u && !(c.commission > 0.0)) {
         if (win > (48ll << 20)) h->flat1_auto |= PMENV_FUSE_DB;
         if (win > (256ll << 20)) h->flat1_auto |= PMENV_FUSE_INPLACE;
         h->one_auto &= ~h->flat1_auto;
     }
+    // Wide envs (step_flat_vec_kernel, 64 < N <= 512): every tile an env straddles runs the
+    // env's whole packed scalar step, which costs more than the kernel boundary it saves
+    // from 4 assets per lane on: 8,192 x 500 in place 1,512 (128 x 8) / 1,605 (256 x 4)
+    // against 1,381 us on two launches, 2,048 x 200 143.5 vs 140.0; at 2 assets per lane
+    // it wins on HBM-streamed windows: 16,384 x 100 532.9 vs 549.7 us (profiles/ab_r03/
+    // wide_r03wide.err). AUTO gives it in-place windows > 1 GiB at N <= 128 without commission.
+    if (h->flat1_ok && c.num_assets > 64 && c.num_assets <= 128 && win > (1ll << 30) && !(c.commission > 0.0))
+        h->flat1_auto |= PMENV_FUSE_INPLACE;
 #ifdef PMENV_AB
     if (const char* knob = ab_knob("PMENV_FLAT1")) {   // tools: 1 = the flat step for every window, 0 = never
         h->flat1_auto = h->flat1_ok && atoi(knob) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
@@ -1084,7 +1132,7 @@ int pmenv_set_step_path(pmenv* h, int32_t path) {
     if (bits < 0 || fbits < 0) {
         set_err(h, "step path %d does not fit this shape (one launch: F = 5, W >= 2, N <= 64, window <= 64 KiB "
                    "of LDS; two launches: F = 5, 16-B granular env windows; flat: F = 5, W >= 2, N <= 64, "
-                   "16-B granular env windows of >= 148 chunks)", path);
+                   "16-B granular env windows of >= 148 chunks, N > 64 up to 512 with W >= 14)", path);
         return PMENV_ERR_ARG;
     }
     h->path = path;
@@ -1158,6 +1206,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
             launch_one(h, p, stream);
             return check_launch(h, "step_env_kernel");
         }
+
 #ifdef PMENV_AB
         if (ph == (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE) && (h->fused & fuse_bit)) {
             launch_fused(h, p, stream);
@@ -1208,7 +1257,7 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-        if (h->flat1 & bit) part[m] = "step_flat_kernel";
+        if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
         else if (h->one & bit) part[m] = "step_env_kernel";
         else if (h->fused & bit) part[m] = "advance_rows_kernel<fused>";
         else {

@@ -102,19 +102,63 @@ __device__ __forceinline__ void halo_store(const StepParams& p, const HaloRegs& 
     }
 }
 
-template <int L, int A, bool STR>
-__global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
-    const HaloRegs halo = halo_load(p);
-    constexpr int EPW = 64 / L;
-    const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    const int b = w * EPW + lane / L;
+// The packed scalar step in three parts, so the one-launch walk step (step_walk.h) can
+// put its window loads between the loads and the compute and run the state writes
+// after its stores: vec_load issues every load (none dependent on another; the bar
+// rows of a resident series follow the env's day index), vec_core computes the
+// normalised weights, mu, the value and the lanes' w', vec_tail writes the state and
+// the reward. scalar_step_vec_kernel runs the three in a row.
+template <int A>
+struct VecIn {
+    int32_t k;
+    double v_prev, sa, sb;
+    float a[A], wl[A], pl[A], cn[A];
+};
+
+template <int A>
+struct VecMid {
+    double value, V;
+    float wp[A];       // the lane's w' (0 for assets past N)
+};
+
+// SNAP (step_flat_vec_kernel): value, counter, get_last() and the last close from the
+// flat step's state snapshot of parity p (sv_in .. slc_in) instead of the canonical state.
+// get_last() feeds only the commission fixed point: without commission it is not read
+// (the descriptor has no records: no traffic), and vec_core never looks at it.
+template <int L, int A, bool STR, bool SNAP = false>
+__device__ __forceinline__ VecIn<A> vec_load(const StepParams& p, int b, int lane) {
     const int j = lane % L;
-    const int N = p.N, W = p.W, Fm = p.F - 1;
+    const int N = p.N, Fm = p.F - 1;
     const bool env_ok = b < p.B;
     const int bc = env_ok ? b : 0;
     const size_t row = (size_t)bc * N;
     const uint32_t nbytes = (uint32_t)p.B * (uint32_t)N * 4u;
+    VecIn<A> in;
+    in.k = SNAP ? p.sk_in[bc] : p.k[bc];
+    in.v_prev = SNAP ? p.sv_in[bc] : p.value[bc];
+    // reward statistics: only the tail's lane 0 reads them; the snapshot form (a tile's
+    // registers are scarce there) loads them in the tail
+    in.sa = SNAP ? 0.0 : p.sa[bc];
+    in.sb = SNAP ? 0.0 : p.sb[bc];
+    load_packed<L, A, STR>(p.action, nbytes, row, j, in.a);
+    load_packed<L, A, STR>(SNAP ? p.sw_in : p.w_new, p.commission > 0.0 ? nbytes : 0u, row, j,
+                           in.wl);                                        // get_last() (weight_buffer.py:28-30)
+    load_packed<L, A, STR>(p.prices ? p.prices : SNAP ? p.slc_in : p.last_close, nbytes, row, j, in.pl);
+    const float* barb = p.bar ? env_bar(p, bc) : nullptr;
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+        const int n = STR ? j + e * L : j * A + e;
+        const int nc = env_ok && n < N ? n : 0;
+        in.cn[e] = barb ? barb[(size_t)nc * Fm + p.close_ch] : NAN;
+    }
+    return in;
+}
+
+template <int L, int A, bool STR>
+__device__ __forceinline__ VecMid<A> vec_core(const StepParams& p, int b, int lane, const VecIn<A>& in) {
+    const int j = lane % L;
+    const int N = p.N;
+    const bool env_ok = b < p.B;
     int nn[A];                                    // the lane's assets
     bool act[A];
 #pragma unroll
@@ -122,44 +166,28 @@ __global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
         nn[e] = STR ? j + e * L : j * A + e;
         act[e] = env_ok && nn[e] < N;
     }
-
-    // every load first, none dependent on another (the bar rows of a resident series
-    // follow the env's day index)
-    const int32_t k = p.k[bc];
-    const double v_prev = p.value[bc];
-    const double sa = p.sa[bc], sb = p.sb[bc];
-    float a[A], wl[A], pl[A], cn[A];
-    load_packed<L, A, STR>(p.action, nbytes, row, j, a);
-    load_packed<L, A, STR>(p.w_new, nbytes, row, j, wl);                  // get_last() (weight_buffer.py:28-30)
-    load_packed<L, A, STR>(p.prices ? p.prices : p.last_close, nbytes, row, j, pl);
-    const float* barb = p.bar ? env_bar(p, bc) : nullptr;
-#pragma unroll
-    for (int e = 0; e < A; ++e) {
-        const int nc = act[e] ? nn[e] : 0;
-        cn[e] = barb ? barb[(size_t)nc * Fm + p.close_ch] : NAN;
-    }
-
-    // instrument.py:79: the relative is the correctly rounded fp32 quotient of today's
-    // close over the window's last close (caller prices when given)
-    double x[A], y[A];
+    double x[A];
     double s_loc = 0.0, mn_loc = INFINITY;
     bool nan_here = false;
 #pragma unroll
     for (int e = 0; e < A; ++e) {
-        x[e] = act[e] ? (double)a[e] : 0.0;
-        y[e] = !act[e] ? 1.0 : (p.bar && !p.prices) ? (double)(cn[e] / pl[e]) : (double)pl[e];
+        x[e] = act[e] ? (double)in.a[e] : 0.0;
         s_loc += x[e];
         mn_loc = fmin(mn_loc, act[e] ? x[e] : INFINITY);
-        nan_here |= act[e] && isnan(a[e]);
+        nan_here |= act[e] && isnan(in.a[e]);
     }
-    // trading_env.py:58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min < 0
+    // trading_env.py:58 normalise iff !isclose(sum, 1, atol=1e-6) AND (OR: trainer) min < 0;
+    // AND mode with every group's sum close to 1 cannot normalise (the min is skipped)
     const double sum = gred<L, 0>(s_loc, lane);
-    double mn = gred<L, 2>(mn_loc, lane);
-    const uint64_t gmask = L == 64 ? ~0ull : (((1ull << (L & 63)) - 1ull) << (lane & ~(L - 1)));
-    if (__ballot(nan_here) & gmask) mn = NAN;     // torch.min propagates NaN
     const bool not_close = !(fabs(sum - 1.0) <= 1e-6 + 1e-5);
-    const bool negative = mn < 0.0;
-    const bool norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    bool norm = false;
+    if (p.norm_mode != PMENV_NORM_AND || __any(not_close)) {
+        double mn = gred<L, 2>(mn_loc, lane);
+        const uint64_t gmask = L == 64 ? ~0ull : (((1ull << (L & 63)) - 1ull) << (lane & ~(L - 1)));
+        if (__ballot(nan_here) & gmask) mn = NAN;     // torch.min propagates NaN
+        const bool negative = mn < 0.0;
+        norm = p.norm_mode == PMENV_NORM_AND ? (not_close && negative) : (not_close || negative);
+    }
     double wv[A];
 #pragma unroll
     for (int e = 0; e < A; ++e) wv[e] = x[e];
@@ -185,12 +213,12 @@ __global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
     }
 
     // :67-75 commission fixed point (f64, capped), per env group
-    double V = v_prev;
+    double V = in.v_prev;
     if (p.commission > 0.0) {
         const double c = p.commission;
         const int g0 = lane & ~(L - 1);
         const double w0 = __shfl(wv[0], g0, 64);
-        const double wl0 = (double)__shfl(wl[0], g0, 64);
+        const double wl0 = (double)__shfl(in.wl[0], g0, 64);
         double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
         int it = 0;
         bool done = !(fabs(mu - mu_last) > p.mu_tol) || p.mu_max_iter <= 0;
@@ -198,7 +226,7 @@ __global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
             double part = 0.0;
 #pragma unroll
             for (int e = 0; e < A; ++e) {
-                const double d = (act[e] && nn[e] > 0) ? (double)wl[e] - mu * wv[e] : 0.0;
+                const double d = (act[e] && nn[e] > 0) ? (double)in.wl[e] - mu * wv[e] : 0.0;
                 part += d > 0.0 ? d : 0.0;        // torch.maximum(x, 0) as intended
             }
             const double tot = gred<L, 0>(part, lane);
@@ -212,47 +240,75 @@ __global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
         V = mu * V;
     }
 
-    // :78-79 portfolio value; :83-84 w' = portfolio / value -> ring slot (1 + k) % W
+    // :78-79 portfolio value; :83-84 w' = portfolio / value. instrument.py:79: the price
+    // relative is the correctly rounded fp32 quotient of today's close over the window's
+    // last close (caller prices when given), formed here where it is used
     double pv[A], pv_loc = 0.0;
 #pragma unroll
     for (int e = 0; e < A; ++e) {
-        pv[e] = act[e] ? V * (wv[e] * y[e]) : 0.0;
+        const double y = !act[e] ? 1.0 : (p.bar && !p.prices) ? (double)(in.cn[e] / in.pl[e]) : (double)in.pl[e];
+        pv[e] = act[e] ? V * (wv[e] * y) : 0.0;
         pv_loc += pv[e];
     }
-    const double value = gred<L, 0>(pv_loc, lane);
+    VecMid<A> m;
+    m.value = gred<L, 0>(pv_loc, lane);
+    m.V = V;
+#pragma unroll
+    for (int e = 0; e < A; ++e) m.wp[e] = act[e] ? (float)(pv[e] / m.value) : 0.0f;
+    return m;
+}
+
+// SNAP: only the env's owner workgroup (`owner`) writes, and it also writes the next
+// step's snapshot (sv_out .. slc_out), as scalar_tail
+template <int L, int A, bool STR, bool SNAP = false>
+__device__ __forceinline__ void vec_tail(const StepParams& p, int b, int lane, const VecIn<A>& in,
+                                         const VecMid<A>& m, bool owner = true) {
+    if (SNAP && !owner) return;
+    const int j = lane % L;
+    const int N = p.N, W = p.W;
+    const bool env_ok = b < p.B;
+    const int bc = env_ok ? b : 0;
+    const int32_t k = in.k;
+    const double value = m.value, V = m.V;
+    // :83-84 ring.update(w') at slot (1 + k) % W
     const int slot = (int)((1 + (int64_t)k) % W);
     float* ring_row = p.ring + (size_t)bc * W * N + (size_t)slot * N;
 #pragma unroll
     for (int e = 0; e < A; ++e) {
-        if (!act[e]) continue;
-        const int n = nn[e];
-        const float wp = (float)(pv[e] / value);
+        const int n = STR ? j + e * L : j * A + e;
+        if (!(env_ok && n < N)) continue;
+        const float wp = m.wp[e];
         ring_row[n] = wp;
         p.w_new[(size_t)bc * N + n] = wp;
         if (p.weights) p.weights[(size_t)bc * N + n] = wp;
-        if (p.bar) p.last_close[(size_t)bc * N + n] = cn[e];
+        if (p.bar) p.last_close[(size_t)bc * N + n] = in.cn[e];
+        if (SNAP) {
+            if (p.commission > 0.0) p.sw_out[(size_t)bc * N + n] = wp;
+            p.slc_out[(size_t)bc * N + n] = in.cn[e];
+        }
     }
     if (env_ok && j == 0) {
+        const double in_sa = SNAP ? p.sa[b] : in.sa, in_sb = SNAP ? p.sb[b] : in.sb;
         // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
-        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / v_prev;
+        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / in.v_prev;
         double r;
         switch (p.reward_kind) {
         case PMENV_REWARD_RETURN:
             r = ret * p.scale;
             break;
         case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
-            const double m = (double)(k + 1);
-            double mean = sa, m2 = sb;
+            const double mm = (double)(k + 1);
+            double mean = in_sa, m2 = in_sb;
             const double d = ret - mean;
-            mean += d / m;
+            mean += d / mm;
             m2 += d * (ret - mean);
             p.sa[b] = mean;
             p.sb[b] = m2;
-            r = m < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (m - 1.0)) * p.scale;
+            r = mm < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (mm - 1.0)) * p.scale;
             break;
         }
         case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
-            const double R = ret - 1.0, Am = sa, Bm = sb;
+            const double R = ret - 1.0, Am = in_sa, Bm = in_sb;
             const double dA = R - Am, dB = R * R - Bm, var = Bm - Am * Am;
             r = var > 1e-12 ? (Bm * dA - 0.5 * Am * dB) / (var * sqrt(var)) * p.scale : 0.0;
             p.sa[b] = Am + p.eta * dA;
@@ -264,10 +320,26 @@ __global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
         }
         p.value[b] = value;
         p.k[b] = k + 1;
+        if (SNAP) {
+            p.sv_out[b] = value;
+            p.sk_out[b] = k + 1;
+        }
         if (p.reward) p.reward[b] = (float)r;
         if (p.ret) p.ret[b] = ret;
         if (!isfinite(r) || !isfinite(value)) atomicAdd(p.nonfinite, 1ull);
     }
+}
+
+template <int L, int A, bool STR>
+__global__ __launch_bounds__(256) void scalar_step_vec_kernel(StepParams p) {
+    const HaloRegs halo = halo_load(p);
+    constexpr int EPW = 64 / L;
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int b = w * EPW + lane / L;
+    const VecIn<A> in = vec_load<L, A, STR>(p, b, lane);
+    const VecMid<A> m = vec_core<L, A, STR>(p, b, lane, in);
+    vec_tail<L, A, STR>(p, b, lane, in, m);
     halo_store(p, halo);
 }
 

@@ -11,14 +11,15 @@
 //   2. every wave issues its aligned 16-B window loads (wave w owns V of the env's
 //      1 KiB-aligned 64-chunk blocks, lane l chunk l of each: each load one aligned,
 //      coalesced 1 KiB) — nothing waits in between;
-//   3. wave 0 runs the scalar step (scalar_finish: normalisation :54-60, commission
-//      fixed point :62-75, value :77-79, w' :83-84 into the ring / w_new, return and
-//      reward :87-100, counter) while the window is in flight, and leaves w', the
-//      bar rows and the counter in LDS;
+//   3. wave 0 runs the scalar step up to w' (scalar_core: normalisation :54-60,
+//      commission fixed point :62-75, value :77-79, w' :83-84) while the window is in
+//      flight, and leaves w', the bar rows and the counter in LDS;
 //   4. every wave parks its chunks in the LDS image of the window; one barrier;
 //   5. each lane composes its output chunk from LDS neighbours (the shifted source
 //      floats 4c+5 .. 4c+8 = chunks c+1, c+2) and the env's w' / bar row, and stores
-//      it with one 16-B store (flat_compose, env_step.h).
+//      it with one 16-B store (flat_compose, env_step.h);
+//   6. wave 0 finishes the step (scalar_tail: w' into the ring / w_new, return and
+//      reward :87-100, counter) after its stores, off the barrier's critical path.
 //
 // The workgroup owns the whole env, so the in-place advance needs no halo and no
 // inter-workgroup ordering: every load of the env lands before any of its stores
@@ -78,12 +79,13 @@ __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4
         sh_wp[lane] = 0.5f;
         sh_bar[lane] = f4{1.f, 1.f, 1.f, 1.f};
         if (lane == 0) sh_k = 0;
-    } else if (wave == 0) {
-        int32_t kb;
-        const float wp = scalar_finish<64, true>(p, b, lane, sin, kb);
-        sh_wp[lane] = wp;
+    }
+    ScalarMid mid;
+    if (!(ABL & 1) && wave == 0) {
+        mid = scalar_core<64, true>(p, b, lane, sin);
+        sh_wp[lane] = mid.wp;
         sh_bar[lane] = sin.bar_ok ? sin.bar : f4{NAN, NAN, NAN, NAN};   // day outside the series: NaN bar
-        if (lane == 0) sh_k = kb;
+        if (lane == 0) sh_k = mid.k;
     }
     // 4. the window image
 #pragma unroll
@@ -122,6 +124,8 @@ __device__ __forceinline__ void step_env_body(const StepParams& p, uint32_t per4
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
         buf_store4<kAux>(rd, c * 16u, flat_compose(p, sd, un, sh));          // outside the env: dropped
     }
+    // 6. the rest of the scalar step after the stores: state, ring slot, return, reward
+    if (!(ABL & 1) && wave == 0) scalar_tail<64>(p, b, lane, sin, mid);
 }
 
 // Held to 80 SGPRs (the compiler spills ~20 to VGPR lanes): gfx950 admits

@@ -13,12 +13,15 @@
 //      state snapshot: value, counter, get_last(), last close);
 //   2. every wave issues its aligned 16-B window loads (one coalesced 1 KiB per wave
 //      instruction), and lanes 0-1 the two chunks past the tile (the halo);
-//   3. wave w < ne runs env (e_lo + w)'s scalar step (scalar_finish: f64 DPP
+//   3. wave w < ne runs env (e_lo + w)'s scalar step up to w' (scalar_core: f64 DPP
 //      reductions, bitwise the same as every other step path) while the window is in
 //      flight, and leaves w', the bar rows and the counter in LDS;
 //   4. the window image goes to LDS; ONE barrier;
 //   5. each lane composes its output chunks (shifted source from LDS neighbours, the
-//      env's bar / w' where a row's last day or weight slot falls) and stores them.
+//      env's bar / w' where a row's last day or weight slot falls) and stores them;
+//   6. wave w < ne finishes env (e_lo + w)'s step after the stores (scalar_tail: the
+//      state, ring slot and snapshot writes, lane 0's return and reward), so the barrier
+//      of step 4 waits only for what the compose needs (scalar_core: w').
 //
 // Several workgroups run the scalar step of an env that straddles their tiles; only the
 // workgroup holding the env's first chunk (its owner) writes the env's state, reward and
@@ -37,7 +40,7 @@
 // the parity and the snapshot's validity from device words and primes on the device; the
 // kernel then reads the parity from memory (below).
 #pragma once
-#include "env_step.h"
+#include "scalar_vec.h"
 
 namespace pmenv_dev {
 
@@ -105,15 +108,13 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t per4 = p.per4;
-    // 3. the scalar steps, one env per wave
+    // 3. the scalar steps' cores, one env per wave (their tails run after the stores)
+    ScalarMid mid;
     if (wave < t.ne) {
-        const int b = (int)t.e_lo + wave;
-        int32_t kb;
-        const bool owner = (uint64_t)b * per4 >= t.c0;                 // the env's first chunk is ours
-        const float wp = scalar_finish<64, true, true>(p, b, lane, t.sin, kb, owner);
-        sh_wp[wave][lane] = wp;
+        mid = scalar_core<64, true>(p, (int)t.e_lo + wave, lane, t.sin);
+        sh_wp[wave][lane] = mid.wp;
         sh_bar[wave][lane] = t.sin.bar_ok ? t.sin.bar : f4{NAN, NAN, NAN, NAN};   // day outside the series
-        if (lane == 0) sh_k[wave] = kb;
+        if (lane == 0) sh_k[wave] = mid.k;
     }
     // 4. the window image
 #pragma unroll
@@ -154,6 +155,36 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
         buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                     // past the end: dropped
         if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
     }
+    // 6. the scalar steps' tails: state, ring slot, snapshot and reward (the owner only)
+    if (wave < t.ne) {
+        const int b = (int)t.e_lo + wave;
+        const bool owner = (uint64_t)b * per4 >= t.c0;                 // the env's first chunk is ours
+        scalar_tail<64, true>(p, b, lane, t.sin, mid, owner);
+    }
+}
+
+// The device-sequenced step (p.seq set): take the parity C that flat_seq_kernel published
+// (nothing writes C during this launch) — swap the *_in / *_out snapshot and halo pointers
+// when it is 1 — and from workgroup 0 publish the next step's D, V and HOBS (nothing reads
+// them during this launch).
+template <bool OUT>
+__device__ __forceinline__ void flat_seq_enter(StepParams& p) {
+    if (!p.seq) return;
+    const int c = __builtin_amdgcn_readfirstlane(p.seq[1]);
+    if (c) {
+        const double* v = p.sv_in; p.sv_in = p.sv_out; p.sv_out = const_cast<double*>(v);
+        const int32_t* k = p.sk_in; p.sk_in = p.sk_out; p.sk_out = const_cast<int32_t*>(k);
+        const float* w = p.sw_in; p.sw_in = p.sw_out; p.sw_out = const_cast<float*>(w);
+        const float* l = p.slc_in; p.slc_in = p.slc_out; p.slc_out = const_cast<float*>(l);
+        const float* h = p.halo_in; p.halo_in = p.halo_out; p.halo_out = const_cast<float*>(h);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint64_t hobs = OUT ? 0ull : (uint64_t)(uintptr_t)p.obs;
+        p.seq[0] = 1 - c;
+        p.seq[2] = 1;
+        p.seq[4] = (int32_t)(uint32_t)hobs;
+        p.seq[5] = (int32_t)(uint32_t)(hobs >> 32);
+    }
 }
 
 // POL: cache policy of the window stream (0 default, 1 nt; tools A/B: 3 nt loads only,
@@ -174,29 +205,122 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void st
         const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = tile & 7, i = tile >> 3;
         tile = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
     }
-    if (p.seq) {
-        // device-sequenced step: the parity C that flat_seq_kernel published (nothing
-        // writes C during this launch); workgroup 0 publishes the next step's D, V and
-        // HOBS (nothing reads them during this launch)
-        const int c = __builtin_amdgcn_readfirstlane(p.seq[1]);
-        if (c) {
-            const double* v = p.sv_in; p.sv_in = p.sv_out; p.sv_out = const_cast<double*>(v);
-            const int32_t* k = p.sk_in; p.sk_in = p.sk_out; p.sk_out = const_cast<int32_t*>(k);
-            const float* w = p.sw_in; p.sw_in = p.sw_out; p.sw_out = const_cast<float*>(w);
-            const float* l = p.slc_in; p.slc_in = p.slc_out; p.slc_out = const_cast<float*>(l);
-            const float* h = p.halo_in; p.halo_in = p.halo_out; p.halo_out = const_cast<float*>(h);
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            const uint64_t hobs = OUT ? 0ull : (uint64_t)(uintptr_t)p.obs;
-            p.seq[0] = 1 - c;
-            p.seq[2] = 1;
-            p.seq[4] = (int32_t)(uint32_t)hobs;
-            p.seq[5] = (int32_t)(uint32_t)(hobs >> 32);
-        }
-    }
+    flat_seq_enter<OUT>(p);
     FlatTile<V> t;
     flat1_load<BLOCK, V, POL, OUT>(p, qtot, tile, t);
     flat1_process<BLOCK, V, POL, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
+}
+
+// ---------------------------------------------------------------- wide envs (64 < N <= 512)
+// step_flat_kernel with the packed scalar step (scalar_vec.h: A strided assets per lane,
+// the two-launch path's own loads and reductions, so the two give the same bits): an env
+// window there spans 4,000 - 32,000 chunks, so a 16 KiB tile holds parts of at most two
+// envs and most tiles one. Each tile runs the scalar step of the env(s) it holds — the
+// reductions need every asset — but stages only the rows it touches: the bar rows and w'
+// of at most 64 rows per env (host-checked), the same LDS as the narrow kernel. The
+// snapshot, the halo and the device sequencing are step_flat_kernel's.
+constexpr int kWideMaxAssets = 512;
+
+template <int A, int BLOCK, int V, int POL, bool OUT>
+__global__ __launch_bounds__(BLOCK) void step_flat_vec_kernel(StepParams p, uint32_t qtot) {
+    constexpr int kAuxL = POL == 1 ? 2 : 0, kAuxS = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64, F = 5;
+    __shared__ f4 sh4[CPW + 2];
+    __shared__ f4 sh_bar[WAVES][64];
+    __shared__ float sh_wp[WAVES][64];
+    __shared__ int32_t sh_k[WAVES], sh_rlo[WAVES];
+    const uint32_t tile = blockIdx.x;
+    flat_seq_enter<OUT>(p);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = p.N, WF = p.W * F;
+    const uint32_t per4 = p.per4;
+    const uint32_t c0 = tile * (uint32_t)CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const uint32_t e_lo = fdiv(c0, p.div_units);
+    const int ne = (int)(fdiv(c0 + nblk - 1u, p.div_units) - e_lo) + 1;   // <= WAVES (host-checked)
+    // 1. wave w < ne: env (e_lo + w)'s scalar loads and the bar rows the tile touches
+    VecIn<A> vin;
+    f4 brow = f4{0.f, 0.f, 0.f, 0.f};
+    int rlo = 0;
+    bool bar_ok = false;
+    const int b = (int)e_lo + wave;
+    if (wave < ne) {
+        vin = vec_load<64, A, true, true>(p, b, lane);
+        const uint64_t eb = (uint64_t)b * per4;
+        const uint32_t qa = (uint32_t)(max((uint64_t)c0, eb) - eb);                          // env-local chunks
+        const uint32_t qb = (uint32_t)(min((uint64_t)c0 + nblk - 1u, eb + per4 - 1u) - eb);  // in this tile
+        rlo = (int)fdiv(4u * qa, p.div_wf);
+        const int rhi = min((int)fdiv(4u * qb + 3u, p.div_wf), N - 1);
+        const float* barb = env_bar(p, b);
+        bar_ok = barb != nullptr;
+        const auto rb = make_rsrc(barb ? barb : p.bar, barb ? (uint32_t)(rhi + 1) * 16u : 0u);
+        brow = buf_load4<0>(rb, (uint32_t)(rlo + lane) * 16u);                             // rows past rhi: 0
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. the window stream and the halo
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    f4 own[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAuxL>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    const uint32_t ntiles = (qtot + CPW - 1) / CPW;
+    const uint32_t nh = tile + 1 < ntiles ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : p.halo_in + (size_t)tile * 8;
+    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    __builtin_amdgcn_sched_barrier(0);
+    // 3. the scalar steps (state, ring slot, snapshot and reward by the env's owner only)
+    if (wave < ne) {
+        const VecMid<A> mid = vec_core<64, A, true>(p, b, lane, vin);
+#pragma unroll
+        for (int e = 0; e < A; ++e) {
+            const int n = lane + 64 * e;
+            if ((unsigned)(n - rlo) < 64u) sh_wp[wave][n - rlo] = mid.wp[e];
+        }
+        sh_bar[wave][lane] = bar_ok ? brow : f4{NAN, NAN, NAN, NAN};                      // day outside the series
+        if (lane == 0) {
+            sh_k[wave] = vin.k;
+            sh_rlo[wave] = rlo;
+        }
+        const bool owner = (uint64_t)b * per4 >= c0;                    // the env's first chunk is ours
+        vec_tail<64, A, true, true>(p, b, lane, vin, mid, owner);
+    }
+    // 4. the window image
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
+    __syncthreads();
+    // 5. compose and store
+    const auto rd = make_rsrc((OUT ? p.obs_out : p.obs) + (size_t)c0 * 4, nblk * 16u);
+    const bool first_out = !OUT && tile > 0;                            // feeds the previous tile's halo
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);            // lanes past the end: any chunk
+        const uint32_t e = fdiv(q, p.div_units);
+        const int le = (int)(e - e_lo);
+        const uint32_t j0 = 4u * (q - e * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        FlatSide sd;
+        sd.kk = (int)(j0 - row * (uint32_t)WF);
+        sd.bar_nan = false;
+        sd.k = sh_k[le];
+        const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && sd.k >= p.W - 1);
+        const int slot_w =
+            (int)(((uint32_t)(1 + sd.k) - fdiv((uint32_t)(1 + sd.k), p.div_w) * (uint32_t)p.W) * F + (F - 1));
+        const bool need = sd.kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - sd.kk) <= 3u);
+        sd.xb = f4{0.f, 0.f, 0.f, 0.f};
+        sd.xwp = 0.f;
+        if (need) {
+            const int r = (int)row - sh_rlo[le];
+            sd.xb = sh_bar[le][r];
+            sd.xwp = sh_wp[le][r];
+        }
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        const f4 o = flat_compose(p, sd, un, sh);
+        buf_store4<kAuxS>(rd, (uint32_t)j * 16u, o);                    // past the end: dropped
+        if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
+    }
 }
 
 // The snapshot copy (sv_out .. slc_out <- the canonical state, when `snap`) and the halo

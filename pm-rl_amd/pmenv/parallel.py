@@ -1,8 +1,10 @@
 """Multi-GPU: envs shard embarrassingly across ranks (one process per GPU).
 
-The env step itself has no cross-env coupling, so the only exchange is the
+The env step itself has no cross-env coupling, so the env path's only exchange is the
 advantage-normalisation moments {count, sum, sum of squares} (24 bytes, f64) —
 one all-reduce per policy update over RCCL/xGMI (backend "nccl"), or gloo on CPU.
+A policy replicated over the ranks adds one gradient all-reduce per optimizer step
+(allreduce_grads: every parameter's gradient in one flat bucket).
 """
 import torch
 import torch.distributed as dist
@@ -45,3 +47,33 @@ def normalize(adv, group=None, eps=1e-8):
         m = local_moments_cpu(adv)
     _, mean, var = allreduce_moments(m, group)
     return (adv - mean) / (var ** 0.5 + eps)
+
+
+def world(group=None):
+    """Ranks in the default (or given) process group; 1 without torch.distributed."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
+
+
+def allreduce_grads(params, loss_sum, count, group=None):
+    """Average replicated parameters' gradients over every rank's samples: the per-rank
+    gradient SUMS, the loss sum and the sample count go through ONE all-reduce (a flat
+    f64 bucket: the gradients of a small policy are a few hundred KB, one latency-bound
+    exchange over xGMI), then every gradient is divided by the global count. Returns
+    (global loss sum, global count) as python floats."""
+    ps = [p for p in params if p.grad is not None]
+    dev = ps[0].grad.device if ps else torch.device("cpu")
+    parts = [p.grad.detach().reshape(-1).to(torch.float64) for p in ps]
+    extra = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64).reshape(()).to(dev),
+                         torch.tensor(float(count), dtype=torch.float64, device=dev)])
+    bucket = torch.cat(parts + [extra])
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
+    total, n = float(bucket[-2]), float(bucket[-1])
+    off = 0
+    for p in ps:
+        k = p.grad.numel()
+        p.grad.copy_((bucket[off:off + k] / n).reshape(p.grad.shape).to(p.grad.dtype))
+        off += k
+    return total, n

@@ -121,6 +121,8 @@ def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
             assert args[0] == "512" and args[3] == "0" and args[4] == "false", k    # ABL = 0, not fused
         if name == "step_flat_kernel":
             assert args[:2] in (["256", "4"], ["128", "8"], ["512", "2"]), k        # the product geometries
+        if name == "step_flat_vec_kernel":
+            assert args[0] in ("2", "4", "8") and args[1:3] == ["256", "4"], k      # A, 256 x 4
     assert not any(k.startswith(("gae_tile_vec_kernel", "replay_gather_f5_kernel", "advance_flat_kernel<",
                                  "batch_reward_fwd_"))
                    for k in kernels)

@@ -78,3 +78,88 @@ def test_sharded_envs_equal_unsharded_and_moments_allreduce():
         assert np.isclose(mean, x.mean(), rtol=1e-12, atol=1e-15)
         assert np.isclose(var, x.var(), rtol=1e-9, atol=1e-18)
         np.testing.assert_allclose(z, (full[:, lo:hi] - mean) / (var ** 0.5 + 1e-8), rtol=1e-5, atol=1e-6)
+
+
+# ---------------------------------------------------------------- actor-critic update, sharded
+AC_G, AC_N, AC_W, AC_T = 12, 5, 6, 4
+
+
+def _ac_data():
+    rng = np.random.default_rng(11)
+    s = (100 * np.exp(0.01 * rng.standard_normal((AC_T + 1, AC_G, AC_N, AC_W, 5)))).astype(np.float64)
+    z = rng.standard_normal((AC_T + 1, AC_G, AC_N))
+    a = np.exp(z) / np.exp(z).sum(-1, keepdims=True)
+    r = rng.standard_normal((AC_T, AC_G))
+    return torch.tensor(s), torch.tensor(a, dtype=torch.float32), torch.tensor(r)
+
+
+def _ac_update(lo, hi, group=None):
+    """One OnPolicy.update_actor_critic over envs [lo, hi) of the synthetic rollout (a slab
+    buffer on the host: the update's torch math, the advantage moments and the gradient
+    all-reduce; the env step is not involved). Returns the policy's parameters."""
+    from types import SimpleNamespace
+    from pmenv.config import EnvConfig
+    from pmenv.on_policy import OnPolicy, WindowPolicy
+    from pmenv.parallel import normalize
+    s, a, r = _ac_data()
+    B = hi - lo
+    env = SimpleNamespace(cfg=EnvConfig(num_envs=B, num_assets=AC_N, window=AC_W), device=torch.device("cpu"))
+    torch.manual_seed(0)
+    policy = WindowPolicy(AC_W).double()
+    loop = OnPolicy(env, policy, horizon=AC_T, explore_std=0.5)
+    # plain SGD: Adam's first step g / (|g| + eps) magnifies reassociation in gradients
+    # near eps; the gradients themselves are compared too
+    loop.optim = torch.optim.SGD(policy.parameters(), lr=1e-2)
+    buf = loop.buf
+    buf.s = buf.s.double()
+    buf.s.copy_(s[:, lo:hi])
+    buf.a.copy_(a[:, lo:hi])
+    buf.step = AC_T + 1
+    adv = normalize(r[:, lo:hi], group=group)            # the 24-byte moment all-reduce
+    loss = loop.update_actor_critic(adv, group=group, chunk=5)   # gradient accumulated over chunks
+    return [p.detach().clone() for p in policy.parameters()] + [p.grad.clone() for p in policy.parameters()], loss
+
+
+def _ac_worker(rank, world, port, root, q):
+    import sys
+    for p in (os.path.join(root, "pm-rl_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pmenv.parallel import shard_range
+    lo, hi = shard_range(AC_G, rank, world)
+    params, loss = _ac_update(lo, hi)
+    q.put((rank, [p.numpy() for p in params], loss))
+    dist.destroy_process_group()
+
+
+def test_actor_critic_sharded_update_equals_unsharded():
+    """Two gloo ranks, each holding half of the envs' rollout: globally normalised
+    advantages (moment all-reduce) -> advantage-weighted log-likelihood loss -> one
+    gradient all-reduce -> optimizer step. Both ranks' averaged gradients and parameters
+    equal one unsharded update's to f64 reassociation."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ac_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full, loss = _ac_update(0, AC_G)
+    torch.manual_seed(0)
+    from pmenv.on_policy import WindowPolicy
+    init = [p.detach() for p in WindowPolicy(AC_W).double().parameters()]
+    assert any(not torch.equal(x, y) for x, y in zip(full, init))          # the update moved the policy
+    for rank, params, l in res:
+        assert abs(l - loss) <= 1e-12 * max(1.0, abs(loss)), f"rank {rank} loss"
+        half = len(full) // 2                  # parameters, then their averaged gradients
+        for i, (x, y) in enumerate(zip(params, full)):
+            group = full[:half] if i < half else full[half:]
+            scale = max(float(g.abs().max()) for g in group)   # (the last bias's gradient is 0: a
+            np.testing.assert_allclose(x, y.numpy(), rtol=1e-12, atol=1e-13 * scale,   # shift of every score)
+                                       err_msg=f"rank {rank} tensor {i}")

@@ -143,3 +143,83 @@ def test_gpu_on_policy_compact_loop():
     adv, ret, values = loop.advantages(critic)
     assert adv.shape == (T, B) and bool(torch.isfinite(adv).all())
     assert abs(float(adv.mean())) < 1e-4 and abs(float(adv.std(unbiased=False)) - 1.0) < 1e-3
+
+
+# ---------------------------------------------------------------- actor-critic, two ranks
+AC = dict(G=1001, N=30, W=50, T=8)
+
+
+def _ac_run(lo, hi, dev, group=None):
+    """OnPolicy over global envs [lo, hi): an exploring rollout (noise keyed by global env
+    id), the critic's GAE advantages normalised over every rank (the HIP moments + the
+    24-byte all-reduce), one update_actor_critic (one gradient all-reduce). f64 policy and
+    critic, so the ranks' sums differ from the unsharded run's by reassociation only."""
+    from pmenv import TradingEnv, synth
+    from pmenv.on_policy import OnPolicy, WindowCritic, WindowPolicy
+    G, N, W, T = AC["G"], AC["N"], AC["W"], AC["T"]
+    B = hi - lo
+    ser = synth.series(W + T, B, N, env_offset=lo, seed=42, device=dev)
+    obs0 = synth.window_from_series(ser, W)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=dev)
+    torch.manual_seed(0)
+    policy = WindowPolicy(W).double().to(dev)
+    critic = WindowCritic(W).double().to(dev)
+    loop = OnPolicy(env, policy, horizon=T, explore_std=0.3, env_offset=lo)
+    loop.optim = torch.optim.SGD(policy.parameters(), lr=1e-2)
+    rewards = loop.rollout(obs0, ser[W:])
+    adv, ret, values = loop.advantages(critic, group=group)
+    loss = loop.update_actor_critic(adv, group=group, chunk=2048)
+    return (rewards.cpu(), [p.detach().cpu() for p in policy.parameters()],
+            [p.grad.detach().cpu() for p in policy.parameters()], loss)
+
+
+def _ac_worker(rank, world, port, root, q):
+    import os
+    import sys
+    for p in (os.path.join(root, "pm-rl_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        from pmenv import parallel
+        lo, hi = parallel.shard_range(AC["G"], rank, world)
+        r, params, grads, loss = _ac_run(lo, hi, dev)
+        q.put((rank, lo, hi, r.numpy(), [p.numpy() for p in params], [g.numpy() for g in grads], loss))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_actor_critic_two_ranks_equal_unsharded_update():
+    """The normalised advantages feed a loss: two gloo ranks (spawned, both on cuda:0), each
+    stepping half of the envs, take the same actor-critic update as one unsharded run —
+    the rollouts bit for bit, the averaged gradients and the parameters to f64
+    reassociation."""
+    import os
+    import socket
+    import torch.multiprocessing as mp
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ac_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    r_full, params, grads, loss = _ac_run(0, AC["G"], DEV)
+    for rank, lo, hi, r, ps, gs, l in res:
+        assert np.array_equal(r, r_full.numpy()[:, lo:hi]), f"rank {rank}: rollout rewards"
+        assert abs(l - loss) <= 1e-10 * abs(loss), f"rank {rank}: loss {l} vs {loss}"
+        gmax = max(float(g.abs().max()) for g in grads)
+        for i, (x, y) in enumerate(zip(gs, grads)):
+            np.testing.assert_allclose(x, y.numpy(), rtol=1e-9, atol=1e-11 * gmax, err_msg=f"rank {rank} grad {i}")
+        for i, (x, y) in enumerate(zip(ps, params)):
+            np.testing.assert_allclose(x, y.numpy(), rtol=1e-12, atol=1e-13, err_msg=f"rank {rank} param {i}")
