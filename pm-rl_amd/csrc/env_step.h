@@ -268,6 +268,19 @@ __device__ __forceinline__ double group_min(double v, int lane) {
     return lane < 32 ? fmin(r0, r1) : fmin(r2, r3);
 }
 
+// lane 0 of the lane's L-lane group (0 or 32), read through the scalar unit
+template <int L>
+__device__ __forceinline__ int group_lane0_i(int v, int lane) {
+    const int a = __builtin_amdgcn_readlane(v, 0);
+    if (L == 64) return a;
+    const int b = __builtin_amdgcn_readlane(v, 32);
+    return lane < 32 ? a : b;
+}
+template <int L>
+__device__ __forceinline__ double group_lane0(double v, int lane) {
+    return __hiloint2double(group_lane0_i<L>(__double2hiint(v), lane), group_lane0_i<L>(__double2loint(v), lane));
+}
+
 // The per-env step of lane group (b, lane % L) in two halves, so a caller can put
 // other loads between them: a load half issues every load (none dependent on
 // another, no data-dependent branch), scalar_finish computes and returns the
@@ -396,21 +409,43 @@ __device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int
         if (norm) w = e / z;                                      // :60
     }
 
-    // :67-75 commission fixed point (f64, capped), per env group
+    // :67-75 commission fixed point (f64, capped), per env group: the reference's iteration
+    // mu <- (1 - c wl0 - (2c - c^2) S(mu)) / (1 - c w0), S(mu) = sum_{n>=1} max(wl_n - mu w_n, 0),
+    // with S in active-set form: S(mu) = A - mu Bw over the assets P(mu) where wl_n > mu w_n
+    // (the same set the max keeps). P is one ballot per iteration; A and Bw are reduced only
+    // when P changes — in practice on the first one or two iterations — so the later
+    // iterations are a few scalar f64 operations instead of a group reduction each. The
+    // iterates equal the reference's up to f64 rounding of S (parity: value rtol 1e-12).
+    // The division by 1 - c w0 (fixed over the iterations) is a multiplication by its
+    // reciprocal, and the group's asset-0 values are read with v_readlane (SALU path) rather
+    // than a cross-lane shuffle through LDS.
     double V = v_prev;
     if (p.commission > 0.0) {
         const double c = p.commission;
-        const double w0 = __shfl(w, lane & ~(L - 1), 64);
-        const double wl0 = (double)__shfl(wlf, lane & ~(L - 1), 64);
+        const double w0 = group_lane0<L>(w, lane);
+        const double wl0 = (double)__int_as_float(group_lane0_i<L>(__float_as_int(wlf), lane));
+        const double K = 1.0 - c * wl0, Dc = 2.0 * c - c * c, invE = 1.0 / (1.0 - c * w0);
+        const uint64_t gmask = L == 64 ? ~0ull : (lane < 32 ? 0xFFFFFFFFull : 0xFFFFFFFF00000000ull);
+        const bool cand = act && n > 0;
+        const double wld = (double)wlf;
         double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
+        double Aw = 0.0, Bw = 0.0;
+        uint64_t pset = 0;
+        bool have = false;
         int it = 0;
         bool done = !(fabs(mu - mu_last) > p.mu_tol) || p.mu_max_iter <= 0;
         while (__any(!done)) {
-            const double d = (act && n > 0) ? (double)wlf - mu * w : 0.0;
-            const double tot = group_sum<L>(d > 0.0 ? d : 0.0, lane);   // torch.maximum(x, 0) as intended
+            const bool in_p = cand && wld - mu * w > 0.0;            // torch.maximum(x, 0) as intended
+            const uint64_t m = __ballot(in_p) & gmask;
+            if (__any(!done && (!have || m != pset))) {             // a group's active set changed
+                Aw = group_sum<L>(in_p ? wld : 0.0, lane);
+                Bw = group_sum<L>(in_p ? w : 0.0, lane);
+                pset = m;
+                have = true;
+            }
             if (!done) {
                 mu_last = mu;
-                mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
+                mu = (K - Dc * (Aw - mu * Bw)) * invE;
                 ++it;
                 done = !(fabs(mu - mu_last) > p.mu_tol) || it >= p.mu_max_iter;
             }

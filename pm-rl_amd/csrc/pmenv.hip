@@ -959,14 +959,15 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // N = 16 681 vs 689; it loses at N = 8 (500 chunks, 4 envs per tile: 713 vs 691) and in
     // place on cache-resident windows (4,096 envs: 46.3 vs 44.2 us, 8,192: 85.2 vs 84.2);
     // double-buffered it wins from 2,048 envs (25.4 vs 27.0) (profiles/ab_r02/r02w_flat1d_*).
-    // With commission > 0 the capped fixed point, run by every tile an env straddles,
-    // costs it 6-8 % (65,536 envs: 701 vs 662 us at 0.0025, 718 vs 664 at 0.01; 16,384:
-    // 179.5 vs 168.8), so AUTO keeps the other paths there; differential Sharpe: 646 vs
-    // 659 (profiles/ab_r02/r02w_flat1e_*).
+    // Commission > 0: every tile an env straddles runs the capped fixed point. With the
+    // active-set iteration (scalar_core), a uniform wave index (no waterfall loops around
+    // the scalar loads) and the reciprocal of 1 - c w0, the flat step leads there too:
+    // 65,536 x 30 at 0.0025 642.8 vs 661.9 us on two launches (profiles/ab_r03/comm3_r03.err;
+    // in round 2 the fixed point cost it 6-8 %: 701 vs 662).
     h->flat1_auto = 0;
     const int one_auto_base = h->one_auto;   // tools: PMENV_FLAT1=0 restores it
     (void)one_auto_base;
-    if (h->flat1_ok && c.num_assets <= 64 && h->flat1_block <= 256 && h->per4 >= 1000u && !(c.commission > 0.0)) {
+    if (h->flat1_ok && c.num_assets <= 64 && h->flat1_block <= 256 && h->per4 >= 1000u) {
         if (win > (48ll << 20)) h->flat1_auto |= PMENV_FUSE_DB;
         if (win > (256ll << 20)) h->flat1_auto |= PMENV_FUSE_INPLACE;
         h->one_auto &= ~h->flat1_auto;

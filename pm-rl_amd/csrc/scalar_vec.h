@@ -212,27 +212,51 @@ __device__ __forceinline__ VecMid<A> vec_core(const StepParams& p, int b, int la
         }
     }
 
-    // :67-75 commission fixed point (f64, capped), per env group
+    // :67-75 commission fixed point (f64, capped), per env group, in the active-set form of
+    // scalar_core (env_step.h): S(mu) = A - mu Bw over the assets where wl_n > mu w_n, A and
+    // Bw reduced only when that set changes (A ballots per iteration)
     double V = in.v_prev;
     if (p.commission > 0.0) {
         const double c = p.commission;
         const int g0 = lane & ~(L - 1);
-        const double w0 = __shfl(wv[0], g0, 64);
-        const double wl0 = (double)__shfl(in.wl[0], g0, 64);
+        const double w0 = L == 64 ? group_lane0<64>(wv[0], lane) : __shfl(wv[0], g0, 64);
+        const double wl0 = L == 64 ? (double)__int_as_float(group_lane0_i<64>(__float_as_int(in.wl[0]), lane))
+                                   : (double)__shfl(in.wl[0], g0, 64);
+        const double K = 1.0 - c * wl0, Dc = 2.0 * c - c * c, invE = 1.0 / (1.0 - c * w0);
+        const uint64_t gmask = L == 64 ? ~0ull : (((1ull << (L & 63)) - 1ull) << (lane & ~(L - 1)));
         double mu_last = 1.0, mu = 1.0 - 2.0 * c + c * c;
+        double Aw = 0.0, Bw = 0.0;
+        uint64_t pset[A];
+#pragma unroll
+        for (int e = 0; e < A; ++e) pset[e] = 0;
+        bool have = false;
         int it = 0;
         bool done = !(fabs(mu - mu_last) > p.mu_tol) || p.mu_max_iter <= 0;
         while (__any(!done)) {
-            double part = 0.0;
+            bool in_p[A];
+            bool changed = !have;
+            uint64_t m[A];
 #pragma unroll
             for (int e = 0; e < A; ++e) {
-                const double d = (act[e] && nn[e] > 0) ? (double)in.wl[e] - mu * wv[e] : 0.0;
-                part += d > 0.0 ? d : 0.0;        // torch.maximum(x, 0) as intended
+                in_p[e] = act[e] && nn[e] > 0 && (double)in.wl[e] - mu * wv[e] > 0.0;   // max(x, 0) as intended
+                m[e] = __ballot(in_p[e]) & gmask;
+                changed |= m[e] != pset[e];
             }
-            const double tot = gred<L, 0>(part, lane);
+            if (__any(!done && changed)) {
+                double pa = 0.0, pb = 0.0;
+#pragma unroll
+                for (int e = 0; e < A; ++e) {
+                    pa += in_p[e] ? (double)in.wl[e] : 0.0;
+                    pb += in_p[e] ? wv[e] : 0.0;
+                    pset[e] = m[e];
+                }
+                Aw = gred<L, 0>(pa, lane);
+                Bw = gred<L, 0>(pb, lane);
+                have = true;
+            }
             if (!done) {
                 mu_last = mu;
-                mu = (1.0 - c * wl0 - (2.0 * c - c * c) * tot) / (1.0 - c * w0);
+                mu = (K - Dc * (Aw - mu * Bw)) * invE;
                 ++it;
                 done = !(fabs(mu - mu_last) > p.mu_tol) || it >= p.mu_max_iter;
             }

@@ -82,7 +82,7 @@ __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, u
     // window loads: nt for POL 1, 3 (tools A/B: 5 sc0 nt, 6 sc1 nt, 7 nt)
     constexpr int kAux = (POL == 1 || POL == 3 || POL == 7) ? 2 : POL == 5 ? 3 : POL == 6 ? 18 : 0;
     constexpr int CPW = BLOCK * V;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     t.c0 = tile * (uint32_t)CPW;
     t.nblk = min((uint32_t)CPW, qtot - t.c0);
     t.e_lo = fdiv(t.c0, p.div_units);                                  // div_units: per4
@@ -106,7 +106,7 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
     // window stores: nt for POL 1, 4 (tools A/B: 5 sc0 nt, 6 and 7 sc1 nt)
     constexpr int kAux = (POL == 1 || POL == 4) ? 2 : POL == 5 ? 3 : (POL == 6 || POL == 7) ? 18 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t per4 = p.per4;
     // 3. the scalar steps' cores, one env per wave (their tails run after the stores)
     ScalarMid mid;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(BLOCK) void step_flat_vec_kernel(StepParams p, uint
     __shared__ int32_t sh_k[WAVES], sh_rlo[WAVES];
     const uint32_t tile = blockIdx.x;
     flat_seq_enter<OUT>(p);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = p.N, WF = p.W * F;
     const uint32_t per4 = p.per4;
     const uint32_t c0 = tile * (uint32_t)CPW;

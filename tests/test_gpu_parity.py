@@ -268,8 +268,9 @@ def test_gpu_auto_path_rule():
     bound: it wins there at every asset count measured); above, env windows of >= 1,000
     chunks take the flat one-launch step (step_flat_kernel) — double-buffered from 48 MiB,
     in place from 256 MiB (in place, cache-resident windows are faster on the two-launch
-    stream), commission 0 — and the rest the two-launch stream. Checked against the oracle
-    just above the 48 MiB threshold (1,700 envs x 30 x 50: 51 MB)."""
+    stream), with or without commission — and the rest the two-launch stream; wide envs
+    (64 < N <= 128) take step_flat_vec_kernel in place above 1 GiB. Checked against the
+    oracle just above the 48 MiB threshold (1,700 envs x 30 x 50: 51 MB)."""
     from pmenv import TradingEnv
     small = TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV)          # 45 MB
     assert small.step_path.count("step_env_kernel") == 2
@@ -283,9 +284,14 @@ def test_gpu_auto_path_rule():
     wide = TradingEnv(num_envs=2000, num_assets=65, window=50, device=DEV)           # N > 64
     assert "step_flat_kernel" not in wide.step_path
     comm = TradingEnv(num_envs=9000, num_assets=30, window=50, device=DEV, commission=0.0025)
-    assert "step_flat_kernel" not in comm.step_path                                 # the fixed point per tile
-    comm.set_step_impl("flat")                                                      # forced: still available
-    assert comm.step_path.count("step_flat_kernel") == 2
+    assert comm.step_path.count("step_flat_kernel") == 2                            # the fixed point per tile
+    comm.set_step_impl("two_launch")                                                # forced: still available
+    assert "step_flat_kernel" not in comm.step_path
+    wide_big = TradingEnv(num_envs=16384, num_assets=100, window=50, device=DEV)     # 1.6 GB
+    db, ip = wide_big.step_path.split(" | ")
+    assert ip.startswith("step_flat_vec_kernel") and not db.startswith("step_flat")
+    wide_500 = TradingEnv(num_envs=8192, num_assets=500, window=50, device=DEV)      # config 5: two launches
+    assert "step_flat" not in wide_500.step_path
     _run_both({}, B=1700, N=30, W=50, T=9, kind="mixed", seed=31)
     _run_both({"ring": "chrono"}, B=1700, N=30, W=50, T=5, kind="simplex", seed=32, double_buffer=True)
     _run_both({}, B=9000, N=30, W=50, T=7, kind="mixed", seed=33)

@@ -129,7 +129,8 @@ for e in envs:
         ref = got
         same.append(True)
     else:
-        same.append(bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])))
+        same.append(bool(torch.equal(got[0].nan_to_num(7.0), ref[0].nan_to_num(7.0)) and
+                         torch.equal(got[1].nan_to_num(7.0), ref[1].nan_to_num(7.0))))
 
 times = {n: [] for n in names}
 for r in range(a.rounds):
