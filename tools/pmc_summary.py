@@ -54,6 +54,11 @@ if main:
     res["hbm_bytes_per_launch"] = res["kernels"][main[0]]["hbm_bytes"]
     res["dominant_kernel"] = main[0]
     res["traffic_over_algorithmic"] = res["hbm_bytes_per_launch"] / alg
+# the library these counters were collected on (the in-tree build the GPU run loaded):
+# bench.py reports roofline.traffic only while the running library has this sha256
+import hashlib  # noqa: E402
+lib = os.path.join(ROOT, "pm-rl_amd", "pmenv", "libpmenv.so")
+res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
 json.dump(res, open(os.path.join(ROOT, "profiles", f"pmc_{tag}.json"), "w"), indent=1)
