@@ -239,13 +239,24 @@ __device__ __forceinline__ double group_combine(double r0, double r1, double r2,
     if (L == 64) return (r0 + r1) + (r2 + r3);
     return lane < 32 ? r0 + r1 : r2 + r3;
 }
+// After the row shifts, DPP row_bcast:15 on rows 1 and 3 (row_mask 0xA) adds the previous
+// row's total into them: lane 31 holds r1 + r0 and lane 63 r3 + r2, the pair sums of
+// group_combine, in the same order (f64 addition commutes bitwise) — two readlanes per
+// half instead of four, the same bits.
+constexpr int kRowBcast15 = 0x142;
 template <int L>
 __device__ __forceinline__ double group_sum(double v, int lane) {
     v += dpp_shift<kRowShr1>(v, 0.0);
     v += dpp_shift<kRowShr2>(v, 0.0);
     v += dpp_shift<kRowShr4>(v, 0.0);
     v += dpp_shift<kRowShr8>(v, 0.0);
-    return group_combine<L>(lane_value(v, 15), lane_value(v, 31), lane_value(v, 47), lane_value(v, 63), lane);
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const double prev = __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, kRowBcast15, 0xA, 0xF, false),
+                                         __builtin_amdgcn_update_dpp(0, lo, kRowBcast15, 0xA, 0xF, false));
+    v += prev;                                    // rows 0 and 2: + 0.0
+    const double p01 = lane_value(v, 31), p23 = lane_value(v, 63);
+    if (L == 64) return p01 + p23;
+    return lane < 32 ? p01 : p23;
 }
 template <int L>
 __device__ __forceinline__ double group_max(double v, int lane) {
