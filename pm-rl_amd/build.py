@@ -15,6 +15,8 @@ ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "pmenv", "libpmenv.so")
 AB_LIB = os.path.join(ROOT, "tools", "libpmenv_ab.so")
 SRC = os.path.join(HERE, "csrc", "pmenv.hip")
+AB_DIR = os.path.join(ROOT, "tools", "ab")
+AB_SRC = os.path.join(AB_DIR, "pmenv_ab.hip")     # the tools build's hooks (linked with SRC)
 ORACLE_SRC = os.path.join(ROOT, "oracle", "pmenv_oracle.c")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -34,17 +36,20 @@ def _run(cmd):
 
 
 def build_pmenv(force=False, ab=False):
-    """The product library; ab=True: the tools build (-DPMENV_AB -> tools/libpmenv_ab.so),
-    which alone reads the PMENV_* A/B knobs and carries the measured alternatives and the
-    timing-only ablations."""
+    """The product library; ab=True: the tools build (tools/libpmenv_ab.so: the product's
+    translation unit linked with tools/ab/pmenv_ab.hip, whose pmenv_tools hooks alone read
+    the PMENV_* A/B knobs and launch the measured alternatives and the timing-only
+    ablations)."""
     out = AB_LIB if ab else LIB
     deps = [os.path.join(ROOT, "include", "pmenv.h")] + [
         os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
-    if not force and not _stale(out, SRC, *deps, __file__):
+    srcs = [SRC] + ([AB_SRC] if ab else [])
+    if ab:
+        deps += [os.path.join(AB_DIR, f) for f in os.listdir(AB_DIR) if f.endswith(".h")]
+    if not force and not _stale(out, *srcs, *deps, __file__):
         return out
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-          "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
-         + (["-DPMENV_AB"] if ab else []) + ["-o", out, SRC])
+          "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-o", out] + srcs)
     return out
 
 

@@ -9,6 +9,8 @@
 
 namespace pmenv_dev {
 
+constexpr int kWideMaxAssets = 512;   // the widest env the packed scalar step and the wide flat step take
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-B access
 

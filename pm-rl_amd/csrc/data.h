@@ -35,7 +35,7 @@ __device__ __forceinline__ void normals4(uint32_t c0, uint32_t c1, uint64_t g, u
 
 // One thread per (env, asset): close_t = close_{t-1} exp(sigma z - sigma^2/2), OHLC
 // around it (SURVEY.md §8d synthetic inputs). series [T][B][N][4].
-__global__ void synth_series_kernel(f4* series, int T, int B, int N, int64_t env_offset,
+static __global__ void synth_series_kernel(f4* series, int T, int B, int N, int64_t env_offset,
                                     uint64_t seed, double sigma) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)B * N) return;
@@ -56,7 +56,7 @@ __global__ void synth_series_kernel(f4* series, int T, int B, int N, int64_t env
 }
 
 // One thread per (t, env): softmax of N(0,1) logits over the N assets.
-__global__ void synth_actions_kernel(float* actions, int T, int B, int N, int64_t env_offset, uint64_t seed) {
+static __global__ void synth_actions_kernel(float* actions, int T, int B, int N, int64_t env_offset, uint64_t seed) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)T * B) return;
     const int t = (int)(i / B), b = (int)(i % B);
@@ -82,7 +82,7 @@ __global__ void synth_actions_kernel(float* actions, int T, int B, int N, int64_
     }
 }
 
-__global__ void window_init_kernel(float* obs, const f4* series, int B, int N, int W, int F) {
+static __global__ void window_init_kernel(float* obs, const f4* series, int B, int N, int W, int F) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over B*N*W
     if (i >= (int64_t)B * N * W) return;
     const int t = (int)(i % W);
@@ -95,7 +95,7 @@ __global__ void window_init_kernel(float* obs, const f4* series, int B, int N, i
 }
 
 // obs[b, n, t, f] = series[start[b] + t, n, f]; one thread per (b, n, t) row of F floats
-__global__ void window_init_days_kernel(float* obs, const float* series, int T, int N, int F,
+static __global__ void window_init_days_kernel(float* obs, const float* series, int T, int N, int F,
                                         const int32_t* start, int B, int W) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over B*N*W
     if (i >= (int64_t)B * N * W) return;

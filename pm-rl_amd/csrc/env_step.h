@@ -216,7 +216,7 @@ __device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scrat
 // One wave per env, kScalarWaves envs per workgroup, no barriers.
 __device__ __forceinline__ void copy_halo(const StepParams& p);
 
-__global__ __launch_bounds__(64 * kScalarWaves) void scalar_step_kernel(StepParams p, int scratch_floats) {
+static __global__ __launch_bounds__(64 * kScalarWaves) void scalar_step_kernel(StepParams p, int scratch_floats) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     copy_halo(p);
     const int wave = threadIdx.x >> 6;
@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) 
 // ---------------------------------------------------------------- surface kernel
 // The reference contract: obs is the caller's next-day window; only channel F-1
 // is rewritten with ActionBuffer.get_all() (trading_env.py:103).
-__global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
+static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1201,7 +1201,7 @@ __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
 }
 
 // ---------------------------------------------------------------- reset kernel
-__global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask) {
+static __global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask) {
     const int b = blockIdx.x;
     if (mask && !mask[b]) return;
     const int tid = threadIdx.x;

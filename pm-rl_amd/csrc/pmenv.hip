@@ -1,646 +1,53 @@
-// pmenv.hip — host side and C ABI (include/pmenv.h) of the MI355X-native
-// vectorised portfolio environment. Device code lives in step_env.h (the one-launch
-// step), env_step.h (scalar step, window streams, reset, fallbacks), scalar_vec.h
-// (packed scalar step), data.h (synthetic market data), rollout.h / gae_vec.h (GAE,
-// moments), replay.h (replay gather, metrics) and trainer.h (batched reward).
+// pmenv.hip — host side and C ABI (include/pmenv.h) of the MI355X-native vectorised
+// portfolio environment: the product library, libpmenv.so. Device code lives in
+// step_flat.h (the one-launch step over fixed window tiles), step_env.h (the one-launch
+// step, one workgroup per env), env_step.h (scalar step, window streams, reset,
+// fallbacks), scalar_vec.h (packed scalar step), data.h (synthetic market data),
+// rollout.h (GAE, moments), replay.h (replay gather, metrics) and trainer.h (batched
+// reward); the step's launchers in launch.h, the handle and its shape planning in handle.h.
 //
-// Every entry point enqueues on the caller's stream and never synchronises,
-// allocates or frees (graph-capturable), except create / destroy / the explicit
-// synchronous queries documented in the header.
-//
-// Kernel choice is a function of the shape only (and of pmenv_set_step_path). The
-// A/B variants measured while choosing — other geometries, cache policies, the
-// timing-only ablations that skip work — exist only in the tools build
-// (-DPMENV_AB -> tools/libpmenv_ab.so), which alone reads the PMENV_* knobs.
+// Every entry point enqueues on the caller's stream and never synchronises, allocates or
+// frees (graph-capturable), except create / destroy / the explicit synchronous queries
+// documented in the header. Kernel choice is a function of the shape and of
+// pmenv_set_step_path only: this library reads no environment variable. The A/B
+// alternatives measured while choosing live in the tools build (tools/ab/pmenv_ab.hip,
+// linked with this file into tools/libpmenv_ab.so), behind the pmenv_tools hooks whose
+// definitions here, at the end of the file, do nothing.
 #include <hip/hip_runtime.h>
 
-#include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pmenv.h"
-#include "common.h"
 #include "data.h"
-#include "env_step.h"
-#include "scalar_vec.h"
-#include "step_env.h"
-#include "step_flat.h"
-#include "rollout.h"
-#include "gae_vec.h"
+#include "handle.h"
+#include "launch.h"
 #include "replay.h"
+#include "rollout.h"
 #include "trainer.h"
 
 using namespace pmenv_dev;
-
-#ifdef PMENV_AB
-static const char* ab_knob(const char* name) { return getenv(name); }
-static int ab_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-#else
-static inline const char* ab_knob(const char*) { return nullptr; }
-static inline int ab_int(const char*, int dflt) { return dflt; }
-#endif
-
-struct pmenv {
-    pmenv_cfg cfg;
-    int device;
-    void* state;          // value | stat_a | stat_b | counter | ring | nonfinite | last_close | w_new
-    size_t state_bytes;
-    bool owns_state;
-    double* value;
-    double* sa;
-    double* sb;
-    int32_t* k;
-    float* ring;
-    float* last_close;
-    float* w_new;
-    unsigned long long* nonfinite;
-    // LDS single-launch fallback geometry
-    int rows_per_tile, tile_floats;
-    bool vec;
-    size_t lds_tile, lds_surface;
-    // two-launch streaming path geometry
-    bool streaming;       // scalar step kernel + window stream
-    int unit_rows, units_per_env, stream_vec;          // row-kernel advance in place
-    int unit_rows_db, units_per_env_db, stream_vec_db; // row-kernel advance double-buffered (obs_out)
-    int stream_block, stream_block_db;                 // threads per row-kernel workgroup (tools: 128 | 256)
-    int stream_pol;       // cache policy of the row kernel
-    bool flat;            // double-buffered advance as the flat 16-B stream
-    int flat_block, flat_pol, flat_ip_pol;   // cache policy: double-buffered / in-place stream
-    bool flat_inplace;    // in-place advance as the flat stream + halo (advance_flat_inplace_kernel)
-    int flat_ip_block, flat_ip_vec;   // threads per workgroup, chunks per thread
-    bool flat_db_wg;      // double-buffered flat stream in the workgroup form (tools: ds_bpermute form)
-    float* halo;          // [halo_wgs][2] float4: first two chunks of every in-place flat workgroup
-    uint32_t halo_wgs, flat_qtot;
-    int scalar_scratch_floats;
-    int k1_groups;        // env groups per wave in scalar_step_reg_kernel
-    int k1_vec;           // scalar_step_vec_kernel shape 100 * L + A (0: register / LDS form)
-    // one launch per step
-    bool one_ok;          // the shape fits step_env_kernel
-    int one_auto;         // PMENV_FUSE_* bits the automatic choice gives step_env_kernel
-    int one;              // PMENV_FUSE_* bits: which windows take step_env_kernel now
-    int one_v, one_waves; // step_env_kernel: chunks per lane, waves per workgroup
-    uint32_t per4;        // 16-B chunks per env window
-    // one launch over the flat stream (step_flat_kernel)
-    bool flat1_ok;        // the shape fits step_flat_kernel
-    int flat1_auto;       // PMENV_FUSE_* bits the automatic choice gives step_flat_kernel
-    int flat1;            // PMENV_FUSE_* bits: which windows take step_flat_kernel now
-    void* snap;           // the state snapshot, two parities: value f64 | counter i32 | get_last() | last close
-    double* sv[2];
-    int32_t* sk[2];
-    float* sw[2];
-    float* slc[2];
-    float* halo1[2];      // [halo1_wgs][2] float4 per parity: the next tile's first two chunks
-    uint32_t halo1_wgs;
-    int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread (tools: PMENV_FLAT1_GEOM)
-    bool flat1_xcd;               // tools: XCD-contiguous tile ranges (PMENV_FLAT1_XCD)
-    int flat1_pol;                // tools: 3 nt loads only, 4 nt stores only, 5 sc0 nt, 6 sc1 nt, 7 nt loads + sc1 nt stores
-    int par;              // parity of the snapshot / halo the next step reads
-    bool snap_ok;         // sv[par] .. slc[par] equal the canonical state
-    const float* halo1_obs;   // the window whose halo halo1[par] holds (null: none)
-    // device-sequenced form (hipGraph-safe): from the first flat step enqueued under
-    // stream capture on, every flat step is flat_seq_kernel + step_flat_kernel reading
-    // the parity and the validity from seq (device words) instead of the host fields above
-    bool device_seq;
-    int32_t* seq;         // {D, C, V, pad, HOBS lo, HOBS hi} (step_flat.h)
-    uint64_t snap_stride; // bytes between the two parities of the snapshot / halo
-    int path;             // pmenv_step_path_kind
-    // tools build only
-    int fused;            // PMENV_FUSE_* bits: advance_rows_kernel<fused> (PMENV_FUSED)
-    int fused_vec;
-    int ablate;           // PMENV_ABLATE timing-only variants
-    bool one_nocap, flat_s80;
-    int flat1_lds_pad;
-    size_t lds_scalar, lds_stream;
-    char err[512];
-};
+using namespace pmenv_host;
 
 namespace {
 
 thread_local char g_create_err[512] = "";
 
-void set_err(pmenv* h, const char* fmt, ...) {
-    if (!h) return;
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(h->err, sizeof(h->err), fmt, ap);
-    va_end(ap);
-}
-
-struct DeviceGuard {
-    int prev = -1;
-    bool changed = false;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) changed = hipSetDevice(dev) == hipSuccess;
-    }
-    ~DeviceGuard() {
-        if (changed) (void)hipSetDevice(prev);
-    }
-};
-
-StepParams base_params(const pmenv* h) {
-    StepParams p;
-    memset(&p, 0, sizeof(p));
-    const pmenv_cfg& c = h->cfg;
-    p.B = c.num_envs; p.N = c.num_assets; p.W = c.window; p.F = c.features;
-    p.close_ch = c.close_channel;
-    p.reward_kind = c.reward_kind; p.norm_mode = c.norm_mode; p.ring_mode = c.ring_mode;
-    p.ret_mode = c.ret_mode; p.mu_max_iter = c.mu_max_iter;
-    p.rows_per_tile = h->rows_per_tile;
-    p.tile_floats = h->tile_floats;
-    p.unit_rows = h->unit_rows;
-    p.units_per_env = h->units_per_env;
-    p.init_cash = c.init_cash; p.commission = c.commission; p.scale = c.reward_scale;
-    p.rf = c.risk_free_rate; p.eta = c.sharpe_eta; p.mu_tol = c.mu_tol;
-    p.value = h->value; p.k = h->k; p.ring = h->ring; p.last_close = h->last_close;
-    p.w_new = h->w_new;
-    p.sa = h->sa; p.sb = h->sb;
-    p.nonfinite = h->nonfinite;
-    p.div_wf = make_fastdiv((uint32_t)(c.window * c.features));
-    p.div_f = make_fastdiv((uint32_t)c.features);
-    p.div_w = make_fastdiv((uint32_t)c.window);
-    p.div_units = make_fastdiv((uint32_t)(h->units_per_env > 0 ? h->units_per_env : 1));
-    return p;
-}
-
-inline bool aligned4(const void* ptr) { return ((uintptr_t)ptr & 3u) == 0; }
-
-int check_launch(pmenv* h, const char* what) {
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_err(h, "%s launch failed: %s", what, hipGetErrorString(e));
-        return PMENV_ERR_HIP;
-    }
-    return PMENV_OK;
-}
-
-constexpr int PMENV_FUSE_DB = 1, PMENV_FUSE_INPLACE = 2;
-
-// Geometry of the row-kernel stream (the fallback of the flat stream): units of R
-// whole asset rows per `block`-thread workgroup, R*W*F floats <= 4*block*V (V float4
-// per thread) and R*W*F % 4 == 0 so every unit starts 16-B aligned. `v_order` lists V
-// in preference order. Returns false when the shape needs the LDS fallback.
-bool plan_streaming(const pmenv_cfg& c, const int* v_order, int block, int* unit_rows, int* vec_per_thread) {
-    const int64_t WF = (int64_t)c.window * c.features;
-    if (c.features != 5 || ((int64_t)c.num_assets * WF) % 4 != 0) return false;
-    int align = 1;                       // rows per unit must be a multiple of this
-    while ((align * WF) % 4 != 0) ++align;
-    const int want = ab_int("PMENV_UNIT_ROWS", 0);
-    static const int kAscending[3] = {1, 2, 4};
-    if (want > 0) v_order = kAscending;   // a forced unit takes the fewest float4 per thread that hold it
-    for (int vi = 0; vi < 3; ++vi) {
-        const int V = v_order[vi];
-        const int64_t cap = (int64_t)block * 4 * V;
-        int R = (int)(cap / WF);
-        if (R >= c.num_assets) R = c.num_assets;
-        else R -= R % align;
-        if (R < 1 || (int64_t)R * WF > cap) continue;
-        if (want > 0) {
-            if (want > R) continue;
-            if (want != c.num_assets && want % align) return false;
-            R = want;
-        }
-        *unit_rows = R;
-        *vec_per_thread = V;
-        return true;
-    }
-    return false;
-}
-
-// ---------------------------------------------------------------- launchers
-// the row-kernel stream (fallback of the flat stream: W = 1, or windows past 2^31 chunks)
-template <int BLOCK, int V, int ABL, int POL>
-void launch_advance_bv(const StepParams& p, unsigned grid, hipStream_t stream) {
-    if (p.obs_out == p.obs)
-        advance_rows_kernel<BLOCK, V, true, ABL, false, POL><<<grid, BLOCK, 0, stream>>>(p);
-    else
-        advance_rows_kernel<BLOCK, V, false, ABL, false, POL><<<grid, BLOCK, 0, stream>>>(p);
-}
-
-template <int BLOCK, int ABL, int POL>
-void launch_advance_b(int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
-    if (vec == 1) launch_advance_bv<BLOCK, 1, ABL, POL>(p, grid, stream);
-    else if (vec == 2) launch_advance_bv<BLOCK, 2, ABL, POL>(p, grid, stream);
-    else launch_advance_bv<BLOCK, 4, ABL, POL>(p, grid, stream);
-}
-
-template <int POL>
-void launch_advance_p(int block, int vec, const StepParams& p, unsigned grid, hipStream_t stream) {
-#ifdef PMENV_AB
-    if (block == 128) { launch_advance_b<128, 0, POL>(vec, p, grid, stream); return; }
-    if (block == 256) { launch_advance_b<256, 0, POL>(vec, p, grid, stream); return; }
-#endif
-    (void)block;
-    launch_advance_b<kStreamBlock, 0, POL>(vec, p, grid, stream);
-}
-
-// the double-buffered flat stream: the workgroup (LDS) form, 512 threads x 2 chunks
-void launch_flat(const pmenv* h, StepParams p, hipStream_t stream) {
-    const pmenv_cfg& c = h->cfg;
-    const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
-    const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
-    p.div_units = make_fastdiv(per4);
-#ifdef PMENV_AB
-    if (!h->flat_db_wg) {        // the ds_bpermute form, one chunk per thread
-        const int bk = h->flat_block;
-        const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
-#define PMENV_FLATB(BK)                                                                             \
-        if (bk == BK) {                                                                             \
-            if (h->flat_pol == 1) advance_flat_kernel<BK, 1><<<grid, BK, 0, stream>>>(p, qtot);      \
-            else if (h->flat_pol == 2) advance_flat_kernel<BK, 2><<<grid, BK, 0, stream>>>(p, qtot); \
-            else advance_flat_kernel<BK, 0><<<grid, BK, 0, stream>>>(p, qtot);                       \
-            return;                                                                                 \
-        }
-        PMENV_FLATB(128) PMENV_FLATB(512) PMENV_FLATB(256)
-#undef PMENV_FLATB
-    }
-    if (h->flat_pol == 2) {
-        advance_flat_wg_kernel<512, 2, 2><<<(unsigned)((qtot + 1023) / 1024), 512, 0, stream>>>(p, qtot);
-        return;
-    }
-#endif
-    const unsigned g = (unsigned)((qtot + 1023) / 1024);
-    if (h->flat_pol == 0) advance_flat_wg_kernel<512, 2, 0><<<g, 512, 0, stream>>>(p, qtot);
-    else advance_flat_wg_kernel<512, 2, 1><<<g, 512, 0, stream>>>(p, qtot);
-}
-
-// the in-place flat stream: 512 threads x 2 chunks, the halo copied by the scalar step
-void launch_flat_inplace(const pmenv* h, StepParams p, hipStream_t stream) {
-    const pmenv_cfg& c = h->cfg;
-    const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
-    p.div_units = make_fastdiv(per4);
-    p.halo = h->halo;
-    const int cpw = h->flat_ip_block * h->flat_ip_vec;
-    const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
-#ifdef PMENV_AB
-    const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
-    const int pol = h->flat_ip_pol;
-    if (h->ablate >= 64 && h->ablate < 128) {     // timing-only ablations (PMENV_ABLATE = 64 + SKIP bits)
-        const unsigned g1 = (unsigned)((h->flat_qtot + 511) / 512);
-#define PMENV_ABL(X) case 64 + X: advance_flat_inplace_kernel<512, 1, 1, X><<<g1, 512, 0, stream>>>(p, h->flat_qtot); break;
-        switch (h->ablate) {
-            PMENV_ABL(1) PMENV_ABL(2) PMENV_ABL(4) PMENV_ABL(6) PMENV_ABL(15) PMENV_ABL(31) PMENV_ABL(32)
-            PMENV_ABL(33)
-            default: break;
-        }
-#undef PMENV_ABL
-        return;
-    }
-    if (h->flat_s80 && key == 5122) {
-        if (pol == 1) advance_flat_inplace_s80_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
-        else advance_flat_inplace_s80_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
-        return;
-    }
-#define PMENV_FIP(BK, V)                                                                                      \
-    if (key == BK * 10 + V) {                                                                                 \
-        if (pol == 1) advance_flat_inplace_kernel<BK, V, 1><<<grid, BK, 0, stream>>>(p, h->flat_qtot);         \
-        else if (pol == 2) advance_flat_inplace_kernel<BK, V, 2><<<grid, BK, 0, stream>>>(p, h->flat_qtot);    \
-        else advance_flat_inplace_kernel<BK, V, 0><<<grid, BK, 0, stream>>>(p, h->flat_qtot);                  \
-        return;                                                                                               \
-    }
-    PMENV_FIP(256, 1) PMENV_FIP(256, 2) PMENV_FIP(256, 4) PMENV_FIP(512, 1) PMENV_FIP(1024, 1)
-#undef PMENV_FIP
-#endif
-    if (h->flat_ip_block == 256) advance_flat_inplace_kernel<256, 2, 0><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-    else if (h->flat_ip_pol == 1) advance_flat_inplace_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
-    else advance_flat_inplace_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
-}
-
-// the second launch of the two-launch step
-void launch_advance(const pmenv* h, StepParams p, hipStream_t stream) {
-    const bool db = p.obs_out != p.obs;
-    if (db && h->flat && !h->ablate) {
-        launch_flat(h, p, stream);
-        return;
-    }
-    if (!db && h->flat_inplace && (!h->ablate || (h->ablate >= 64 && h->ablate < 128))) {
-        launch_flat_inplace(h, p, stream);
-        return;
-    }
-    p.unit_rows = db ? h->unit_rows_db : h->unit_rows;
-    p.units_per_env = db ? h->units_per_env_db : h->units_per_env;
-    p.div_units = make_fastdiv((uint32_t)p.units_per_env);
-    const int vec = db ? h->stream_vec_db : h->stream_vec;
-    const int block = db ? h->stream_block_db : h->stream_block;
-    const unsigned grid = (unsigned)(h->cfg.num_envs * p.units_per_env);
-#ifdef PMENV_AB
-    switch (h->ablate) {     // timing-only builds: 512-thread geometry, default policy
-    case 1: launch_advance_b<kStreamBlock, 1, 0>(vec, p, grid, stream); return;
-    case 2: launch_advance_b<kStreamBlock, 2, 0>(vec, p, grid, stream); return;
-    case 3: launch_advance_b<kStreamBlock, 3, 0>(vec, p, grid, stream); return;
-    case 7: launch_advance_b<kStreamBlock, 7, 0>(vec, p, grid, stream); return;
-    default: break;
-    }
-    if (h->stream_pol == 2) { launch_advance_p<2>(block, vec, p, grid, stream); return; }
-#endif
-    if (h->stream_pol == 1) launch_advance_p<1>(block, vec, p, grid, stream);
-    else launch_advance_p<0>(block, vec, p, grid, stream);
-}
-
-// K1, the first launch of the two-launch step: the register form (N <= 64)
-template <int L>
-void launch_scalar_reg_l(int groups, const StepParams& p, hipStream_t stream) {
-    const int per_wave = (64 / L) * groups;
-    const unsigned waves = (unsigned)((p.B + per_wave - 1) / per_wave);
-    const unsigned grid = (waves + 3) / 4;
-#ifdef PMENV_AB
-    if (groups == 4) { scalar_step_reg_kernel<L, 4><<<grid, 256, 0, stream>>>(p); return; }
-    if (groups == 2) { scalar_step_reg_kernel<L, 2><<<grid, 256, 0, stream>>>(p); return; }
-#endif
-    scalar_step_reg_kernel<L, 1><<<grid, 256, 0, stream>>>(p);
-}
-
-void launch_scalar_reg(const pmenv* h, const StepParams& p, hipStream_t stream) {
-    if (p.N <= 32) launch_scalar_reg_l<32>(h->k1_groups, p, stream);
-    else launch_scalar_reg_l<64>(h->k1_groups, p, stream);
-}
-
-// K1 packed form (scalar_vec.h): L lanes x A assets per env, consecutive or strided
-// (STR); h->k1_vec = 100 * L + A (+ kK1Str for the strided layout)
-constexpr int kK1Str = 100000;
-
-template <int L, int A, bool STR>
-void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
-    const unsigned waves = (unsigned)((p.B + 64 / L - 1) / (64 / L));
-    scalar_step_vec_kernel<L, A, STR><<<(waves + 3) / 4, 256, 0, stream>>>(p);
-}
-
-bool launch_scalar_vec(int vec, const StepParams& p, hipStream_t stream) {
-    switch (vec) {   // the shapes pick_k1_vec chooses per asset count (N > 64)
-    case kK1Str + 6402: launch_scalar_vec_la<64, 2, true>(p, stream); return true;
-    case kK1Str + 6404: launch_scalar_vec_la<64, 4, true>(p, stream); return true;
-    case kK1Str + 6408: launch_scalar_vec_la<64, 8, true>(p, stream); return true;
-#ifdef PMENV_AB
-    case 801: launch_scalar_vec_la<8, 1, false>(p, stream); return true;
-    case 802: launch_scalar_vec_la<8, 2, false>(p, stream); return true;
-    case 1602: launch_scalar_vec_la<16, 2, false>(p, stream); return true;
-    case 1604: launch_scalar_vec_la<16, 4, false>(p, stream); return true;
-    case 804: launch_scalar_vec_la<8, 4, false>(p, stream); return true;
-    case 1601: launch_scalar_vec_la<16, 1, false>(p, stream); return true;
-    case 1608: launch_scalar_vec_la<16, 8, false>(p, stream); return true;
-    case 3202: launch_scalar_vec_la<32, 2, false>(p, stream); return true;
-    case 3204: launch_scalar_vec_la<32, 4, false>(p, stream); return true;
-    case kK1Str + 3202: launch_scalar_vec_la<32, 2, true>(p, stream); return true;
-    case kK1Str + 3204: launch_scalar_vec_la<32, 4, true>(p, stream); return true;
-#endif
-    default: return false;
-    }
-}
-
-// K1 shape per asset count (tools build: the PMENV_K1 knob "reg" | "LxA" | "LxAs"
-// strided, e.g. "16x2", "64x8s"). 0: the register form (N <= 64) or the LDS form (N > 512).
-// N <= 64 takes the register form: its reductions (one asset per lane, DPP row shifts,
-// the fixed-order row combine) are bitwise those of the one-launch step's scalar part,
-// so the two paths — and therefore sharded and unsharded runs, whose path can differ
-// by env count — give the same bits. It costs 4.6 us at 65,536 envs over the packed
-// 16 x 2 form (29.1 vs 24.5 us), and the two-launch path runs for N <= 64 only on
-// cache-resident in-place windows (<= 8,192 envs at N = 30): < 1 us per step.
+// K1 shape per asset count: N <= 64 takes the register form (one asset per lane; its
+// reductions — DPP row shifts, the fixed-order row combine — are bitwise those of the
+// one-launch steps' scalar part, so the paths, and sharded and unsharded runs whose
+// path can differ by env count, give the same bits); 64 < N <= 512 the packed strided
+// form (64 lanes x A assets, every dword load a coalesced run; step_flat_vec_kernel
+// shares it); N > 512 the LDS form.
 int pick_k1_vec(const pmenv_cfg& c) {
     const int N = c.num_assets;
     if ((int64_t)c.num_envs * N * 4 >= (1ll << 32)) return 0;     // descriptors span the [B*N] arrays
-    int v = 0;
-#ifdef PMENV_AB
-    if (N <= 8) v = 801;
-    else if (N <= 16) v = 802;
-    else if (N <= 32) v = 1602;
-    else if (N <= 64) v = 1604;
-    else
-#endif
-    if (N <= 64) v = 0;
-    else if (N <= 128) v = kK1Str + 6402;
-    else if (N <= 256) v = kK1Str + 6404;
-    else if (N <= 512) v = kK1Str + 6408;
-    if (const char* knob = ab_knob("PMENV_K1")) {
-        static const int kK1Vec[] = {801, 802, 804, 1601, 1602, 1604, 1608, 3202, 3204,
-                                     kK1Str + 3202, kK1Str + 3204, kK1Str + 6402, kK1Str + 6404, kK1Str + 6408};
-        int L = 0, A = 0;
-        char s = 0;
-        if (!strcmp(knob, "reg")) return 0;
-        if (sscanf(knob, "%dx%d%c", &L, &A, &s) >= 2) {
-            const int want = 100 * L + A + (s == 's' ? kK1Str : 0);
-            for (int k : kK1Vec)
-                if (k == want && L * A >= N) return k;
-        }
-    }
-    return v;
-}
-
-// the first launch of the two-launch step (with the in-place stream's halo copy)
-int launch_scalar(pmenv* h, StepParams p, hipStream_t stream) {
-    if (p.obs_out == p.obs && h->flat_inplace && !h->ablate) {   // the in-place advance's halo
-        p.halo = h->halo;
-        p.halo_wgs = h->halo_wgs;
-        p.halo_block = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
-        p.halo_qtot = h->flat_qtot;
-    }
-    const int N = h->cfg.num_assets;
-    if (h->k1_vec && launch_scalar_vec(h->k1_vec, p, stream)) {
-        // packed form
-    } else if (N <= 64) {
-        launch_scalar_reg(h, p, stream);
-    } else {
-        const int B = h->cfg.num_envs;
-        scalar_step_kernel<<<(B + kScalarWaves - 1) / kScalarWaves, 64 * kScalarWaves, h->lds_scalar, stream>>>(
-            p, h->scalar_scratch_floats);
-    }
-    return check_launch(h, "scalar_step_kernel");
-}
-
-// the whole step in one launch, one workgroup per env (step_env.h)
-template <int V>
-void launch_one_v(const pmenv* h, const StepParams& p, hipStream_t stream) {
-    const bool out = p.obs_out != p.obs;
-    const int pol = out ? h->flat_pol : h->flat_ip_pol;
-    const unsigned threads = 64u * (unsigned)h->one_waves;
-    size_t lds = ((size_t)threads * V + 2) * 16;
-    const unsigned grid = (unsigned)h->cfg.num_envs;
-#ifdef PMENV_AB
-    lds += (size_t)ab_int("PMENV_ONE_LDS_PAD", 0);    // occupancy study: fewer workgroups per CU
-    if (h->ablate >= 128 && h->ablate < 144) {    // timing-only / A/B bits (step_env.h ABL), nt policy
-#define PMENV_ONEABL(X)                                                                                     \
-        case 128 + X:                                                                                     \
-            if (out) step_env_kernel<V, true, 1, X><<<grid, threads, lds, stream>>>(p, h->per4);            \
-            else step_env_kernel<V, false, 1, X><<<grid, threads, lds, stream>>>(p, h->per4);               \
-            return;
-        switch (h->ablate) {
-            PMENV_ONEABL(1) PMENV_ONEABL(2) PMENV_ONEABL(4) PMENV_ONEABL(8) PMENV_ONEABL(12)
-            default: break;
-        }
-#undef PMENV_ONEABL
-    }
-    if (h->one_nocap) {
-        if (out && pol == 1) step_env_nocap_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (out) step_env_nocap_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
-        else if (pol == 1) step_env_nocap_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else step_env_nocap_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
-        return;
-    }
-#endif
-    if (out) {
-        if (pol == 1) step_env_kernel<V, true, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else step_env_kernel<V, true, 0><<<grid, threads, lds, stream>>>(p, h->per4);
-    } else {
-        if (pol == 1) step_env_kernel<V, false, 1><<<grid, threads, lds, stream>>>(p, h->per4);
-        else step_env_kernel<V, false, 0><<<grid, threads, lds, stream>>>(p, h->per4);
-    }
-}
-
-void launch_one(const pmenv* h, const StepParams& p, hipStream_t stream) {
-#ifdef PMENV_AB
-    switch (h->one_v) {
-    case 1: launch_one_v<1>(h, p, stream); return;
-    case 2: launch_one_v<2>(h, p, stream); return;
-    case 3: launch_one_v<3>(h, p, stream); return;
-    case 6: launch_one_v<6>(h, p, stream); return;
-    case 8: launch_one_v<8>(h, p, stream); return;
-    default: break;
-    }
-#endif
-    launch_one_v<4>(h, p, stream);
-}
-
-#ifdef PMENV_AB
-// tools build: the previous one-launch form (whole-env row units, scalar step inside)
-void launch_fused(const pmenv* h, StepParams p, hipStream_t stream) {
-    p.unit_rows = h->cfg.num_assets;
-    p.units_per_env = 1;
-    p.div_units = make_fastdiv(1u);
-    const unsigned grid = (unsigned)h->cfg.num_envs;
-    const bool inplace = p.obs_out == p.obs;
-#define PMENV_FUSED_LAUNCH(V)                                                                        \
-    if (inplace) advance_rows_kernel<kStreamBlock, V, true, 0, true><<<grid, kStreamBlock, 0, stream>>>(p); \
-    else advance_rows_kernel<kStreamBlock, V, false, 0, true><<<grid, kStreamBlock, 0, stream>>>(p);
-    if (h->fused_vec == 1) { PMENV_FUSED_LAUNCH(1) }
-    else if (h->fused_vec == 2) { PMENV_FUSED_LAUNCH(2) }
-    else { PMENV_FUSED_LAUNCH(4) }
-#undef PMENV_FUSED_LAUNCH
-}
-#endif
-
-// step_flat_vec_kernel (64 < N <= 512): A strided assets per lane, as pick_k1_vec's
-// packed two-launch scalar step, so the two paths give the same bits
-template <int A, int BK, int VV>
-void launch_flat1_vec_g(const StepParams& p, uint32_t qtot, unsigned grid, bool out, int pol, hipStream_t stream) {
-    if (out) {
-        if (pol == 1) step_flat_vec_kernel<A, BK, VV, 1, true><<<grid, BK, 0, stream>>>(p, qtot);
-        else step_flat_vec_kernel<A, BK, VV, 0, true><<<grid, BK, 0, stream>>>(p, qtot);
-    } else {
-        if (pol == 1) step_flat_vec_kernel<A, BK, VV, 1, false><<<grid, BK, 0, stream>>>(p, qtot);
-        else step_flat_vec_kernel<A, BK, VV, 0, false><<<grid, BK, 0, stream>>>(p, qtot);
-    }
-}
-
-template <int A>
-void launch_flat1_vec_a(const pmenv* h, const StepParams& p, unsigned grid, bool out, int pol, hipStream_t stream) {
-#ifdef PMENV_AB
-    if (h->flat1_block == 128) { launch_flat1_vec_g<A, 128, 8>(p, h->flat_qtot, grid, out, pol, stream); return; }
-#endif
-    launch_flat1_vec_g<A, 256, 4>(p, h->flat_qtot, grid, out, pol, stream);
-}
-
-void launch_flat1_vec(const pmenv* h, const StepParams& p, unsigned grid, bool out, int pol, hipStream_t stream) {
-    const int N = h->cfg.num_assets;
-    if (N <= 128) launch_flat1_vec_a<2>(h, p, grid, out, pol, stream);
-    else if (N <= 256) launch_flat1_vec_a<4>(h, p, grid, out, pol, stream);
-    else launch_flat1_vec_a<8>(h, p, grid, out, pol, stream);
-}
-
-// the whole step in one launch over the flat stream (step_flat.h): prime the snapshot
-// and the halo when something other than this kernel touched them, then one launch
-void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
-    const bool out = p.obs_out != p.obs;
-    const int q = h->par;
-    p.per4 = h->per4;
-    p.div_units = make_fastdiv(h->per4);
-    const bool need_halo = !out && h->halo1_obs != p.obs;
-    if (h->device_seq) {
-        // parity 0 in *_in / halo_in, parity 1 in *_out / halo_out; the sequencer primes
-        // parity D if needed and publishes it, the kernel swaps when it is 1
-        p.sv_in = h->sv[0]; p.sk_in = h->sk[0]; p.sw_in = h->sw[0]; p.slc_in = h->slc[0];
-        p.sv_out = h->sv[1]; p.sk_out = h->sk[1]; p.sw_out = h->sw[1]; p.slc_out = h->slc[1];
-        p.halo_in = h->halo1[0];
-        p.halo_out = h->halo1[1];
-        p.seq = h->seq;
-        StepParams pp = p;
-        pp.sv_out = h->sv[0]; pp.sk_out = h->sk[0]; pp.sw_out = h->sw[0]; pp.slc_out = h->slc[0];
-        pp.halo = h->halo1[0];
-        pp.halo_wgs = h->halo1_wgs;
-        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
-        pp.halo_qtot = h->flat_qtot;
-        const int64_t work = (int64_t)h->cfg.num_envs * h->cfg.num_assets;
-        const unsigned g = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
-        flat_seq_kernel<<<g, 256, 0, stream>>>(pp, out ? 1 : 0, h->snap_stride);
-    } else if (!h->snap_ok || need_halo) {
-        StepParams pp = p;
-        pp.sv_out = h->sv[q]; pp.sk_out = h->sk[q]; pp.sw_out = h->sw[q]; pp.slc_out = h->slc[q];
-        pp.halo = need_halo ? h->halo1[q] : nullptr;
-        pp.halo_wgs = h->halo1_wgs;
-        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
-        pp.halo_qtot = h->flat_qtot;
-        const int64_t work = (int64_t)h->cfg.num_envs * h->cfg.num_assets;
-        const unsigned g = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
-        flat_prime_kernel<<<g, 256, 0, stream>>>(pp);
-    }
-    if (!h->device_seq) {
-        p.sv_in = h->sv[q]; p.sk_in = h->sk[q]; p.sw_in = h->sw[q]; p.slc_in = h->slc[q];
-        p.sv_out = h->sv[1 - q]; p.sk_out = h->sk[1 - q]; p.sw_out = h->sw[1 - q]; p.slc_out = h->slc[1 - q];
-        p.halo_in = h->halo1[q];
-        p.halo_out = h->halo1[1 - q];
-    }
-    const int pol = out ? h->flat_pol : h->flat_ip_pol;
-    const unsigned grid = (h->flat_qtot + (uint32_t)(h->flat1_block * h->flat1_vec) - 1) /
-                          (uint32_t)(h->flat1_block * h->flat1_vec);
-    if (h->cfg.num_assets > 64) {                 // wide envs: the packed scalar step per tile
-        launch_flat1_vec(h, p, grid, out, pol, stream);
-        h->par = 1 - q;
-        h->snap_ok = true;
-        h->halo1_obs = out ? nullptr : p.obs;
-        return;
-    }
-    size_t pad = 0;                               // tools: extra LDS per workgroup (occupancy study)
-#ifdef PMENV_AB
-    pad = (size_t)h->flat1_lds_pad;
-#endif
-#define PMENV_FLAT1_LAUNCH(BK, VV)                                                                           \
-    if (out) {                                                                                              \
-        if (pol == 1) step_flat_kernel<BK, VV, 1, true><<<grid, BK, pad, stream>>>(p, h->flat_qtot);        \
-        else step_flat_kernel<BK, VV, 0, true><<<grid, BK, pad, stream>>>(p, h->flat_qtot);                 \
-    } else {                                                                                                \
-        if (pol == 1) step_flat_kernel<BK, VV, 1, false><<<grid, BK, pad, stream>>>(p, h->flat_qtot);       \
-        else step_flat_kernel<BK, VV, 0, false><<<grid, BK, pad, stream>>>(p, h->flat_qtot);                \
-    }
-    const int key = h->flat1_block * 100 + h->flat1_vec;
-#ifdef PMENV_AB
-    if (key == 25604 && h->flat1_pol >= 3 && h->flat1_pol <= 7) {   // other cache policies
-#define PMENV_FLAT1_POLV(PV)                                                                      \
-        if (h->flat1_pol == PV) {                                                                 \
-            if (out) step_flat_kernel<256, 4, PV, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);  \
-            else step_flat_kernel<256, 4, PV, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);     \
-        }
-        PMENV_FLAT1_POLV(3) PMENV_FLAT1_POLV(4) PMENV_FLAT1_POLV(5) PMENV_FLAT1_POLV(6) PMENV_FLAT1_POLV(7)
-#undef PMENV_FLAT1_POLV
-    }
-    else if (key == 25604 && h->flat1_xcd) {
-        if (out) step_flat_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-        else step_flat_kernel<256, 4, 1, false, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-    }
-    else if (key == 51204) { PMENV_FLAT1_LAUNCH(512, 4) }
-    else if (key == 102402) { PMENV_FLAT1_LAUNCH(1024, 2) }
-    else if (key == 25608) { PMENV_FLAT1_LAUNCH(256, 8) }
-    else if (key == 25602) { PMENV_FLAT1_LAUNCH(256, 2) }
-    else if (key == 12804) { PMENV_FLAT1_LAUNCH(128, 4) }
-    else
-#endif
-    if (key == 25604) { PMENV_FLAT1_LAUNCH(256, 4) }
-    else if (key == 12808) { PMENV_FLAT1_LAUNCH(128, 8) }
-    else { PMENV_FLAT1_LAUNCH(512, 2) }
-#undef PMENV_FLAT1_LAUNCH
-    h->par = 1 - q;
-    h->snap_ok = true;
-    h->halo1_obs = out ? nullptr : p.obs;
+    if (N <= 64) return 0;
+    if (N <= 128) return kK1Str + 6402;
+    if (N <= 256) return kK1Str + 6404;
+    if (N <= 512) return kK1Str + 6408;
+    return 0;
 }
 
 // the stream is being captured into a hipGraph: step_flat_kernel's host-chosen parity
@@ -691,7 +98,6 @@ int flat1_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_AUTO) return h->flat1_auto;
     return 0;
 }
-
 
 }  // namespace
 
@@ -766,6 +172,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     auto fail = [&](int code) {
         // no handle reaches the caller: pmenv_last_error(NULL) reports this one
         snprintf(g_create_err, sizeof(g_create_err), "%s", h->err);
+        pmenv_tools::release(h);
         if (h->state && h->owns_state) (void)hipFree(h->state);
         if (h->halo) (void)hipFree(h->halo);
         if (h->snap) (void)hipFree(h->snap);
@@ -814,29 +221,22 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
 
     // ---- the two-launch stream: row-kernel geometry (fallback) and the flat stream
     static const int kInplaceOrder[3] = {2, 4, 1}, kDoubleOrder[3] = {4, 2, 1};
-    h->stream_block = h->stream_block_db = kStreamBlock;
-    {
-        const int bk = ab_int("PMENV_STREAM_BLOCK", kStreamBlock);   // tools: 128 | 256
-        if (bk == 128 || bk == 256) h->stream_block = h->stream_block_db = bk;
-    }
-    h->streaming = plan_streaming(c, kInplaceOrder, h->stream_block, &h->unit_rows, &h->stream_vec) &&
-                   plan_streaming(c, kDoubleOrder, h->stream_block_db, &h->unit_rows_db, &h->stream_vec_db);
+    h->streaming = plan_streaming(c, kInplaceOrder, kStreamBlock, 0, &h->unit_rows, &h->stream_vec) &&
+                   plan_streaming(c, kDoubleOrder, kStreamBlock, 0, &h->unit_rows_db, &h->stream_vec_db);
     const int64_t per = (int64_t)c.num_assets * c.window * c.features;
-    const int64_t win = (int64_t)c.num_envs * per * 4;
+    const int64_t win = window_bytes(c);
     // Flat 16-B stream (F = 5, W >= 2, 16-B granular envs, chunk count < 2^31) in place
     // (with the halo) and double-buffered: 512 threads x 2 chunks, side data through the
     // scalar unit (6.38 TB/s against 5.37 for whole-row units).
-    const bool flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
-                         (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
-    h->flat = h->flat_inplace = flat_ok;
-    h->flat_db_wg = true;
-    h->flat_block = 512;
+    h->flat_ok = h->streaming && c.features == 5 && c.window >= 2 && per % 4 == 0 &&
+                 (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024;
+    h->flat = h->flat_inplace = h->flat_ok;
     // in place, cache-resident windows (<= 256 MiB) take 8 KiB workgroups: 80.2 vs 83.2 us
     // at 8,192 x 30, 44.4 vs 44.7 at 4,096 (profiles/ab_r02/r02w_smallip_*); above, 16 KiB
     // (round 1: 512 x 2 against 256 x 1 / 2 / 4, 512 x 1, 1024 x 1)
-    h->flat_ip_block = (int64_t)c.num_envs * per * 4 <= (256ll << 20) ? 256 : 512;
+    h->flat_ip_block = win <= (256ll << 20) ? 256 : 512;
     h->flat_ip_vec = 2;
-    h->flat_qtot = flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
+    h->flat_qtot = h->flat_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
     // nt unless the stream's working set fits the 256 MiB Infinity Cache: the window in
     // place (<= 256 MiB), the window and its double buffer otherwise (<= 128 MiB each).
     // Step at 4,096 x 30 x 50 x 5 (123 MB) 44.4 us with the default policy against 46.5
@@ -844,115 +244,44 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // 16,384: 199.6 / 164.6 (profiles/ab_r01/pol_small_r01j.log, pol_ip_r01m.log)
     h->flat_pol = win <= (128ll << 20) ? 0 : 1;
     h->flat_ip_pol = win <= (256ll << 20) ? 0 : 1;
-    h->stream_pol = 0;
-    if (const char* knob = ab_knob("PMENV_STREAM_POL")) {       // tools: 0 | 1 (nt) | 2 (sc0 nt)
-        const int pol = atoi(knob);
-        if (pol >= 0 && pol <= 2) h->stream_pol = h->flat_pol = h->flat_ip_pol = pol;
-    }
-#ifdef PMENV_AB
-    if (const char* knob = ab_knob("PMENV_FLAT")) h->flat = flat_ok && atoi(knob) != 0;
-    if (const char* knob = ab_knob("PMENV_FLAT_INPLACE")) h->flat_inplace = flat_ok && atoi(knob) != 0;
-    h->flat_db_wg = ab_int("PMENV_FLAT_DB_WG", 1) != 0;
-    h->flat_ip_block = ab_int("PMENV_FLAT_IP_BLOCK", h->flat_ip_block);
-    h->flat_ip_vec = ab_int("PMENV_FLAT_IP_VEC", 2);
-    {   // the launcher's (block, vec) table: anything else takes the default 512 x 2
-        const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
-        if (key != 2561 && key != 2562 && key != 2564 && key != 5121 && key != 5122 && key != 10241) {
-            h->flat_ip_block = 512;
-            h->flat_ip_vec = 2;
-        }
-    }
-    {
-        const int bk = ab_int("PMENV_FLAT_BLOCK", 512);
-        if (bk == 128 || bk == 256 || bk == 512) h->flat_block = bk;
-    }
-    if (const char* knob = ab_knob("PMENV_ADVANCE"))   // force the single-launch LDS kernel
-        if (!strcmp(knob, "lds")) h->streaming = h->flat = h->flat_inplace = false;
-    h->ablate = ab_int("PMENV_ABLATE", 0);
-    h->one_nocap = ab_int("PMENV_ONE_NOCAP", 0) != 0;
-    h->flat1_lds_pad = ab_int("PMENV_FLAT1_LDS_PAD", 0);
-    h->flat_s80 = ab_int("PMENV_FLAT_S80", 0) != 0;
-#endif
-    h->k1_groups = ab_int("PMENV_K1_GROUPS", 1);
-    if (h->k1_groups != 2 && h->k1_groups != 4) h->k1_groups = 1;
     h->k1_vec = pick_k1_vec(c);
-    if (h->streaming) {
-        h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
-        h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
-        h->lds_stream = 0;
-    }
+    h->per4 = (uint32_t)(per / 4);
 
     // ---- the one-launch step (step_env_kernel, one workgroup per env): F = 5, W >= 2,
     // N <= 64 (the scalar step on one wave), 16-B granular env windows whose 1 KiB
-    // blocks fit 16 waves and 64 KiB of LDS. AUTO gives it the windows of at most
-    // 48 MiB, where launch latency dominates and it wins by 7-38 % (tools/gpu_ab_smallb.sh,
+    // blocks fit 16 waves and 64 KiB of LDS, 4 chunks per lane (650 us against 662-666
+    // for 8, 762 for 3, 860 for 2 at the BASELINE shape). AUTO gives it the windows of at
+    // most 48 MiB, where launch latency dominates and it wins by 7-38 % (tools/gpu_ab_smallb.sh,
     // profiles/ab_r02/r02u_*: N = 8..64, 256..4,096 envs; N = 30: 64 envs 6.5 vs 9.6 us,
     // 1,024: 13.1 vs 18.2). Larger windows take the two-launch stream: its fixed 16 KiB
     // workgroups run 640-670 us on a 2 GB window at every asset count measured, while the
     // one-workgroup-per-env geometry ties it only at N = 30 (650-658 us) and loses 4-15 %
     // at N = 8, 16, 24, 32, 40, 48, 60, 64 (profiles/ab_r02/r02r_*, r02s_*, r02t_*).
-    h->per4 = (uint32_t)(per / 4);
-    // 4 chunks per lane (tools: PMENV_ONE_V = 1 | 2 | 3 | 6 | 8; 4 measured best: 650 us
-    // against 662-666 for 8, 762 for 3, 860 for 2 at the BASELINE shape)
-    h->one_v = ab_int("PMENV_ONE_V", 4);
-    if (h->one_v != 1 && h->one_v != 2 && h->one_v != 3 && h->one_v != 6 && h->one_v != 8) h->one_v = 4;
-    {
-        // the env's chunks start anywhere in a 64-chunk block: up to 63 slots ahead of it
-        const uint32_t blocks = (h->per4 + 63u + 63u) / 64u;
-        h->one_waves = (int)((blocks + (uint32_t)h->one_v - 1) / (uint32_t)h->one_v);
-    }
-    h->one_ok = h->streaming && c.features == 5 && c.window >= 2 && c.num_assets <= 64 && per % 4 == 0 &&
-                h->one_waves <= 16 && ((int64_t)64 * h->one_v * h->one_waves + 2) * 16 <= 65536;
-    // (also beyond the flat stream's 2^31-chunk index, where the two-launch path would fall
-    // back to the whole-row stream)
+    // (Also beyond the flat stream's 2^31-chunk index, where the two-launch path would
+    // fall back to the whole-row stream.)
+    plan_one(h, kOneV);
     h->one_auto = h->one_ok && (win <= (48ll << 20) || !h->flat_inplace) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
-#ifdef PMENV_AB
-    if (const char* knob = ab_knob("PMENV_ONE")) {    // 0 | db | ip | all
-        if (!h->one_ok || !strcmp(knob, "0")) h->one_auto = 0;
-        else if (!strcmp(knob, "db")) h->one_auto = PMENV_FUSE_DB;
-        else if (!strcmp(knob, "ip")) h->one_auto = PMENV_FUSE_INPLACE;
-        else if (!strcmp(knob, "all")) h->one_auto = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
-    }
-    {   // the previous one-launch form (advance_rows_kernel<fused>), PMENV_FUSED = db | all
-        int fused_rows = 0;
-        const bool fusable = h->streaming && c.num_assets <= 64 && !h->ablate &&
-                             plan_streaming(c, kDoubleOrder, kStreamBlock, &fused_rows, &h->fused_vec) &&
-                             fused_rows == c.num_assets;
-        if (const char* knob = ab_knob("PMENV_FUSED")) {
-            if (fusable && !strcmp(knob, "db")) h->fused = PMENV_FUSE_DB;
-            else if (fusable && !strcmp(knob, "all")) h->fused = PMENV_FUSE_DB | PMENV_FUSE_INPLACE;
-            if (h->fused) h->one_auto &= ~h->fused;
-        }
-    }
-#endif
-    // ---- the one-launch flat step (step_flat_kernel): the flat stream's shape rules, the
-    // scalar step on one wave per env (N <= 64), at most one env per wave in a tile.
-    // Geometry: 256 threads x 4 chunks (16 KiB tiles, 4 waves) where env windows have
-    // >= 511 chunks, 512 x 2 (8 waves) from 148 chunks. 256 x 4 against 512 x 2 / 512 x 4 /
-    // 1024 x 2 / 256 x 8 / 256 x 2 / 128 x 8 / 128 x 4 at 65,536 x 30 in place: 629.5 against
-    // 714 / 678 / 790 / 695 / 675 / 624 / 641 us; 128 x 8 loses 15 % at N = 16 and 64 where
-    // 256 x 4 wins (profiles/ab_r02/r02w_flat1b_*, r02w_flat1c_*). A persistent form that
-    // keeps the next tile's loads in flight needs 160 VGPRs (3 waves per SIMD): 2x slower.
-    // Wide envs (64 < N <= 512, step_flat_vec_kernel) also need the rows a tile touches
-    // per env to fit one wave's 64 staged bar rows (W >= 14 at F = 5 for 16 KiB tiles).
-    auto flat1_fits = [&](int block, int vec) {
-        const uint32_t cpw = (uint32_t)(block * vec);
-        const uint32_t ne_max = h->per4 ? (cpw + h->per4 - 2u) / h->per4 + 1u : 0u;
-        const int64_t span_rows = (4ll * cpw - 1) / (WF > 0 ? WF : 1) + 2;
-        const bool wide_ok = c.num_assets <= kWideMaxAssets && span_rows <= 64;
-        return flat_ok && (c.num_assets <= 64 || wide_ok) && ne_max <= (uint32_t)(block / 64);
-    };
+
+    // ---- the one-launch flat step (step_flat_kernel; step_flat_vec_kernel for 64 < N <=
+    // 512): the flat stream's shape rules, the scalar step on one wave per env, at most one
+    // env per wave in a tile (flat1_fits). Geometry: 256 threads x 4 chunks (16 KiB tiles,
+    // 4 waves) where env windows have >= 511 chunks, 512 x 2 (8 waves) from 148 chunks.
+    // 256 x 4 against 512 x 2 / 512 x 4 / 1024 x 2 / 256 x 8 / 256 x 2 / 128 x 8 / 128 x 4 at
+    // 65,536 x 30 in place: 629.5 against 714 / 678 / 790 / 695 / 675 / 624 / 641 us; 128 x 8
+    // loses 15 % at N = 16 and 64 where 256 x 4 wins (profiles/ab_r02/r02w_flat1b_*,
+    // r02w_flat1c_*). A persistent form that keeps the next tile's loads in flight needs
+    // 160 VGPRs (3 waves per SIMD): 2x slower.
     // 128 x 8 (2 waves, 8 chunks per lane, the same 16 KiB tiles) where every tile holds at
     // most two envs (1,023 .. 1,999 chunks per env: N = 20 .. 39 at W = 50) and the window
     // streams through HBM: 0.5-1.1 % ahead of 256 x 4 from 49,152 envs at N = 30 (65,536:
     // 625.7 vs 629.4 and 628.8 vs 631.6 us; 98,304: 941.1 vs 951.6), N = 20 / 24 / 28 by
     // 1.0 / 0.7 / 0.5 %; behind it at 16,384 envs (162.9 vs 161.4) and at N = 16 / 64
-    // (profiles/ab_r02/r02w_flat1k_*, r02w_flat1l_*, r02w_flat1c_*)
-    const bool band128 = h->per4 >= 1023u && h->per4 < 2000u && win > (1ll << 30);
-    if (band128 && flat1_fits(128, 8)) { h->flat1_block = 128; h->flat1_vec = 8; }
-    else if (flat1_fits(256, 4)) { h->flat1_block = 256; h->flat1_vec = 4; }
+    // (profiles/ab_r02/r02w_flat1k_*, r02w_flat1l_*, r02w_flat1c_*). Wide envs: 256 x 4.
+    const bool band128 = c.num_assets <= 64 && h->per4 >= 1023u && h->per4 < 2000u && win > (1ll << 30);
+    if (band128 && flat1_fits(h, 128, 8)) { h->flat1_block = 128; h->flat1_vec = 8; }
+    else if (flat1_fits(h, 256, 4)) { h->flat1_block = 256; h->flat1_vec = 4; }
     else { h->flat1_block = 512; h->flat1_vec = 2; }
-    h->flat1_ok = flat1_fits(h->flat1_block, h->flat1_vec);
+    h->flat1_ok = flat1_fits(h, h->flat1_block, h->flat1_vec) && (c.num_assets <= 64 || h->flat1_block == 256);
     // AUTO: above the one-launch-per-env windows (48 MiB) the flat step beats the two-launch
     // stream by 1-3.5 % for env windows of >= 1,000 chunks (N >= 16 at W = 50): 65,536 x 30
     // 629.5 / 639.7 against 642.4 / 648.8 us on two boxes, N = 24 / 40 / 48 / 64 by 1-3.4 %,
@@ -965,8 +294,6 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // 65,536 x 30 at 0.0025 642.8 vs 661.9 us on two launches (profiles/ab_r03/comm3_r03.err;
     // in round 2 the fixed point cost it 6-8 %: 701 vs 662).
     h->flat1_auto = 0;
-    const int one_auto_base = h->one_auto;   // tools: PMENV_FLAT1=0 restores it
-    (void)one_auto_base;
     if (h->flat1_ok && c.num_assets <= 64 && h->flat1_block <= 256 && h->per4 >= 1000u) {
         if (win > (48ll << 20)) h->flat1_auto |= PMENV_FUSE_DB;
         if (win > (256ll << 20)) h->flat1_auto |= PMENV_FUSE_INPLACE;
@@ -980,25 +307,12 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // wide_r03wide.err). AUTO gives it in-place windows > 1 GiB at N <= 128 without commission.
     if (h->flat1_ok && c.num_assets > 64 && c.num_assets <= 128 && win > (1ll << 30) && !(c.commission > 0.0))
         h->flat1_auto |= PMENV_FUSE_INPLACE;
-#ifdef PMENV_AB
-    if (const char* knob = ab_knob("PMENV_FLAT1")) {   // tools: 1 = the flat step for every window, 0 = never
-        h->flat1_auto = h->flat1_ok && atoi(knob) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
-        h->one_auto = h->flat1_auto ? 0 : one_auto_base;
+
+    pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
+    if (h->streaming) {
+        h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
+        h->units_per_env_db = (c.num_assets + h->unit_rows_db - 1) / h->unit_rows_db;
     }
-    h->flat1_xcd = ab_int("PMENV_FLAT1_XCD", 0) != 0;
-    h->flat1_pol = ab_int("PMENV_FLAT1_POL", 0);
-    if (const char* knob = ab_knob("PMENV_FLAT1_GEOM")) {   // "512x2" | "512x4" | "1024x2" | "256x8" | ...
-        int bk = 0, vv = 0;
-        if (sscanf(knob, "%dx%d", &bk, &vv) == 2) {
-            const int key = bk * 100 + vv;
-            if ((key == 51202 || key == 51204 || key == 102402 || key == 25604 || key == 25608 || key == 25602 ||
-                 key == 12808 || key == 12804) && flat1_fits(bk, vv)) {
-                h->flat1_block = bk;
-                h->flat1_vec = vv;
-            }
-        }
-    }
-#endif
     h->path = PMENV_STEP_PATH_AUTO;
     h->one = h->one_auto;
     h->flat1 = h->flat1_auto;
@@ -1115,6 +429,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
 int pmenv_destroy(pmenv* h) {
     if (!h) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
+    pmenv_tools::release(h);
     if (h->state && h->owns_state) (void)hipFree(h->state);
     if (h->halo) (void)hipFree(h->halo);
     if (h->snap) (void)hipFree(h->snap);
@@ -1207,15 +522,10 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
             launch_one(h, p, stream);
             return check_launch(h, "step_env_kernel");
         }
-
-#ifdef PMENV_AB
-        if (ph == (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE) && (h->fused & fuse_bit)) {
-            launch_fused(h, p, stream);
-            return check_launch(h, "advance_rows_kernel<fused>");
-        }
-#endif
+        if (pmenv_tools::launch_fused(h, p, fuse_bit, ph, stream)) return check_launch(h, "tools: fused step");
         if (ph & PMENV_PHASE_SCALAR) {
-            const int rc = launch_scalar(h, p, stream);
+            launch_scalar(h, p, stream);
+            const int rc = check_launch(h, "scalar_step_kernel");
             if (rc) return rc;
         }
         if (ph & PMENV_PHASE_ADVANCE) {
@@ -1251,8 +561,7 @@ const char* pmenv_step_path(const pmenv* h) {
     // per window mode: the one-launch kernel, or the scalar step (K1) then the stream
     const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
                    : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
-    const char* db2 = h->flat ? (h->flat_db_wg ? "advance_flat_wg_kernel" : "advance_flat_kernel")
-                    : "advance_rows_kernel";
+    const char* db2 = h->flat ? "advance_flat_wg_kernel" : "advance_rows_kernel";
     const char* ip2 = h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
     static thread_local char buf[2][128], out[320];
     const char* part[2];
@@ -1260,7 +569,6 @@ const char* pmenv_step_path(const pmenv* h) {
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
         if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
         else if (h->one & bit) part[m] = "step_env_kernel";
-        else if (h->fused & bit) part[m] = "advance_rows_kernel<fused>";
         else {
             snprintf(buf[m], sizeof buf[m], "%s+%s", k1, m ? ip2 : db2);
             part[m] = buf[m];
@@ -1349,47 +657,15 @@ int pmenv_window_init_days(float* obs, const float* series, int32_t T, int32_t N
 int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
               int32_t B, float gamma, float lam, hipStream_t stream) {
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
+    int rc = PMENV_OK;
+    if (pmenv_tools::gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream, &rc)) return rc;
     // measured on MI355X (tools/bench_rows.py, profiles/rows_r01.json): the tiled scan
     // beats the per-env loop 2.7x at T = 256 x B = 65536 and 14x at 2048 x 8192; the
     // wave-per-env scan only for a handful of envs with long horizons
-    const char* knob = ab_knob("PMENV_GAE");      // tools: loop | scan | tile
     const bool fits = (size_t)(T + 1) * (size_t)B * 4u < (1ull << 31);   // gae_tile_kernel's buffer offsets
-    const bool scan = knob ? !strcmp(knob, "scan") : (B < 64 && T >= 256);
-    const bool tile = fits && (knob ? !strcmp(knob, "tile") : !scan);
-    const int U = ab_int("PMENV_GAE_U", B >= 16384 ? 8 : 16);   // tools: steps per lane and segment
-#ifdef PMENV_AB
-    // PMENV_GAE_E: envs per lane of the pipelined tile (gae_tile_vec_kernel; 1, 2 or 4,
-    // needs B % E == 0); 0 = gae_tile_kernel
-    int E = ab_int("PMENV_GAE_E", 0);
-    if (E != 1 && E != 2 && E != 4) E = 0;
-    if (E && B % E) E = 0;
-    if (knob && !strcmp(knob, "tile8") && fits) {   // tools: the tile held to 64 VGPRs (8 waves per SIMD)
-        gae_tile_kernel<8, 8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-    if (knob && !strcmp(knob, "stream") && fits) {   // PMENV_GAE_P: days per block (16 or 32)
-        const unsigned g = (unsigned)((B + 63) / 64);
-        if (ab_int("PMENV_GAE_P", 16) == 32)
-            gae_stream_kernel<32><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
-        else if (ab_int("PMENV_GAE_P", 16) == 8)
-            gae_stream_kernel<8><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
-        else
-            gae_stream_kernel<16><<<g, 64, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam);
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-    if (tile && E) {
-        const unsigned g = (unsigned)((B + 64 * E - 1) / (64 * E));
-#define PMENV_GAEV(U_, E_) \
-    gae_tile_vec_kernel<8, U_, E_><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam)
-        if (E == 1 && U == 16) PMENV_GAEV(16, 1);
-        else if (E == 1) PMENV_GAEV(8, 1);
-        else if (E == 2 && U == 4) PMENV_GAEV(4, 2);
-        else if (E == 2) PMENV_GAEV(8, 2);
-        else PMENV_GAEV(4, 4);                    // E = 4 at U = 8 spills
-#undef PMENV_GAEV
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-#endif
+    const bool scan = B < 64 && T >= 256;
+    const bool tile = fits && !scan;
+    const int U = B >= 16384 ? 8 : 16;           // steps per lane and segment
     // many envs and at least four 64-day segments: the tile held to 64 VGPRs (8 waves per
     // SIMD, so a 65,536-env rollout's 1,024 workgroups are resident at once; the same bits):
     // 56.7 vs 58.5 us at 256 x 65,536, 110.1 vs 114.7 at 512 x 65,536; slower below 65,536
@@ -1441,8 +717,9 @@ int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
     int lc = 0;
     const int n = gae_chunks(T, B, &lc);
-    const char* knob = ab_knob("PMENV_GAE");      // tools: an explicit kernel choice wins
-    if (!n || knob || !work || work_bytes < (size_t)2 * n * B * sizeof(double))
+    int rc = PMENV_OK;
+    if (pmenv_tools::gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream, &rc)) return rc;
+    if (!n || !work || work_bytes < (size_t)2 * n * B * sizeof(double))
         return pmenv_gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream);
     const dim3 grid((unsigned)((B + 63) / 64), (unsigned)n);
     gae_chunk_kernel<8, 16, true><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
@@ -1470,6 +747,10 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     if (!series || !days || !actions || !rewards || !h0 || !env || !s || !s_next || !a_out || !r_out || T < 1 ||
         N < 1 || F < 2 || W < 1 || H < W + 1 || B < 1 || S < 1)
         return PMENV_ERR_ARG;
+    int rc = PMENV_OK;
+    if (pmenv_tools::replay_gather(series, T, N, F, W, days, actions, rewards, H, B, h0, env, S, s, s_next, a_out,
+                                   r_out, stream, &rc))
+        return rc;
     // F = 5: vector staging per asset group (replay_gather_f5p_kernel, persistent; or
     // replay_gather_f5_kernel, one workgroup per sample); otherwise one workgroup per
     // sample with the W+1 staged days in LDS when they fit in 64 KiB, else one thread per
@@ -1482,7 +763,7 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     // of 4 (16-B aligned groups), R*(W+1) <= 2,048 (day, asset) pairs (at most 8 per
     // thread); N = 30, W = 50: R = 30, one group per sample
     int R = 0;
-    if (F == 5 && al16 && !ab_knob("PMENV_REPLAY_LDS")) {   // tools: the per-element staging kernel
+    if (F == 5 && al16) {
         // the largest group within 2,048 pairs: whole samples measured faster than
         // 10-asset groups (131 vs 148 us at N = 30, W = 50) — every workgroup pays the
         // sample's dependent index loads once
@@ -1495,64 +776,29 @@ int pmenv_replay_gather(const float* series, int32_t T, int32_t N, int32_t F, in
     if (R > 0) {
         const FastDiv dr = make_fastdiv((uint32_t)R), dwf = make_fastdiv((uint32_t)(W * F));
         const size_t glds = (size_t)R * (W + 1) * F * sizeof(float);
-        const dim3 grid((unsigned)S, (unsigned)(N / R));
         const int pairs = R * (W + 1);
         // s / s' are written once per sample: nt stores, 129.6 -> 118.6 us at S = 8,192
         // (tools/ab_replay.py, profiles/ab_r01/replay_nt_tpb_r01h.log). Persistent form
         // (replay_gather_f5p_kernel): one workgroup per CU loops over the samples with the
         // next sample's loads in flight. One per CU is the measured optimum (S = 8,192:
         // 96 us at 256 workgroups; 114-121 us at 192, 288, 512, 768, 1,280 and one
-        // workgroup per sample, 117 us; profiles/ab_r01/replay_grid_r01j.log). Tools knobs:
-        // PMENV_REPLAY_NT=0 (default-policy stores), PMENV_REPLAY_PERSIST=0 (one workgroup
-        // per sample), PMENV_REPLAY_TPB=512, PMENV_REPLAY_GRID=G.
-        const bool nt = ab_int("PMENV_REPLAY_NT", 1) != 0;
-        const bool t512 = ab_int("PMENV_REPLAY_TPB", 256) == 512;
-        const bool persist = !t512 && ab_int("PMENV_REPLAY_PERSIST", 1) != 0;
-        if (persist) {
-            static int cus = 0;
-            if (!cus) {
-                int dev = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                    cus = 256;
-            }
-            const int gy = N / R;
-            int G = cus / gy > 0 ? cus / gy : 1;
-            G = ab_int("PMENV_REPLAY_GRID", G) > 0 ? ab_int("PMENV_REPLAY_GRID", G) : G;
-            const dim3 pgrid((unsigned)(S < G ? S : G), (unsigned)(N / R));
-            const int ppt = pairs <= 2 * 256 ? 2 : pairs <= 4 * 256 ? 4 : 8;
-#define PMENV_RGP(PPT, NTV)                                                                                   \
-    replay_gather_f5p_kernel<PPT, NTV><<<pgrid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, \
-                                                                     h0, env, S, s, s_next, a_out, r_out, R, dr, dwf)
-#ifdef PMENV_AB
-            if (!nt) {
-                if (ppt == 2) PMENV_RGP(2, 0); else if (ppt == 4) PMENV_RGP(4, 0); else PMENV_RGP(8, 0);
-                return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-            }
-#endif
-            if (ppt == 2) PMENV_RGP(2, 2); else if (ppt == 4) PMENV_RGP(4, 2); else PMENV_RGP(8, 2);
+        // workgroup per sample, 117 us; profiles/ab_r01/replay_grid_r01j.log).
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+        const int gy = N / R;
+        const int G = cus / gy > 0 ? cus / gy : 1;
+        const dim3 pgrid((unsigned)(S < G ? S : G), (unsigned)(N / R));
+        const int ppt = pairs <= 2 * 256 ? 2 : pairs <= 4 * 256 ? 4 : 8;
+#define PMENV_RGP(PPT)                                                                                        \
+    replay_gather_f5p_kernel<PPT, 2><<<pgrid, 256, glds, stream>>>(series, T, N, W, days, actions, rewards, H, B, \
+                                                                   h0, env, S, s, s_next, a_out, r_out, R, dr, dwf)
+        if (ppt == 2) PMENV_RGP(2); else if (ppt == 4) PMENV_RGP(4); else PMENV_RGP(8);
 #undef PMENV_RGP
-            return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-        }
-#ifdef PMENV_AB
-        const int tpb = t512 ? 512 : 256;
-        const int ppt = pairs <= 2 * tpb ? 2 : pairs <= 4 * tpb ? 4 : 8;
-#define PMENV_RG(PPT, NTV, TPB)                                                                              \
-    replay_gather_f5_kernel<PPT, NTV, TPB><<<grid, TPB, glds, stream>>>(series, T, N, W, days, actions, rewards, \
-                                                                        H, B, h0, env, s, s_next, a_out, r_out, \
-                                                                        R, dr, dwf)
-        if (t512) {
-            if (nt) { if (ppt == 2) PMENV_RG(2, 2, 512); else if (ppt == 4) PMENV_RG(4, 2, 512); else PMENV_RG(8, 2, 512); }
-            else { if (ppt == 2) PMENV_RG(2, 0, 512); else if (ppt == 4) PMENV_RG(4, 0, 512); else PMENV_RG(8, 0, 512); }
-        } else {
-            if (nt) { if (ppt == 2) PMENV_RG(2, 2, 256); else if (ppt == 4) PMENV_RG(4, 2, 256); else PMENV_RG(8, 2, 256); }
-            else { if (ppt == 2) PMENV_RG(2, 0, 256); else if (ppt == 4) PMENV_RG(4, 0, 256); else PMENV_RG(8, 0, 256); }
-        }
-#undef PMENV_RG
-#else
-        (void)grid;
-        (void)nt;
-#endif
     } else if (lds <= 64 * 1024 && N <= 256 && ((uintptr_t)s & 15u) == 0 && ((uintptr_t)s_next & 15u) == 0) {
         replay_gather_lds_kernel<<<(unsigned)S, 256, lds, stream>>>(series, T, N, F, W, days, actions, rewards, H, B,
                                                                    h0, env, s, s_next, a_out, r_out);
@@ -1570,22 +816,15 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     if (!series || !start || (!weights && T_rec > 0) || !t_idx || !env || !s || T < 1 || N < 1 || F < 2 || W < 1 ||
         T_rec < 0 || B < 1 || S < 1 || ring_mode < 0 || ring_mode > 1)
         return PMENV_ERR_ARG;
-#ifdef PMENV_AB
-    if (ab_knob("PMENV_RGATHER_ELEM")) {          // tools: one thread per output float
-        const int64_t threads = (int64_t)S * N * W * F;
-        rollout_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
-            series, T, N, F, W, start, weights, T_rec, B, ring_mode, t_idx, env, S, s);
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-#endif
+    int rc = PMENV_OK;
+    if (pmenv_tools::rollout_gather(series, T, N, F, W, start, weights, T_rec, B, ring_mode, t_idx, env, S, s,
+                                    stream, &rc))
+        return rc;
     const size_t lds = (size_t)W * N * F * sizeof(float);
     // market [W][N][4] + weights [W][N]; the tile's 16-B series loads and window stores need
     // 16-B aligned series / s (C callers may pass sliced views: those take the row form)
     const bool al16 = (((uintptr_t)series | (uintptr_t)s) & 15u) == 0;
-    bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && al16;
-#ifdef PMENV_AB
-    if (ab_knob("PMENV_RGATHER_ROWS")) tile = false;      // tools: the wave-per-row form
-#endif
+    const bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && al16;
     if (tile) {                                            // one workgroup per sample, staged in LDS
         rollout_gather_tile_kernel<<<(unsigned)S, 256, lds, stream>>>(
             series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N),
@@ -1601,28 +840,16 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
 int pmenv_metrics(const double* returns, const double* values, const float* weights, int32_t T, int32_t B, int32_t N,
                   double risk_free_rate, double periods, double* out, hipStream_t stream) {
     if (!returns || !values || !weights || !out || T < 1 || B < 1 || N < 1 || !(periods > 0.0)) return PMENV_ERR_ARG;
-    // measured on MI355X (tools/bench_rows.py): the horizon split over four waves per
-    // 64 envs against the thread-per-env walk — see profiles/rows_r01*/
+    int rc = PMENV_OK;
+    if (pmenv_tools::metrics(returns, values, weights, T, B, N, risk_free_rate, periods, out, stream, &rc)) return rc;
+    // measured on MI355X (tools/bench_rows.py): the segment walk (the horizon split over
+    // four waves per 64 envs) beside the turnover stream, in one launch — against the
+    // thread-per-env walk and the two-launch form (profiles/rows_r01*/)
     const int tpe = N <= 256 ? N : 256, eb = 256 / tpe;
     const int nseg = (B + 63) / 64, nturn = (B + eb - 1) / eb;
-    // one launch for both passes (metrics_fused_kernel); A/B knobs: PMENV_METRICS_FUSED=0
-    // (two launches), PMENV_METRICS_SEG_FIRST=0 (turnover blocks dispatched first)
-    const bool walk = ab_knob("PMENV_METRICS_WALK") != nullptr;  // tools: the thread-per-env walk
-    const bool fused = !walk && ab_int("PMENV_METRICS_FUSED", 1) != 0;
-    if (fused) {
-        const int seg_first = ab_int("PMENV_METRICS_SEG_FIRST", 1) != 0;
-        metrics_fused_kernel<<<(unsigned)(nseg + nturn), 256, 0, stream>>>(returns, values, weights, T, B, N,
-                                                                           risk_free_rate, periods, tpe, eb, nseg,
-                                                                           nturn, seg_first, out);
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-#ifdef PMENV_AB
-    if (walk)
-        metrics_kernel<<<(B + 255) / 256, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
-    else
-        metrics_seg_kernel<<<(unsigned)nseg, 256, 0, stream>>>(returns, values, T, B, risk_free_rate, periods, out);
-    metrics_turnover_kernel<<<(unsigned)nturn, 256, 0, stream>>>(weights, T, B, N, tpe, eb, out);
-#endif
+    metrics_fused_kernel<<<(unsigned)(nseg + nturn), 256, 0, stream>>>(returns, values, weights, T, B, N,
+                                                                       risk_free_rate, periods, tpe, eb, nseg,
+                                                                       nturn, 1, out);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
@@ -1636,38 +863,12 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         reward_kind != PMENV_REWARD_SHARPE)
         return PMENV_ERR_ARG;
     if (norm < PMENV_BNORM_GLOBAL_OR || norm > PMENV_BNORM_NONE) return PMENV_ERR_ARG;
-    // one launch: the row blocks' partials and, in the block that finishes last, the
-    // final fold (batch_reward_fwd_*_kernel; the ticket it counts on is zeroed first)
-#ifdef PMENV_AB
-    // tools: the forward in one launch (batch_reward_fwd_*_kernel: the block that draws
-    // the last ticket folds the partials). Measured slower than the two launches below at
-    // every shape, so the product keeps the two.
-    if (ab_knob("PMENV_BR_ONE")) {
-        if (hipMemsetAsync(work + 6 * (size_t)B + 6, 0, sizeof(uint32_t), stream) != hipSuccess) return PMENV_ERR_HIP;
-        const bool quad = N <= kQuadMaxN;
-        const int nblk = quad ? (B + kQuadRows - 1) / kQuadRows : (int)batch_reward_blocks(B);
-        int grid = nblk, fence = 1;
-        if (const char* knob = ab_knob("PMENV_BR_GRID")) grid = std::max(1, std::min(nblk, atoi(knob)));
-        if (const char* knob = ab_knob("PMENV_BR_FENCE")) fence = atoi(knob);
-        const unsigned g = (unsigned)grid;
-#define PMENV_FWD_ARGS a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, nblk
-        if (quad) {
-            if (fence == 0) {
-                if (N <= 32) batch_reward_fwd_quad_kernel<8, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-                else batch_reward_fwd_quad_kernel<16, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-            } else if (N <= 32) batch_reward_fwd_quad_kernel<8, 1><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-            else batch_reward_fwd_quad_kernel<16, 1><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-        } else {
-            if (N <= 128) batch_reward_fwd_rows_kernel<2, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-            else if (N <= 256) batch_reward_fwd_rows_kernel<4, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-            else if (N <= 512) batch_reward_fwd_rows_kernel<8, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-            else batch_reward_fwd_rows_kernel<0, 0><<<g, kTrainBlock, 0, stream>>>(PMENV_FWD_ARGS);
-        }
-#undef PMENV_FWD_ARGS
-        if (ret_out) batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
-        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
-    }
-#endif
+    int rc = PMENV_OK;
+    if (pmenv_tools::batch_reward_forward(a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, ret_out,
+                                          stream, &rc))
+        return rc;
+    // two launches: the row blocks' partials, then the final fold (a one-launch form with a
+    // last-block ticket measured slower at every shape: DESIGN.md §7 f2)
     int nparts;
     if (N <= kQuadMaxN) {         // a quad of lanes per row
         nparts = (B + kQuadRows - 1) / kQuadRows;
@@ -1718,3 +919,45 @@ int pmenv_batch_reward_backward(const float* a, const float* v_prev, const float
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- tools-build hooks
+// The product library's hooks do nothing; tools/ab/pmenv_ab.hip (linked only into
+// tools/libpmenv_ab.so) overrides these weak definitions.
+namespace pmenv_tools {
+__attribute__((weak, noinline)) void plan(pmenv*) {}
+__attribute__((weak, noinline)) void release(pmenv*) {}
+__attribute__((weak, noinline)) bool launch_scalar(const pmenv*, const StepParams&, hipStream_t) { return false; }
+__attribute__((weak, noinline)) bool launch_advance(const pmenv*, const StepParams&, hipStream_t) { return false; }
+__attribute__((weak, noinline)) bool launch_one(const pmenv*, const StepParams&, hipStream_t) { return false; }
+__attribute__((weak, noinline)) bool launch_fused(const pmenv*, const StepParams&, int, uint32_t, hipStream_t) {
+    return false;
+}
+__attribute__((weak, noinline)) bool launch_flat1(const pmenv*, const StepParams&, unsigned, bool, int,
+                                                  hipStream_t) {
+    return false;
+}
+__attribute__((weak, noinline)) bool gae(const float*, const float*, const uint8_t*, float*, float*, int32_t,
+                                         int32_t, float, float, hipStream_t, int*) {
+    return false;
+}
+__attribute__((weak, noinline)) bool replay_gather(const float*, int32_t, int32_t, int32_t, int32_t, const int32_t*,
+                                                   const float*, const float*, int32_t, int32_t, const int32_t*,
+                                                   const int32_t*, int32_t, float*, float*, float*, float*,
+                                                   hipStream_t, int*) {
+    return false;
+}
+__attribute__((weak, noinline)) bool rollout_gather(const float*, int32_t, int32_t, int32_t, int32_t, const int32_t*,
+                                                    const float*, int32_t, int32_t, int32_t, const int32_t*,
+                                                    const int32_t*, int32_t, float*, hipStream_t, int*) {
+    return false;
+}
+__attribute__((weak, noinline)) bool metrics(const double*, const double*, const float*, int32_t, int32_t, int32_t,
+                                             double, double, double*, hipStream_t, int*) {
+    return false;
+}
+__attribute__((weak, noinline)) bool batch_reward_forward(const float*, const float*, const float*, int32_t, int32_t,
+                                                          int32_t, int32_t, double, double*, float*, float*,
+                                                          hipStream_t, int*) {
+    return false;
+}
+}  // namespace pmenv_tools

@@ -17,7 +17,7 @@
 namespace pmenv_dev {
 
 // one thread per output float of s and s' (both [S, N, W, F]); a/r by the first threads
-__global__ void replay_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* days,
+static __global__ void replay_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* days,
                                      const float* actions, const float* rewards, int H, int B, const int32_t* h0,
                                      const int32_t* env, int S, float* s, float* s_next, float* a_out,
                                      float* r_out) {
@@ -64,35 +64,6 @@ __global__ void replay_gather_kernel(const float* series, int T, int N, int F, i
 // ring is full (u >= W-1) the reference returns it in storage order (:38-39): position
 // p holds update j with j % W == p, i.e. chronological c = (p - u - 1) mod W.
 // Days outside the series read NaN.
-#ifdef PMENV_AB   // tools build: one thread per output float ([S, N, W, F], coalesced stores)
-__global__ void rollout_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* start,
-                                      const float* weights, int T_rec, int B, int ring_mode, const int32_t* t_idx,
-                                      const int32_t* env, int S, float* s) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t per = (int64_t)N * W * F;
-    if (i >= (int64_t)S * per) return;
-    const int Fm = F - 1;
-    const int j = (int)(i / per);
-    int rem = (int)(i - (int64_t)j * per);
-    const int n = rem / (W * F);
-    rem -= n * W * F;
-    const int p = rem / F, f = rem - p * F;
-    const int b = env[j], t = t_idx[j];
-    float v;
-    if (f < Fm) {
-        const int d = start[b] + t + p;
-        v = (d >= 0 && d < T) ? series[((size_t)d * N + n) * Fm + f] : NAN;
-    } else {
-        const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
-        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
-        const int r = t + c;                       // history row
-        if (r < W - 1) v = 0.0f;
-        else if (r == W - 1) v = n == 0 ? 1.0f : 0.0f;
-        else v = weights[((size_t)(r - W) * B + b) * N + n];
-    }
-    s[i] = v;
-}
-#endif
 
 constexpr int kRowGatherUnroll = 8;   // rows of W*F <= 512 floats: all loads first
 
@@ -100,7 +71,7 @@ constexpr int kRowGatherUnroll = 8;   // rows of W*F <= 512 floats: all loads fi
 // lane, lane + 64, ... of the row (each store one contiguous 256-B run), the day and
 // channel from the row offset by one multiply-shift, the sample's env / step / start
 // wave-uniform. The float-per-thread form (tools build) spends its time in 64-bit divisions.
-__global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const float* series, int T, int N, int F, int W,
+static __global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const float* series, int T, int N, int F, int W,
                                                                   const int32_t* start, const float* weights,
                                                                   int B, int ring_mode, const int32_t* t_idx,
                                                                   const int32_t* env, int S, float* s, FastDiv div_f) {
@@ -145,7 +116,7 @@ __global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const float* s
 // contiguous run of [T_rec, B, N] — and the [N, W, 5] window is written as 16-B chunks
 // from LDS (a lane's four floats walk (asset, day, channel) incrementally). Every weight
 // line is fetched once per sample, where the per-row form fetches it per asset row.
-__global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
+static __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
                                                                   const int32_t* start, const float* weights, int B,
                                                                   int ring_mode, const int32_t* t_idx,
                                                                   const int32_t* env, float* s, FastDiv div_n,
@@ -216,40 +187,6 @@ __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* s
     }
 }
 
-#ifdef PMENV_AB   // tools build: the thread-per-env walk (the fused kernel replaced it)
-// one thread per env walks its column of the trajectory (coalesced across envs)
-//   out[b] = {sharpe, sortino, max drawdown, average turnover, final value}
-__global__ void metrics_kernel(const double* returns, const double* values, int T, int B, double rf,
-                               double periods, double* out) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    // qs.stats.sharpe / sortino: excess returns over the per-period rate
-    // (1 + rf)^(1/periods) - 1, annualised by sqrt(periods)
-    const double rfp = rf != 0.0 ? pow(1.0 + rf, 1.0 / periods) - 1.0 : 0.0;
-    double mean = 0.0, m2 = 0.0, down = 0.0;
-    for (int t = 0; t < T; ++t) {
-        const double x = returns[(size_t)t * B + b] - rfp;
-        const double d = x - mean;
-        mean += d / (t + 1);
-        m2 += d * (x - mean);
-        down += x < 0.0 ? x * x : 0.0;
-    }
-    const double sd = T > 1 ? sqrt(m2 / (T - 1)) : NAN;
-    const double sharpe = mean / sd * sqrt(periods);
-    const double sortino = mean / sqrt(down / T) * sqrt(periods);
-    // qs.stats.max_drawdown on the value curve: min_t (V_t / max_{s<=t} V_s - 1)
-    double peak = -INFINITY, mdd = 0.0;
-    for (int t = 0; t <= T; ++t) {
-        const double v = values[(size_t)t * B + b];
-        peak = fmax(peak, v);
-        mdd = fmin(mdd, v / peak - 1.0);
-    }
-    out[(size_t)b * 5 + 0] = sharpe;
-    out[(size_t)b * 5 + 1] = sortino;
-    out[(size_t)b * 5 + 2] = mdd;
-    out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
-}
-#endif
 
 
 // The same per-env metrics with the horizon split over the four waves of a
@@ -329,12 +266,6 @@ __device__ __forceinline__ void metrics_seg_body(const double* returns, const do
     out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
 }
 
-#ifdef PMENV_AB   // tools build: the two-launch form of metrics_fused_kernel
-__global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
-                                                          double rf, double periods, double* out) {
-    metrics_seg_body(returns, values, T, B, rf, periods, out, (int)blockIdx.x);
-}
-#endif
 
 // util/eval.py:32-37 average turnover, element-parallel: a workgroup owns `eb` whole
 // envs (N <= 256: one thread per (env, asset), so each day's read is eb*N contiguous
@@ -377,18 +308,12 @@ __device__ __forceinline__ void metrics_turnover_body(const float* weights, int 
     }
 }
 
-#ifdef PMENV_AB
-__global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
-                                                               int eb, double* out) {
-    metrics_turnover_body(weights, T, B, N, tpe, eb, out, (int)blockIdx.x);
-}
-#endif
 
 // Both metric passes in one launch: they read disjoint inputs and write disjoint
 // fields of out, so the latency-bound segment walk (returns, values) runs beside the
 // bandwidth-bound turnover stream (weights) instead of before it. Blocks [0, nseg)
 // take the segment walk when seg_first, else the turnover blocks come first.
-__global__ __launch_bounds__(256) void metrics_fused_kernel(const double* returns, const double* values,
+static __global__ __launch_bounds__(256) void metrics_fused_kernel(const double* returns, const double* values,
                                                             const float* weights, int T, int B, int N, double rf,
                                                             double periods, int tpe, int eb, int nseg, int nturn,
                                                             int seg_first, double* out) {
@@ -402,7 +327,7 @@ __global__ __launch_bounds__(256) void metrics_fused_kernel(const double* return
 // spans — market channels from the series, channel F-1 from the recorded actions —
 // are staged in LDS as [N][W+1][F], then s (days 0..W-1) and s' (days 1..W) are
 // written as whole 16-B chunks when the sample block is 16-B granular.
-__global__ __launch_bounds__(256) void replay_gather_lds_kernel(const float* series, int T, int N, int F, int W,
+static __global__ __launch_bounds__(256) void replay_gather_lds_kernel(const float* series, int T, int N, int F, int W,
                                                                 const int32_t* days, const float* actions,
                                                                 const float* rewards, int H, int B,
                                                                 const int32_t* h0, const int32_t* env, float* s,

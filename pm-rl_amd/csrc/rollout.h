@@ -9,7 +9,7 @@ namespace pmenv_dev {
 // ---------------------------------------------------------------- GAE / moments
 // One thread per env walks its column of the [T, B] rollout backwards; for a fixed
 // t the B threads touch B consecutive floats, so every access is coalesced.
-__global__ void gae_kernel(const float* r, const float* v, const uint8_t* dones, float* adv, float* ret,
+static __global__ void gae_kernel(const float* r, const float* v, const uint8_t* dones, float* adv, float* ret,
                            int T, int B, float gamma, float lam) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
@@ -39,7 +39,7 @@ __device__ __forceinline__ void gae_delta(const float* r, const float* v, const 
     *c = (double)gamma * (double)lam * nd;
 }
 
-__global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const float* v, const uint8_t* dones,
+static __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const float* v, const uint8_t* dones,
                                                        float* adv, float* ret, int T, int B, float gamma, float lam) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -337,7 +337,7 @@ constexpr int kMomBlocks = 1024;
 // {sum, sum of squares} per block into work[2 * block]: 16-B loads (after a scalar
 // head up to the first 16-B boundary), four in flight per thread, f64 accumulation,
 // fixed thread -> element assignment (deterministic for a given n).
-__global__ __launch_bounds__(kMomBlock) void moments_partial_kernel(const float* x, int64_t n, double* work) {
+static __global__ __launch_bounds__(kMomBlock) void moments_partial_kernel(const float* x, int64_t n, double* work) {
     __shared__ double sh[2][kMomBlock / 64];
     const int64_t head = min<int64_t>(n, (int64_t)(((16u - ((uintptr_t)x & 15u)) & 15u) / 4u));
     const f4* x4 = reinterpret_cast<const f4*>(x + head);
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(kMomBlock) void moments_partial_kernel(const float*
 // one workgroup folds the block partials in a fixed shape: thread t adds partials
 // t, t + 256, ... in order, then a DPP/shuffle tree per wave and the 4 wave totals
 // in order
-__global__ __launch_bounds__(kMomBlock) void moments_final_kernel(int nblocks, int64_t n, const double* work,
+static __global__ __launch_bounds__(kMomBlock) void moments_final_kernel(int nblocks, int64_t n, const double* work,
                                                                   double* out) {
     __shared__ double sh[2][kMomBlock / 64];
     double s = 0.0, q = 0.0;

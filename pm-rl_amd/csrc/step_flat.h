@@ -219,8 +219,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void st
 // reductions need every asset — but stages only the rows it touches: the bar rows and w'
 // of at most 64 rows per env (host-checked), the same LDS as the narrow kernel. The
 // snapshot, the halo and the device sequencing are step_flat_kernel's.
-constexpr int kWideMaxAssets = 512;
-
 template <int A, int BLOCK, int V, int POL, bool OUT>
 __global__ __launch_bounds__(BLOCK) void step_flat_vec_kernel(StepParams p, uint32_t qtot) {
     constexpr int kAuxL = POL == 1 ? 2 : 0, kAuxS = POL == 1 ? 2 : 0;
@@ -348,7 +346,7 @@ __device__ __forceinline__ void flat_prime(const StepParams& p, bool snap) {
 // step's window, and publishes C = D for the flat kernel (which reads nothing else of
 // seq). *_out / halo point at parity 0, the kernel adds parity D's offset (`stride`
 // bytes between the parities).
-__global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, uint64_t stride) {
+static __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, uint64_t stride) {
     const int d = __builtin_amdgcn_readfirstlane(p.seq[0]);
     const int valid = __builtin_amdgcn_readfirstlane(p.seq[2]);
     const uint64_t hobs = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(p.seq[4]) |
@@ -370,6 +368,6 @@ __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, ui
 
 // Prime the snapshot (parity p) from the canonical state and, in place, the halo of
 // parity p from the window: halo[i] = chunks (i+1)*CPW and (i+1)*CPW + 1 (copy_halo).
-__global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) { flat_prime(p, true); }
+static __global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) { flat_prime(p, true); }
 
 }  // namespace pmenv_dev

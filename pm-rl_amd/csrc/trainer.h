@@ -472,76 +472,15 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
 }
 
 // the second launch of the forward: one workgroup folds the row blocks' partials
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, int kind, int norm, double scale,
+static __global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(int B, int kind, int norm, double scale,
                                                                          double* work, float* reward_out,
                                                                          int nparts) {
     final_fold(B, kind, norm, scale, work, reward_out, nparts);
 }
 
-#ifdef PMENV_AB
-// ---------------------------------------------------------------- tools: the forward in one launch
-// The row blocks write their partials as above; then every block takes a ticket from a
-// device-scope counter (work[6B + 6], zeroed by the host before the launch), and the block
-// that draws the last ticket folds all partials with final_fold — the same code and
-// order as batch_reward_final_kernel, so both forms give the same bits. Release: the
-// partials' writers fence before the block barrier and the ticket; acquire: the last
-// block fences before reading the other blocks' partials (they live in other XCDs' L2).
-// No block waits for another: blocks that are not last simply exit. Measured: the
-// agent-scope fences (an L2 write-back per block) cost more than the second launch they
-// save, at every shape and grid tried — kept here as that evidence.
-__device__ __forceinline__ uint32_t* batch_reward_ticket(double* work, int B) {
-    return reinterpret_cast<uint32_t*>(work + 6 * (size_t)B + 6);
-}
-
-// FENCE 0: every thread fences its own stores; 1: only thread 0 (after the barrier that
-// orders the block's stores, all of which thread 0 made in the quad form)
-template <int FENCE>
-__device__ __forceinline__ bool drew_last_ticket(uint32_t* ticket) {
-    __shared__ uint32_t last;
-    if (FENCE == 0) __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (FENCE == 1) __threadfence();
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!last) return false;
-    __threadfence();
-    return true;
-}
-
-// nblk row blocks over the grid (grid-stride: a block may produce several partials)
-template <int EPL, int FENCE>
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(const float* a, const float* v_prev,
-                                                                            const float* p, int B, int N, int kind,
-                                                                            int norm, double scale, double* work,
-                                                                            float* reward_out, int nblk) {
-    __shared__ double rec_w[4][kPartStride];
-    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, blk, nblk);
-        __syncthreads();                                          // rec_w is reused
-    }
-    if (drew_last_ticket<FENCE>(batch_reward_ticket(work, B)))
-        final_fold(B, kind, norm, scale, work, reward_out, nblk);
-}
-
-template <int EPL, int FENCE>
-__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(const float* a, const float* v_prev,
-                                                                            const float* p, int B, int N, int kind,
-                                                                            int norm, double scale, double* work,
-                                                                            float* reward_out, int nblk) {
-    __shared__ double sh[4][kRowsPerBlock];
-    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, blk, nblk);
-        __syncthreads();
-    }
-    if (drew_last_ticket<FENCE == 1 ? 0 : FENCE>(batch_reward_ticket(work, B)))   // several writer lanes
-        final_fold(B, kind, norm, scale, work, reward_out, nblk);
-}
-#endif
 
 // elementwise: each row's chosen return and normalisation flag (for the backward)
-__global__ __launch_bounds__(256) void batch_reward_select_kernel(int B, int norm, double* work, float* ret_out) {
+static __global__ __launch_bounds__(256) void batch_reward_select_kernel(int B, int norm, double* work, float* ret_out) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= B) return;
     bool nb;

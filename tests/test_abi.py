@@ -101,7 +101,7 @@ def test_product_does_not_reference_the_oracle():
 def test_product_library_reads_no_knobs_and_has_no_ablation_variants():
     """The product library calls no getenv (nothing in the environment can alter the
     timed path) and carries none of the timing-only variants of the tools build
-    (tools/libpmenv_ab.so, -DPMENV_AB): no work-skipping ABL / SKIP instantiations, no
+    (tools/libpmenv_ab.so, linked with tools/ab/pmenv_ab.hip): no work-skipping ABL / SKIP instantiations, no
     80-SGPR twins, no A/B-only geometries."""
     from pmenv import _abi
     undef = subprocess.run(["nm", "-D", "--undefined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
@@ -148,3 +148,18 @@ def test_c_caller_links_the_abi():
     line = next(l for l in out.splitlines() if "libpmenv.so" in l)
     assert "not found" not in line and os.path.realpath(line.split("=>")[1].split()[0]) == \
         os.path.realpath(os.path.join(ROOT, "pm-rl_amd", "pmenv", "libpmenv.so"))
+
+
+def test_product_dispatch_has_no_conditional_compilation():
+    """The product's host side (pmenv.hip, launch.h, handle.h) reads straight through: no
+    #if / #ifdef, no environment variable; the tools build's variants sit in tools/ab/
+    behind the pmenv_tools hooks, whose product definitions are weak no-ops."""
+    csrc = os.path.join(ROOT, "pm-rl_amd", "csrc")
+    for f in ("pmenv.hip", "launch.h", "handle.h"):
+        txt = open(os.path.join(csrc, f)).read()
+        assert not re.search(r"^\s*#\s*if", txt, re.M), f"{f} has conditional compilation"
+        assert "getenv" not in txt, f"{f} reads the environment"
+    from pmenv import _abi
+    syms = subprocess.run(["nm", "-C", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    hooks = [l for l in syms.splitlines() if "pmenv_tools::" in l]
+    assert hooks and all(l.split()[1] == "W" for l in hooks), "the product's tools hooks must be the weak no-ops"

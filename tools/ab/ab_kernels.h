@@ -1,0 +1,146 @@
+// ab_kernels.h — device kernels of the tools build only (tools/libpmenv_ab.so): the
+// alternatives the product measured against and replaced. Moved out of
+// pm-rl_amd/csrc/replay.h and trainer.h, whose device helpers they use.
+#pragma once
+#include "../../pm-rl_amd/csrc/replay.h"
+#include "../../pm-rl_amd/csrc/trainer.h"
+
+namespace pmenv_dev {
+
+// from replay.h: tools build: one thread per output float ([S, N, W, F], coalesced stores)
+static __global__ void rollout_gather_kernel(const float* series, int T, int N, int F, int W, const int32_t* start,
+                                      const float* weights, int T_rec, int B, int ring_mode, const int32_t* t_idx,
+                                      const int32_t* env, int S, float* s) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = (int64_t)N * W * F;
+    if (i >= (int64_t)S * per) return;
+    const int Fm = F - 1;
+    const int j = (int)(i / per);
+    int rem = (int)(i - (int64_t)j * per);
+    const int n = rem / (W * F);
+    rem -= n * W * F;
+    const int p = rem / F, f = rem - p * F;
+    const int b = env[j], t = t_idx[j];
+    float v;
+    if (f < Fm) {
+        const int d = start[b] + t + p;
+        v = (d >= 0 && d < T) ? series[((size_t)d * N + n) * Fm + f] : NAN;
+    } else {
+        const bool storage = ring_mode == PMENV_RING_STORAGE && t >= W - 1;
+        const int c = storage ? (((p - t - 1) % W) + W) % W : p;
+        const int r = t + c;                       // history row
+        if (r < W - 1) v = 0.0f;
+        else if (r == W - 1) v = n == 0 ? 1.0f : 0.0f;
+        else v = weights[((size_t)(r - W) * B + b) * N + n];
+    }
+    s[i] = v;
+}
+
+// from replay.h: tools build: the thread-per-env walk (the fused kernel replaced it)
+// one thread per env walks its column of the trajectory (coalesced across envs)
+//   out[b] = {sharpe, sortino, max drawdown, average turnover, final value}
+static __global__ void metrics_kernel(const double* returns, const double* values, int T, int B, double rf,
+                               double periods, double* out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    // qs.stats.sharpe / sortino: excess returns over the per-period rate
+    // (1 + rf)^(1/periods) - 1, annualised by sqrt(periods)
+    const double rfp = rf != 0.0 ? pow(1.0 + rf, 1.0 / periods) - 1.0 : 0.0;
+    double mean = 0.0, m2 = 0.0, down = 0.0;
+    for (int t = 0; t < T; ++t) {
+        const double x = returns[(size_t)t * B + b] - rfp;
+        const double d = x - mean;
+        mean += d / (t + 1);
+        m2 += d * (x - mean);
+        down += x < 0.0 ? x * x : 0.0;
+    }
+    const double sd = T > 1 ? sqrt(m2 / (T - 1)) : NAN;
+    const double sharpe = mean / sd * sqrt(periods);
+    const double sortino = mean / sqrt(down / T) * sqrt(periods);
+    // qs.stats.max_drawdown on the value curve: min_t (V_t / max_{s<=t} V_s - 1)
+    double peak = -INFINITY, mdd = 0.0;
+    for (int t = 0; t <= T; ++t) {
+        const double v = values[(size_t)t * B + b];
+        peak = fmax(peak, v);
+        mdd = fmin(mdd, v / peak - 1.0);
+    }
+    out[(size_t)b * 5 + 0] = sharpe;
+    out[(size_t)b * 5 + 1] = sortino;
+    out[(size_t)b * 5 + 2] = mdd;
+    out[(size_t)b * 5 + 4] = values[(size_t)T * B + b];
+}
+
+// from replay.h: tools build: the two-launch form of metrics_fused_kernel
+static __global__ __launch_bounds__(256) void metrics_seg_kernel(const double* returns, const double* values, int T, int B,
+                                                          double rf, double periods, double* out) {
+    metrics_seg_body(returns, values, T, B, rf, periods, out, (int)blockIdx.x);
+}
+
+// from replay.h
+static __global__ __launch_bounds__(256) void metrics_turnover_kernel(const float* weights, int T, int B, int N, int tpe,
+                                                               int eb, double* out) {
+    metrics_turnover_body(weights, T, B, N, tpe, eb, out, (int)blockIdx.x);
+}
+
+// from trainer.h
+// ---------------------------------------------------------------- tools: the forward in one launch
+// The row blocks write their partials as above; then every block takes a ticket from a
+// device-scope counter (work[6B + 6], zeroed by the host before the launch), and the block
+// that draws the last ticket folds all partials with final_fold — the same code and
+// order as batch_reward_final_kernel, so both forms give the same bits. Release: the
+// partials' writers fence before the block barrier and the ticket; acquire: the last
+// block fences before reading the other blocks' partials (they live in other XCDs' L2).
+// No block waits for another: blocks that are not last simply exit. Measured: the
+// agent-scope fences (an L2 write-back per block) cost more than the second launch they
+// save, at every shape and grid tried — kept here as that evidence.
+__device__ __forceinline__ uint32_t* batch_reward_ticket(double* work, int B) {
+    return reinterpret_cast<uint32_t*>(work + 6 * (size_t)B + 6);
+}
+
+// FENCE 0: every thread fences its own stores; 1: only thread 0 (after the barrier that
+// orders the block's stores, all of which thread 0 made in the quad form)
+template <int FENCE>
+__device__ __forceinline__ bool drew_last_ticket(uint32_t* ticket) {
+    __shared__ uint32_t last;
+    if (FENCE == 0) __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (FENCE == 1) __threadfence();
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return false;
+    __threadfence();
+    return true;
+}
+
+// nblk row blocks over the grid (grid-stride: a block may produce several partials)
+template <int EPL, int FENCE>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(const float* a, const float* v_prev,
+                                                                            const float* p, int B, int N, int kind,
+                                                                            int norm, double scale, double* work,
+                                                                            float* reward_out, int nblk) {
+    __shared__ double rec_w[4][kPartStride];
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, blk, nblk);
+        __syncthreads();                                          // rec_w is reused
+    }
+    if (drew_last_ticket<FENCE>(batch_reward_ticket(work, B)))
+        final_fold(B, kind, norm, scale, work, reward_out, nblk);
+}
+
+template <int EPL, int FENCE>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(const float* a, const float* v_prev,
+                                                                            const float* p, int B, int N, int kind,
+                                                                            int norm, double scale, double* work,
+                                                                            float* reward_out, int nblk) {
+    __shared__ double sh[4][kRowsPerBlock];
+    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, blk, nblk);
+        __syncthreads();
+    }
+    if (drew_last_ticket<FENCE == 1 ? 0 : FENCE>(batch_reward_ticket(work, B)))   // several writer lanes
+        final_fold(B, kind, norm, scale, work, reward_out, nblk);
+}
+
+}  // namespace pmenv_dev
