@@ -102,6 +102,12 @@ __device__ __forceinline__ const float* env_bar(const StepParams& p, int b) {
     return (d >= 0 && d < p.series_days) ? p.bar + (size_t)d * row : nullptr;
 }
 
+// branch-free float select (bit masks: keeps element loops free of control flow)
+__device__ __forceinline__ float pick(bool c, float a, float b) {
+    const int m = -(int)c;
+    return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+}
+
 // ---------------------------------------------------------------- buffer access
 // Range-checked buffer loads/stores (CDNA SRSRC descriptors): a lane whose byte
 // offset falls outside [0, bytes) reads 0 / stores nothing, so prologues need no

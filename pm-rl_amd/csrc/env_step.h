@@ -386,7 +386,10 @@ __device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int
         if (p.bar) {
             if (ROW) {
                 const int c = p.close_ch;
-                cn = in.bar_ok ? (c == 0 ? in.bar.x : c == 1 ? in.bar.y : c == 2 ? in.bar.z : in.bar.w) : NAN;
+                // bit-mask selects: the nested ?: chain on the runtime channel was miscompiled
+                // in step_split_kernel (ROCm 7.2 clang: channel 3 took the .y component)
+                cn = pick(in.bar_ok, pick(c == 0, in.bar.x, pick(c == 1, in.bar.y, pick(c == 2, in.bar.z, in.bar.w))),
+                          __int_as_float(0x7fc00000));
             } else {
                 cn = in.cn;
             }
@@ -727,11 +730,6 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
 // The bar is fetched only by lanes whose chunk touches the row's last day (the other
 // lanes' offsets are out of the descriptor's range: no traffic).
 // Requirements (host-checked): F == 5, W >= 2, N*W*F % 4 == 0, B*N*W*F/4 < 2^31.
-// branch-free float select (bit masks: keeps the element loop free of control flow)
-__device__ __forceinline__ float pick(bool c, float a, float b) {
-    const int m = -(int)c;
-    return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
-}
 
 // What chunk q of the flat stream needs besides its input chunks: its position in
 // its asset row, the row's bar (only lanes whose chunk touches the last day load it;
@@ -744,8 +742,10 @@ struct FlatSide {
     int32_t k;
 };
 
-// SKIP (timing-only ablation bits, 0 in the product): 1 bar, 2 w', 4 counter, 8 day
-template <int SKIP = 0>
+// SKIP (timing-only ablation bits, 0 in the product): 1 bar, 2 w', 4 counter, 8 day.
+// KOFF: what the counter read lags behind the step's (1: the scalar kernel already counted
+// this step; 0: step_split_kernel's snapshot, the counter before the step)
+template <int SKIP = 0, int KOFF = 1>
 __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t q) {
     constexpr int F = 5;
     const int N = p.N, WF = p.W * F;
@@ -770,7 +770,7 @@ __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t
     const uint32_t bar_off = touch_last && !sd.bar_nan ? (bar_row * (uint32_t)N + row) * 16u : 0xFFFFFFF0u;
     sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f} : buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
     sd.xwp = (SKIP & 2) ? 0.5f : p.w_new[(size_t)b * N + row];
-    sd.k = (SKIP & 4) ? 0 : p.k[b] - 1;                                   // scalar_step_kernel counted this step
+    sd.k = (SKIP & 4) ? 0 : p.k[b] - KOFF;                                // scalar_step_kernel counted this step
     return sd;
 }
 
@@ -881,9 +881,9 @@ __device__ __forceinline__ f4 sel_bar(int i, const i16v_t& r) {
               __int_as_float(sel4(i, r[2], r[6], r[10], r[14])), __int_as_float(sel4(i, r[3], r[7], r[11], r[15]))};
 }
 
-template <int SKIP = 0>
+template <int SKIP = 0, int KOFF = 1>
 __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, const WaveSide& ws, uint32_t q) {
-    if (!ws.ok) return flat_side_load<SKIP>(p, q);
+    if (!ws.ok) return flat_side_load<SKIP, KOFF>(p, q);
     constexpr int F = 5;
     const int N = p.N, WF = p.W * F;
     const uint32_t per4 = (uint32_t)(N * WF) >> 2;
@@ -914,7 +914,7 @@ __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, con
     }
     sd.xwp = (SKIP & 2) ? 0.5f : __int_as_float(sel4(i, ws.w4[0], ws.w4[1], ws.w4[2], ws.w4[3]));
     const int mk = -(int)in_b;
-    sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - 1;   // scalar_step_kernel counted this step
+    sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - KOFF;   // scalar_step_kernel counted this step
     return sd;
 }
 
