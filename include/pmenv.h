@@ -187,7 +187,6 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
  * "<obs_out path> (obs_out) | <in-place path> (in place)", each either
  * "step_flat_kernel" (the whole step in one launch over 16 KiB window tiles),
  * "step_flat_vec_kernel" (the same for 64 < N <= 512),
- * "step_split_kernel" (in place: one launch of stream tiles beside scalar workgroups),
  * "step_env_kernel" (the whole step in one launch, one workgroup per env) or
  * "<scalar step>+<window stream>"
  * (two launches); or "step_advance_lds_kernel" (single-launch fallback, any F). */
@@ -199,14 +198,11 @@ const char* pmenv_step_path(const pmenv* h);
  * kernel followed by the window stream (F = 5, 16-B granular env windows); FLAT forces
  * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:
  * F = 5, W >= 2, env windows of >= 148 16-B chunks, N <= 64 — or, as step_flat_vec_kernel,
- * 64 < N <= 512 with W >= 14); SPLIT forces step_split_kernel for in-place windows (the
- * whole step in one launch whose stream tiles never wait for the scalar step: scalar
- * workgroups, one wave per env, write w' into the window themselves; F = 5, W >= 2,
- * N <= 64, 16-B granular env windows) and FLAT's kernel for obs_out. Returns PMENV_ERR_ARG
+ * 64 < N <= 512 with W >= 14). Returns PMENV_ERR_ARG
  * (handle unchanged) when the shape does not fit the requested path. For N <= 64 every
  * path gives the same bits; the N > 64 scalar-step forms reduce in another order.
  *
- * FLAT and SPLIT keep a per-step snapshot of the state its scalar step reads and, in place, the
+ * FLAT keeps a per-step snapshot of the state its scalar step reads and, in place, the
  * halo of its tiles, both produced by the previous step: a caller that writes the state
  * blob (pmenv_create_in, e.g. the value) or an in-place window outside this API — or that
  * hands in a different window at the address of the last one — must say so before the
@@ -222,8 +218,7 @@ typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,
     PMENV_STEP_PATH_TWO_LAUNCH = 2,
-    PMENV_STEP_PATH_FLAT = 3,
-    PMENV_STEP_PATH_SPLIT = 4
+    PMENV_STEP_PATH_FLAT = 3
 } pmenv_step_path_kind;
 int pmenv_set_step_path(pmenv* h, int32_t path);
 

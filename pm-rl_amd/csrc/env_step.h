@@ -386,8 +386,8 @@ __device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int
         if (p.bar) {
             if (ROW) {
                 const int c = p.close_ch;
-                // bit-mask selects: the nested ?: chain on the runtime channel was miscompiled
-                // in step_split_kernel (ROCm 7.2 clang: channel 3 took the .y component)
+                // bit-mask selects: a nested ?: chain on the runtime channel was miscompiled in
+                // one kernel (ROCm 7.2 clang: channel 3 read the .y component)
                 cn = pick(in.bar_ok, pick(c == 0, in.bar.x, pick(c == 1, in.bar.y, pick(c == 2, in.bar.z, in.bar.w))),
                           __int_as_float(0x7fc00000));
             } else {
@@ -742,10 +742,8 @@ struct FlatSide {
     int32_t k;
 };
 
-// SKIP (timing-only ablation bits, 0 in the product): 1 bar, 2 w', 4 counter, 8 day.
-// KOFF: what the counter read lags behind the step's (1: the scalar kernel already counted
-// this step; 0: step_split_kernel's snapshot, the counter before the step)
-template <int SKIP = 0, int KOFF = 1>
+// SKIP (timing-only ablation bits, 0 in the product): 1 bar, 2 w', 4 counter, 8 day
+template <int SKIP = 0>
 __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t q) {
     constexpr int F = 5;
     const int N = p.N, WF = p.W * F;
@@ -770,7 +768,7 @@ __device__ __forceinline__ FlatSide flat_side_load(const StepParams& p, uint32_t
     const uint32_t bar_off = touch_last && !sd.bar_nan ? (bar_row * (uint32_t)N + row) * 16u : 0xFFFFFFF0u;
     sd.xb = (SKIP & 1) ? f4{1.f, 1.f, 1.f, 1.f} : buf_load4<0>(make_rsrc(p.bar, bar_bytes), bar_off);
     sd.xwp = (SKIP & 2) ? 0.5f : p.w_new[(size_t)b * N + row];
-    sd.k = (SKIP & 4) ? 0 : p.k[b] - KOFF;                                // scalar_step_kernel counted this step
+    sd.k = (SKIP & 4) ? 0 : p.k[b] - 1;                                   // scalar_step_kernel counted this step
     return sd;
 }
 
@@ -881,9 +879,9 @@ __device__ __forceinline__ f4 sel_bar(int i, const i16v_t& r) {
               __int_as_float(sel4(i, r[2], r[6], r[10], r[14])), __int_as_float(sel4(i, r[3], r[7], r[11], r[15]))};
 }
 
-template <int SKIP = 0, int KOFF = 1>
+template <int SKIP = 0>
 __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, const WaveSide& ws, uint32_t q) {
-    if (!ws.ok) return flat_side_load<SKIP, KOFF>(p, q);
+    if (!ws.ok) return flat_side_load<SKIP>(p, q);
     constexpr int F = 5;
     const int N = p.N, WF = p.W * F;
     const uint32_t per4 = (uint32_t)(N * WF) >> 2;
@@ -914,7 +912,7 @@ __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, con
     }
     sd.xwp = (SKIP & 2) ? 0.5f : __int_as_float(sel4(i, ws.w4[0], ws.w4[1], ws.w4[2], ws.w4[3]));
     const int mk = -(int)in_b;
-    sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - KOFF;   // scalar_step_kernel counted this step
+    sd.k = (SKIP & 4) ? 0 : ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - 1;   // scalar_step_kernel counted this step
     return sd;
 }
 

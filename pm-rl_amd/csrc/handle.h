@@ -60,13 +60,6 @@ struct pmenv {
     int flat1_auto;       // PMENV_FUSE_* bits the automatic choice gives it
     int flat1;            // PMENV_FUSE_* bits: which windows take it now
     int flat1_block, flat1_vec;   // threads per workgroup, chunks per thread
-    // one launch in place with the scalar step decoupled from the window stream
-    // (step_split_kernel: scalar workgroups beside the stream tiles)
-    bool split_ok;        // the shape fits it: the flat stream's rules, N <= 64
-    bool split_auto;      // the automatic choice gives it the in-place windows
-    bool split;           // in-place flat steps take it now (instead of step_flat_kernel)
-    int split_block, split_vec;   // stream tile: threads per workgroup, chunks per thread
-    int snap_kind;        // the kernel whose snapshot / halo sv .. halo1 hold: 0 none, 1 flat, 2 split
     void* snap;           // the state snapshot, two parities: value f64 | counter i32 | get_last() | last close
     double* sv[2];
     int32_t* sk[2];
@@ -227,7 +220,6 @@ bool launch_one(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stre
 bool launch_fused(const pmenv* h, const pmenv_dev::StepParams& p, int fuse_bit, uint32_t phases, hipStream_t stream);
 bool launch_flat1(const pmenv* h, const pmenv_dev::StepParams& p, unsigned grid, bool out, int pol,
                   hipStream_t stream);
-bool launch_split(const pmenv* h, const pmenv_dev::StepParams& p, int pol, hipStream_t stream);
 bool gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
          int32_t B, float gamma, float lam, hipStream_t stream, int* rc);
 bool replay_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W, const int32_t* days,

@@ -8,7 +8,6 @@
 #include "scalar_vec.h"
 #include "step_env.h"
 #include "step_flat.h"
-#include "step_split.h"
 
 namespace pmenv_host {
 
@@ -167,48 +166,16 @@ inline void launch_flat1_kernels(const pmenv* h, const StepParams& p, unsigned g
     }
 }
 
-// step_split_kernel: nscalar scalar workgroups (one wave per env) interleaved one per R
-// workgroups with the stream tiles
-template <int BK, int VV>
-inline void launch_split_g(const StepParams& p, uint32_t qtot, int pol, hipStream_t stream) {
-    const uint32_t cpw = (uint32_t)(BK * VV);
-    const uint32_t ntiles = (qtot + cpw - 1) / cpw;
-    const uint32_t nscalar = (uint32_t)((p.B + BK / 64 - 1) / (BK / 64));
-    const uint32_t R = (ntiles + nscalar) / nscalar > 2u ? (ntiles + nscalar) / nscalar : 2u;
-    const uint32_t rest = ntiles > nscalar * (R - 1) ? ntiles - nscalar * (R - 1) : 0u;
-    const unsigned grid = nscalar * R + rest;
-    if (pol == 1) step_split_kernel<BK, VV, 1><<<grid, BK, 0, stream>>>(p, qtot, ntiles, nscalar, R);
-    else step_split_kernel<BK, VV, 0><<<grid, BK, 0, stream>>>(p, qtot, ntiles, nscalar, R);
-}
-
-inline void launch_split_kernels(const pmenv* h, const StepParams& p, int pol, hipStream_t stream) {
-    if (pmenv_tools::launch_split(h, p, pol, stream)) return;
-    if (h->split_block == 512) launch_split_g<512, 2>(p, h->flat_qtot, pol, stream);
-    else launch_split_g<256, 2>(p, h->flat_qtot, pol, stream);
-}
-
-// the whole step in one launch over the flat stream (step_flat.h, step_split.h): prime the
-// snapshot and the halo when something other than this kernel touched them, then one launch
+// the whole step in one launch over the flat stream (step_flat.h): prime the snapshot and
+// the halo when something other than this kernel touched them, then one launch
 inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     const bool out = p.obs_out != p.obs;
-    const bool split = !out && h->split;
-    const int kind = split ? 2 : 1;
-    if (h->snap_kind != kind) {
-        // the other kernel's snapshot (its get_last() / halo geometry differ): prime anew
-        h->snap_ok = false;
-        h->halo1_obs = nullptr;
-        if (h->device_seq) (void)hipMemsetAsync(h->seq + 2, 0, 4, stream);
-        h->snap_kind = kind;
-    }
     const int q = h->par;
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
     const bool need_halo = !out && h->halo1_obs != p.obs;
     const int64_t work = (int64_t)h->cfg.num_envs * h->cfg.num_assets;
     const unsigned prime_grid = (unsigned)(work / 256 + 1 < 2048 ? work / 256 + 1 : 2048);
-    const uint32_t cpw = split ? (uint32_t)(h->split_block * h->split_vec) : (uint32_t)(h->flat1_block * h->flat1_vec);
-    const uint32_t tiles = (h->flat_qtot + cpw - 1) / cpw;
-    const uint32_t halo_wgs = tiles > 0 ? tiles - 1 : 0;
     if (h->device_seq) {
         // parity 0 in *_in / halo_in, parity 1 in *_out / halo_out; the sequencer primes
         // parity D if needed and publishes it, the kernel swaps when it is 1
@@ -220,18 +187,18 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
         StepParams pp = p;
         pp.sv_out = h->sv[0]; pp.sk_out = h->sk[0]; pp.sw_out = h->sw[0]; pp.slc_out = h->slc[0];
         pp.halo = h->halo1[0];
-        pp.halo_wgs = halo_wgs;
-        pp.halo_block = cpw;
+        pp.halo_wgs = h->halo1_wgs;
+        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
         pp.halo_qtot = h->flat_qtot;
-        flat_seq_kernel<<<prime_grid, 256, 0, stream>>>(pp, out ? 1 : 0, h->snap_stride, split ? 1 : 0);
+        flat_seq_kernel<<<prime_grid, 256, 0, stream>>>(pp, out ? 1 : 0, h->snap_stride);
     } else if (!h->snap_ok || need_halo) {
         StepParams pp = p;
         pp.sv_out = h->sv[q]; pp.sk_out = h->sk[q]; pp.sw_out = h->sw[q]; pp.slc_out = h->slc[q];
         pp.halo = need_halo ? h->halo1[q] : nullptr;
-        pp.halo_wgs = halo_wgs;
-        pp.halo_block = cpw;
+        pp.halo_wgs = h->halo1_wgs;
+        pp.halo_block = (uint32_t)(h->flat1_block * h->flat1_vec);
         pp.halo_qtot = h->flat_qtot;
-        flat_prime_kernel<<<prime_grid, 256, 0, stream>>>(pp, split ? 1 : 0);
+        flat_prime_kernel<<<prime_grid, 256, 0, stream>>>(pp);
     }
     if (!h->device_seq) {
         p.sv_in = h->sv[q]; p.sk_in = h->sk[q]; p.sw_in = h->sw[q]; p.slc_in = h->slc[q];
@@ -240,8 +207,9 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
         p.halo_out = h->halo1[1 - q];
     }
     const int pol = out ? h->flat_pol : h->flat_ip_pol;
-    if (split) launch_split_kernels(h, p, pol, stream);
-    else if (!pmenv_tools::launch_flat1(h, p, tiles, out, pol, stream)) launch_flat1_kernels(h, p, tiles, out, pol, stream);
+    const uint32_t cpw = (uint32_t)(h->flat1_block * h->flat1_vec);
+    const unsigned grid = (h->flat_qtot + cpw - 1) / cpw;
+    if (!pmenv_tools::launch_flat1(h, p, grid, out, pol, stream)) launch_flat1_kernels(h, p, grid, out, pol, stream);
     h->par = 1 - q;
     h->snap_ok = true;
     h->halo1_obs = out ? nullptr : p.obs;

@@ -73,7 +73,7 @@ enum { kInvalSnap = 1, kInvalHalo = 2 };
 int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInvalHalo, bool host_only = false) {
     if (what & kInvalSnap) h->snap_ok = false;
     h->halo1_obs = nullptr;
-    if (host_only || !(h->flat1_ok || h->split_ok)) return PMENV_OK;
+    if (host_only || !h->flat1_ok) return PMENV_OK;
     if (!h->device_seq && h->flat1 && capturing(stream)) h->device_seq = true;
     if (!h->device_seq) return PMENV_OK;
     // V = 0 clears both (a stale V re-primes the halo too); HOBS = 0 only the halo
@@ -91,13 +91,11 @@ int one_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_ONE_LAUNCH) return h->one_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
     if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming ? 0 : -1;
     if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? 0 : -1;
-    if (path == PMENV_STEP_PATH_SPLIT) return h->split_ok ? 0 : -1;
     return h->one_auto;
 }
 int flat1_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
-    if (path == PMENV_STEP_PATH_SPLIT) return h->split_ok ? (PMENV_FUSE_INPLACE | (h->flat1_ok ? PMENV_FUSE_DB : 0)) : -1;
-    if (path == PMENV_STEP_PATH_AUTO) return h->flat1_auto | (h->split_auto ? PMENV_FUSE_INPLACE : 0);
+    if (path == PMENV_STEP_PATH_AUTO) return h->flat1_auto;
     return 0;
 }
 
@@ -309,13 +307,6 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // wide_r03wide.err). AUTO gives it in-place windows > 1 GiB at N <= 128 without commission.
     if (h->flat1_ok && c.num_assets > 64 && c.num_assets <= 128 && win > (1ll << 30) && !(c.commission > 0.0))
         h->flat1_auto |= PMENV_FUSE_INPLACE;
-    // ---- the split one-launch step (step_split_kernel, in place): the flat stream's tiles
-    // (8 KiB on cache-resident windows, 16 KiB above, as the two-launch stream) beside one
-    // scalar workgroup per four (eight) envs. AUTO: not yet.
-    h->split_ok = h->flat_ok && c.num_assets <= 64;
-    h->split_block = win <= (256ll << 20) ? 256 : 512;
-    h->split_vec = 2;
-    h->split_auto = false;
 
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {
@@ -325,9 +316,6 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->path = PMENV_STEP_PATH_AUTO;
     h->one = h->one_auto;
     h->flat1 = h->flat1_auto;
-    h->split = h->split_auto;
-    if (h->split) h->flat1 |= PMENV_FUSE_INPLACE;
-    h->snap_kind = 0;
 
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
@@ -373,14 +361,12 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             return fail(PMENV_ERR_HIP);
         }
     }
-    if (h->flat1_ok || h->split_ok) {
-        // two parities of the snapshot (16-B aligned fields) and of the tile halo (for the
-        // smaller of the two kernels' tiles)
+    if (h->flat1_ok) {
+        // two parities of the snapshot (16-B aligned fields) and of the tile halo
         const size_t B = (size_t)c.num_envs, BN = B * (size_t)c.num_assets;
         auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
         const size_t one = up16(B * 8) + up16(B * 4) + 2 * up16(BN * 4);
-        uint32_t cpw = (uint32_t)(h->flat1_block * h->flat1_vec);
-        if (h->split_ok && (uint32_t)(h->split_block * h->split_vec) < cpw) cpw = (uint32_t)(h->split_block * h->split_vec);
+        const uint32_t cpw = (uint32_t)(h->flat1_block * h->flat1_vec);
         const uint32_t wgs = (h->flat_qtot + cpw - 1) / cpw;
         h->halo1_wgs = wgs > 0 ? wgs - 1 : 0;
         const size_t hal = up16(((size_t)h->halo1_wgs + 1) * 32);
@@ -453,7 +439,7 @@ int pmenv_destroy(pmenv* h) {
 
 int pmenv_set_step_path(pmenv* h, int32_t path) {
     if (!h) return PMENV_ERR_ARG;
-    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_SPLIT) {
+    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_FLAT) {
         set_err(h, "unknown step path %d", path);
         return PMENV_ERR_ARG;
     }
@@ -462,14 +448,12 @@ int pmenv_set_step_path(pmenv* h, int32_t path) {
     if (bits < 0 || fbits < 0) {
         set_err(h, "step path %d does not fit this shape (one launch: F = 5, W >= 2, N <= 64, window <= 64 KiB "
                    "of LDS; two launches: F = 5, 16-B granular env windows; flat: F = 5, W >= 2, N <= 64, "
-                   "16-B granular env windows of >= 148 chunks, N > 64 up to 512 with W >= 14; split: F = 5, "
-                   "W >= 2, N <= 64, 16-B granular env windows)", path);
+                   "16-B granular env windows of >= 148 chunks, N > 64 up to 512 with W >= 14)", path);
         return PMENV_ERR_ARG;
     }
     h->path = path;
     h->one = bits;
     h->flat1 = fbits;
-    h->split = path == PMENV_STEP_PATH_SPLIT || (path == PMENV_STEP_PATH_AUTO && h->split_auto);
     return PMENV_OK;
 }
 
@@ -523,7 +507,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         // handle sequences its flat steps on the device (flat_seq_kernel + the kernel)
         if (!h->device_seq && capturing(stream)) h->device_seq = true;
         launch_flat1(h, p, stream);
-        return check_launch(h, fuse_bit == PMENV_FUSE_INPLACE && h->split ? "step_split_kernel" : "step_flat_kernel");
+        return check_launch(h, "step_flat_kernel");
     }
     if (const int rc = flat1_invalidate(h, stream)) return rc;   // every other path skips the snapshot
     if (!a->bar) {
@@ -583,8 +567,7 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-        if ((h->flat1 & bit) && m == 1 && h->split) part[m] = "step_split_kernel";
-        else if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
+        if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
         else if (h->one & bit) part[m] = "step_env_kernel";
         else {
             snprintf(buf[m], sizeof buf[m], "%s+%s", k1, m ? ip2 : db2);
@@ -953,7 +936,6 @@ __attribute__((weak, noinline)) bool launch_flat1(const pmenv*, const StepParams
                                                   hipStream_t) {
     return false;
 }
-__attribute__((weak, noinline)) bool launch_split(const pmenv*, const StepParams&, int, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool gae(const float*, const float*, const uint8_t*, float*, float*, int32_t,
                                          int32_t, float, float, hipStream_t, int*) {
     return false;

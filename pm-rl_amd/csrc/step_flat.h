@@ -322,27 +322,20 @@ __global__ __launch_bounds__(BLOCK) void step_flat_vec_kernel(StepParams p, uint
 }
 
 // The snapshot copy (sv_out .. slc_out <- the canonical state, when `snap`) and the halo
-// copy (copy_halo, when p.halo is set), grid-stride over the launch. WWIN (step_split_kernel):
-// sw_out is the window's own last-day weight dwords instead of get_last(), re-read with the
-// halo as well as with the snapshot (both come from the window).
-__device__ __forceinline__ void flat_prime(const StepParams& p, bool snap, bool wwin) {
+// copy (copy_halo, when p.halo is set), grid-stride over the launch.
+__device__ __forceinline__ void flat_prime(const StepParams& p, bool snap) {
     copy_halo(p);
-    const bool w_win = wwin && (snap || p.halo);
-    if (!snap && !w_win) return;
+    if (!snap) return;
     const uint32_t nthr = gridDim.x * blockDim.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t BN = (size_t)p.B * p.N;
-    const size_t WF = (size_t)p.W * p.F;
-    if (snap) {
-        for (size_t i = tid; i < (size_t)p.B; i += nthr) {
-            p.sv_out[i] = p.value[i];
-            p.sk_out[i] = p.k[i];
-        }
+    for (size_t i = tid; i < (size_t)p.B; i += nthr) {
+        p.sv_out[i] = p.value[i];
+        p.sk_out[i] = p.k[i];
     }
     for (size_t i = tid; i < BN; i += nthr) {
-        if (w_win) p.sw_out[i] = p.obs[i * WF + WF - 1];
-        else p.sw_out[i] = p.w_new[i];
-        if (snap) p.slc_out[i] = p.last_close[i];
+        p.sw_out[i] = p.w_new[i];
+        p.slc_out[i] = p.last_close[i];
     }
 }
 
@@ -353,7 +346,7 @@ __device__ __forceinline__ void flat_prime(const StepParams& p, bool snap, bool 
 // step's window, and publishes C = D for the flat kernel (which reads nothing else of
 // seq). *_out / halo point at parity 0, the kernel adds parity D's offset (`stride`
 // bytes between the parities).
-static __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, uint64_t stride, int wwin) {
+static __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int out, uint64_t stride) {
     const int d = __builtin_amdgcn_readfirstlane(p.seq[0]);
     const int valid = __builtin_amdgcn_readfirstlane(p.seq[2]);
     const uint64_t hobs = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(p.seq[4]) |
@@ -368,15 +361,13 @@ static __global__ __launch_bounds__(256) void flat_seq_kernel(StepParams p, int 
         q.sw_out = (float*)((char*)p.sw_out + off);
         q.slc_out = (float*)((char*)p.slc_out + off);
         q.halo = halo ? (float*)((char*)p.halo + off) : nullptr;
-        flat_prime(q, snap, wwin != 0);
+        flat_prime(q, snap);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) p.seq[1] = d;
 }
 
 // Prime the snapshot (parity p) from the canonical state and, in place, the halo of
 // parity p from the window: halo[i] = chunks (i+1)*CPW and (i+1)*CPW + 1 (copy_halo).
-static __global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p, int wwin) {
-    flat_prime(p, true, wwin != 0);
-}
+static __global__ __launch_bounds__(256) void flat_prime_kernel(StepParams p) { flat_prime(p, true); }
 
 }  // namespace pmenv_dev

@@ -91,8 +91,7 @@ class TradingEnv:
     def __init__(self, num_envs=1, num_assets=None, window=None, features=5, device=None,
                  config=None, track_info=False, step_impl="auto", **overrides):
         """step_impl: "auto" (per shape), "one_launch" (step_env_kernel, one workgroup per
-        env), "flat" (step_flat_kernel, one launch over 16 KiB window tiles), "split"
-        (step_split_kernel in place: window tiles beside scalar workgroups, one launch) or
+        env), "flat" (step_flat_kernel, one launch over 16 KiB window tiles) or
         "two_launch" (scalar-step kernel + window stream); see set_step_impl."""
         if config is None:
             kw = dict(num_envs=num_envs, features=features)
@@ -203,7 +202,7 @@ class TradingEnv:
 
     def set_step_impl(self, impl):
         """Advance-mode step implementation (pmenv_set_step_path): "auto", "one_launch",
-        "flat", "split" or "two_launch". Raises ValueError when the shape does not fit it."""
+        "flat" or "two_launch". Raises ValueError when the shape does not fit it."""
         if impl not in _abi.STEP_PATHS:
             raise ValueError(f"step_impl must be one of {sorted(_abi.STEP_PATHS)}")
         rc = self._lib.pmenv_set_step_path(self._h, _abi.STEP_PATHS[impl])

@@ -123,8 +123,7 @@ int main(int argc, char** argv) {
     HIP(hipMemcpy(h_obs0, d_obs, nobs * sizeof(float), hipMemcpyDeviceToHost));
     const struct { int path; const char* name; } paths[] = {
         {PMENV_STEP_PATH_AUTO, "auto"}, {PMENV_STEP_PATH_FLAT, "flat"},
-        {PMENV_STEP_PATH_ONE_LAUNCH, "one_launch"}, {PMENV_STEP_PATH_TWO_LAUNCH, "two_launch"},
-        {PMENV_STEP_PATH_SPLIT, "split"}};
+        {PMENV_STEP_PATH_ONE_LAUNCH, "one_launch"}, {PMENV_STEP_PATH_TWO_LAUNCH, "two_launch"}};
     int bad = 0;
     for (size_t i = 0; i < sizeof paths / sizeof paths[0]; ++i)
         bad |= run_path(paths[i].path, paths[i].name, B, N, W, T, d_series, d_actions, h_series, h_actions, h_obs0);

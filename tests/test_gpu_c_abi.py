@@ -21,6 +21,6 @@ def test_gpu_c_caller_every_step_path(shape):
     out = subprocess.run([BIN, *map(str, shape)], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("c_abi ok")]
-    assert [l.split()[2] for l in lines] == ["auto", "flat", "one_launch", "two_launch", "split"], out.stdout
+    assert [l.split()[2] for l in lines] == ["auto", "flat", "one_launch", "two_launch"], out.stdout
     flat = next(l for l in lines if l.split()[2] == "flat")
     assert flat.count("step_flat_kernel") == 2

@@ -1,9 +1,6 @@
 """step_flat_kernel: the whole advance step in ONE launch over fixed 16 KiB tiles of the
 flat window (the scalar step run by every workgroup an env straddles, the env's state
-written by its owner, a per-step snapshot and in-place halo by parity; step_flat.h) — and
-step_split_kernel (step_split.h: in place, stream tiles that leave each row's w' dword to
-scalar workgroups running beside them in the same launch; the counter and the old
-last-day weights from the snapshot), through the same tests (`impl`).
+written by its owner, a per-step snapshot and in-place halo by parity; step_flat.h).
 
 Checked against the CPU oracle in every mode, bit for bit against the two-launch path
 (and so against every other path) across resets, masked resets, checkpoint restores,
@@ -23,13 +20,6 @@ pytestmark = pytest.mark.gpu
 # straddling chunks, envs at every offset in a tile, a partial last tile
 SHAPES = [(30, 50, 37), (4, 50, 600), (4, 30, 301), (12, 10, 97), (64, 47, 3), (8, 50, 11), (64, 16, 5),
           (33, 20, 5), (2, 60, 130), (1, 600, 9), (64, 2, 50), (40, 3, 21)]   # W = 2, 3: most days are last days
-# the split step takes any 16-B granular env window: also many envs per wave (5 .. 100 chunks)
-SPLIT_SHAPES = [(1, 4, 300), (4, 20, 77), (8, 8, 500), (2, 2, 1001), (16, 5, 64)]
-IMPLS = ["flat", "split"]
-
-
-def _kernel(impl):
-    return "step_split_kernel" if impl == "split" else "step_flat_kernel"
 
 
 def _mode_id(k):
@@ -39,14 +29,11 @@ def _mode_id(k):
 @pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES, ids=_mode_id)
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_vs_oracle_modes(kind, db, kw, impl):
+def test_gpu_flat_vs_oracle_modes(kind, db, kw):
     """Every reward / ring / norm / commission mode, in place and double-buffered, past
     the ring wrap, against the oracle."""
-    if impl == "split" and db:
-        pytest.skip("split is in place; obs_out takes step_flat_kernel")
     _run_both(kw, B=37, N=30, W=50, T=56, kind=kind, seed=zlib.crc32(f"flat{kw}{kind}{db}".encode()),
-              double_buffer=db, impl=impl)
+              double_buffer=db, impl="flat")
 
 
 @pytest.mark.parametrize("N,W,B", SHAPES)
@@ -55,15 +42,6 @@ def test_gpu_flat_shapes_vs_oracle(N, W, B, db):
     _run_both({}, B=B, N=N, W=W, T=W + 7, kind="mixed", seed=N * 13 + W, double_buffer=db, impl="flat")
     _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 7 * W, double_buffer=db,
               impl="flat")
-
-
-@pytest.mark.parametrize("N,W,B", SHAPES + SPLIT_SHAPES)
-def test_gpu_split_shapes_vs_oracle(N, W, B):
-    _run_both({}, B=B, N=N, W=W, T=W + 7, kind="mixed", seed=N * 13 + W, double_buffer=False, impl="split")
-    _run_both({"ring": "chrono"}, B=B, N=N, W=W, T=W + 3, kind="simplex", seed=N + 7 * W, double_buffer=False,
-              impl="split")
-    _run_both({"commission": 0.0025, "reward": "diff_sharpe"}, B=B, N=N, W=W, T=W + 3, kind="rawpos",
-              seed=N + 5 * W, double_buffer=False, impl="split")
 
 
 def _state(e):
@@ -79,8 +57,7 @@ def _same(ga, gb, what):
 @pytest.mark.parametrize("N,W,B", [(30, 50, 37), (4, 30, 301), (64, 47, 3)])
 @pytest.mark.parametrize("kw", [dict(), dict(commission=0.0025, reward="sharpe_ratio"),
                                 dict(ring="chrono", reward="diff_sharpe")], ids=_mode_id)
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw, impl):
+def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw):
     """The flat one-launch step and the two-launch path, driven with the same inputs
     through everything that invalidates the snapshot / halo — full and masked resets,
     a checkpoint restore, a switch to another path and back, a different window buffer,
@@ -93,8 +70,8 @@ def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw, impl)
     kind_mixed = torch.randn(T, B, N, device=DEV, generator=torch.Generator(DEV).manual_seed(3))
     res = synth.series(T + W + 8, 1, N, seed=9, device=DEV)[:, 0].contiguous()
     envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i, track_info=True, **kw)
-            for i in (impl, "two_launch")]
-    assert _kernel(impl) in envs[0].step_path and _kernel(impl) not in envs[1].step_path
+            for i in ("flat", "two_launch")]
+    assert "step_flat_kernel" in envs[0].step_path and "step_flat_kernel" not in envs[1].step_path
     obs = [synth.window_from_series(ser, W) for _ in envs]
     for e, o in zip(envs, obs):
         e.reset(o)
@@ -112,11 +89,7 @@ def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw, impl)
             if t == 20 and i == 0:
                 e.set_step_impl("two_launch")             # another path writes the state...
             if t == 22 and i == 0:
-                e.set_step_impl(impl)                     # ...and the flat step re-primes
-            if t == 24 and i == 0:                        # the other one-launch kernel, and back
-                e.set_step_impl("split" if impl == "flat" else "flat")
-            if t == 25 and i == 0:
-                e.set_step_impl(impl)
+                e.set_step_impl("flat")                   # ...and the flat step re-primes
             if t == 26:                                   # restore the t = 14 checkpoint
                 e.load_state_dict(cks[i])
                 obs[i].copy_(obs_cks[i])
@@ -143,14 +116,13 @@ def test_gpu_flat_bitwise_vs_two_launch_through_state_changes(N, W, B, kw, impl)
         _same(_state(envs[0]), _state(envs[1]), f"step {t}")
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_masked_reset_same_mask(impl):
+def test_gpu_flat_masked_reset_same_mask():
     """Masked resets every sixth step on both paths, state compared after each step."""
     from pmenv import TradingEnv, synth
     B, N, W, T = 300, 4, 30, 40
     ser = synth.series(W + T, B, N, seed=1, device=DEV)
     act = synth.actions(T, B, N, seed=2, device=DEV)
-    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in (impl, "two_launch")]
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
     obs = [synth.window_from_series(ser, W) for _ in envs]
     for e, o in zip(envs, obs):
         e.reset(o)
@@ -166,8 +138,7 @@ def test_gpu_flat_masked_reset_same_mask(impl):
         _same(_state(envs[0]), _state(envs[1]), f"step {t}")
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_graph_capture_and_replay(impl):
+def test_gpu_flat_graph_capture_and_replay():
     """Flat steps captured into a hipGraph (an odd count, so a host-chosen parity would
     go wrong on the second replay): the handle switches to the device-sequenced form and
     graph replays interleave with eager steps, a full reset, a masked reset and a
@@ -179,7 +150,7 @@ def test_gpu_flat_graph_capture_and_replay(impl):
     ser = synth.series(W + D, B, N, seed=7, device=DEV)
     act = synth.actions(D, B, N, seed=8, device=DEV)
     ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
-    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
     obs_a = synth.window_from_series(ser, W)
     obs_b = obs_a.clone()
     ea.reset(obs_a)
@@ -246,8 +217,7 @@ def test_gpu_flat_graph_capture_and_replay(impl):
     assert day <= D
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_graph_captures_a_reset_before_its_steps(impl):
+def test_gpu_flat_graph_captures_a_reset_before_its_steps():
     """A hipGraph whose first node is a reset (masked) followed by flat steps, captured on a
     handle that was host-sequenced until then: the captured reset clears the snapshot's
     valid word, so every replay re-primes from the reset state — replays 2, 3, ... included,
@@ -259,7 +229,7 @@ def test_gpu_flat_graph_captures_a_reset_before_its_steps(impl):
     ser = synth.series(W + D, B, N, seed=17, device=DEV)
     act = synth.actions(D, B, N, seed=18, device=DEV)
     ea = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
-    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+    eb = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
     obs_a = synth.window_from_series(ser, W)
     obs_b = obs_a.clone()
     ea.reset(obs_a)
@@ -299,8 +269,7 @@ def test_gpu_flat_graph_captures_a_reset_before_its_steps(impl):
     assert torch.equal(ra, rb) and torch.equal(obs_a, obs_b)
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_caller_edits_between_steps(impl):
+def test_gpu_flat_caller_edits_between_steps():
     """The features are the caller's (trading_env.py:102-105: the reference keeps no copy
     and honours every edit). At the BASELINE shape the caller, between steps and without a
     reset, rescales the market channels of the in-place window, writes env.value, and hands
@@ -314,8 +283,8 @@ def test_gpu_flat_caller_edits_between_steps(impl):
     B, N, W, T = 65536, 30, 50, 12
     ser = synth.series(W + T, B, N, seed=31, device=DEV)
     act = synth.actions(T, B, N, seed=32, device=DEV)
-    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in (impl, "two_launch")]
-    assert envs[0].step_path.endswith(f"{_kernel(impl)} (in place)")
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
+    assert envs[0].step_path.endswith("step_flat_kernel (in place)")
     obs = [synth.window_from_series(ser, W) for _ in envs]
     for e, o in zip(envs, obs):
         e.reset(o)
@@ -324,7 +293,7 @@ def test_gpu_flat_caller_edits_between_steps(impl):
         for i, e in enumerate(envs):
             if t in (2, 7):                                # edit the window in place (every tile seam)
                 obs[i][..., :4].mul_(1.0009765625)
-            if t == 8:                                     # and its weight channel (split: the snapshot)
+            if t == 8:                                     # and its weight channel
                 obs[i][..., 4].mul_(0.5)
             if t in (3, 9):                                # write the state through .value
                 e.value.mul_(0.75)
@@ -412,8 +381,7 @@ def test_gpu_flat_full_size_properties():
     np.testing.assert_allclose(obs[:S, ..., 4].cpu().numpy(), cobs[..., 4], rtol=2e-7, atol=1e-12)
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_long_run_bitwise_at_baseline_size(impl):
+def test_gpu_flat_long_run_bitwise_at_baseline_size():
     """400 steps at the BASELINE shape (65,536 envs x 30 x 50) on a resident series, the
     flat one-launch step against the two-launch path: in place with a double-buffered
     step every 7th day and masked resets (a fifth of the envs, fresh windows) every 50
@@ -429,7 +397,7 @@ def test_gpu_flat_long_run_bitwise_at_baseline_size(impl):
     m = MarketSeries(bars.astype(np.float32), device=DEV)
     g = torch.Generator().manual_seed(5)
     start = m.random_starts(B, W, T, generator=g)
-    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in (impl, "two_launch")]
+    envs = [TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=i) for i in ("flat", "two_launch")]
     obs = [m.initial_window(start, W) for _ in envs]
     spare = [torch.empty_like(obs[0]) for _ in envs]
     for e, o in zip(envs, obs):
@@ -461,15 +429,14 @@ def test_gpu_flat_long_run_bitwise_at_baseline_size(impl):
     assert envs[0].nonfinite_count() == 0
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_counts_a_nonfinite_env_once(impl):
+def test_gpu_flat_counts_a_nonfinite_env_once():
     """An env whose tiles straddle several workgroups is still counted once when its reward
     turns non-finite (only the owner writes the env's outputs), and its NaN stays in it."""
     from pmenv import TradingEnv, synth
     B, N, W = 37, 30, 50                                    # 1,875 chunks per env: 2-3 tiles each
     ser = synth.series(W + 2, B, N, seed=3, device=DEV)
     obs = synth.window_from_series(ser, W)
-    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+    env = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
     env.reset(obs)
     a = torch.full((B, N), 1.0 / N, device=DEV)
     a[5, 7] = float("nan")
@@ -479,8 +446,7 @@ def test_gpu_flat_counts_a_nonfinite_env_once(impl):
     assert torch.isfinite(obs[torch.arange(B, device=DEV) != 5]).all()
 
 
-@pytest.mark.parametrize("impl", IMPLS)
-def test_gpu_flat_two_handles_on_two_streams(impl):
+def test_gpu_flat_two_handles_on_two_streams():
     """One handle per stream: two envs stepped on two HIP streams with their launches
     interleaved (each handle's snapshot / halo parities are its own) give the bits of
     each env stepped alone."""
@@ -493,7 +459,7 @@ def test_gpu_flat_two_handles_on_two_streams(impl):
         envs, obs, rews = [], [], []
         for k in range(2):
             with torch.cuda.stream(streams[k]):
-                e = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl)
+                e = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="flat")
                 o = synth.window_from_series(ser[k], W)
                 e.reset(o)
                 envs.append(e)

@@ -46,9 +46,6 @@ struct Tools {
     bool flat_db_wg = true;     // PMENV_FLAT_DB_WG=0: the ds_bpermute double-buffered stream
     int k1_groups = 1;          // PMENV_K1_GROUPS: env groups per wave of scalar_step_reg_kernel
     int one_v = kOneV;          // PMENV_ONE_V: step_env_kernel chunks per lane
-    int split_abl = 0;          // PMENV_SPLIT_ABL: step_split_kernel timing-only bits (1 whole stores, 2 no w'
-                                //   window store, 4 no scalar step)
-    int split_r = 0;            // PMENV_SPLIT_R: workgroups per scalar workgroup (1: every scalar one first)
 };
 
 Tools* tools(const pmenv* h) { return static_cast<Tools*>(h->tools); }
@@ -338,8 +335,6 @@ void plan(pmenv* h) {
     const int one_rule = [&] {
         return h->one_ok && (win <= (48ll << 20) || !h->flat_inplace) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }();
-    t->split_abl = knob_int("PMENV_SPLIT_ABL", 0);
-    t->split_r = knob_int("PMENV_SPLIT_R", 0);
     t->one_v = knob_int("PMENV_ONE_V", kOneV);
     if (t->one_v != 1 && t->one_v != 2 && t->one_v != 3 && t->one_v != 6 && t->one_v != 8) t->one_v = kOneV;
     if (t->one_v != kOneV) {
@@ -455,33 +450,6 @@ bool launch_fused(const pmenv* h, const StepParams& p0, int fuse_bit, uint32_t p
     else if (t->fused_vec == 2) { PMENV_FUSED_LAUNCH(2) }
     else { PMENV_FUSED_LAUNCH(4) }
 #undef PMENV_FUSED_LAUNCH
-    return true;
-}
-
-// step_split_kernel with another interleave (R) or the timing-only ablations
-template <int BK, int ABL>
-void split_var(const StepParams& p, uint32_t qtot, uint32_t r_knob, hipStream_t stream) {
-    const uint32_t cpw = (uint32_t)(BK * 2);
-    const uint32_t ntiles = (qtot + cpw - 1) / cpw;
-    const uint32_t nscalar = (uint32_t)((p.B + BK / 64 - 1) / (BK / 64));
-    uint32_t R = r_knob ? r_knob : ((ntiles + nscalar) / nscalar > 2u ? (ntiles + nscalar) / nscalar : 2u);
-    const uint32_t rest = ntiles > nscalar * (R - 1) ? ntiles - nscalar * (R - 1) : 0u;
-    step_split_kernel<BK, 2, 0, ABL><<<nscalar * R + rest, BK, 0, stream>>>(p, qtot, ntiles, nscalar, R);
-}
-
-bool launch_split(const pmenv* h, const StepParams& p, int pol, hipStream_t stream) {
-    const Tools* t = tools(h);
-    if (!t || (!t->split_abl && !t->split_r) || pol != 0 || h->split_block != 256) return false;
-    const uint32_t r = (uint32_t)t->split_r;
-    switch (t->split_abl) {
-        case 0: split_var<256, 0>(p, h->flat_qtot, r, stream); break;
-        case 1: split_var<256, 1>(p, h->flat_qtot, r, stream); break;
-        case 2: split_var<256, 2>(p, h->flat_qtot, r, stream); break;
-        case 3: split_var<256, 3>(p, h->flat_qtot, r, stream); break;
-        case 4: split_var<256, 4>(p, h->flat_qtot, r, stream); break;
-        case 5: split_var<256, 5>(p, h->flat_qtot, r, stream); break;
-        default: return false;
-    }
     return true;
 }
 
