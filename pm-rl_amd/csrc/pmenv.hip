@@ -874,17 +874,17 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
         nparts = (B + kQuadRows - 1) / kQuadRows;
         if (N <= 32)
             batch_reward_rows_quad_kernel<8><<<(unsigned)nparts, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
-                                                                                           reward_kind, work);
+                                                                                           reward_kind, norm, work);
         else
             batch_reward_rows_quad_kernel<16><<<(unsigned)nparts, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N,
-                                                                                            reward_kind, work);
+                                                                                            reward_kind, norm, work);
     } else {                      // wave per row, registers up to N = 512
         nparts = (int)batch_reward_blocks(B);
         const unsigned g = (unsigned)nparts;
-        if (N <= 128) batch_reward_rows_kernel<2><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
-        else if (N <= 256) batch_reward_rows_kernel<4><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
-        else if (N <= 512) batch_reward_rows_kernel<8><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
-        else batch_reward_rows_kernel<0><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, work);
+        if (N <= 128) batch_reward_rows_kernel<2><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, work);
+        else if (N <= 256) batch_reward_rows_kernel<4><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, work);
+        else if (N <= 512) batch_reward_rows_kernel<8><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, work);
+        else batch_reward_rows_kernel<0><<<g, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, work);
     }
     batch_reward_final_kernel<<<1, kTrainBlock, 0, stream>>>(B, reward_kind, norm, scale, work, reward_out, nparts);
     // the chosen per-row return, when asked for (the backward takes each row's choice itself)

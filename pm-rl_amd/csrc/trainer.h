@@ -46,6 +46,63 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
     n = nn;
 }
 
+// The candidate return vectors the norm mode can choose — GLOBAL_OR: raw or softmax (the
+// whole batch decides, in the final fold); ROW_OR: the per-row choice; NONE: raw — and the
+// statistics the reward kind needs of them: Sharpe the count, mean and M2 (pg.py:80), the
+// others the sum of f(ret) (pg.py:76, :78). The partial records carry only those (the other
+// fields 0), and the folds skip the rest: no Chan merge (two f64 divisions per candidate and
+// step) outside Sharpe.
+__device__ __forceinline__ bool cand_used(int norm, int c) {
+    return norm == PMENV_BNORM_GLOBAL_OR ? c != kCandRow : norm == PMENV_BNORM_ROW_OR ? c == kCandRow : c == kCandRaw;
+}
+__device__ __forceinline__ bool field_used(int kind, int norm, int i) {
+    if (i < 3) return true;                                  // sum a, min a, nan
+    if (i >= 15) return false;
+    const int c = (i - 3) >> 2, f = (i - 3) & 3;
+    if (!cand_used(norm, c)) return false;
+    return kind == PMENV_REWARD_SHARPE ? f < 3 : f == 3;
+}
+
+// the candidate fields of one record (count, mean, M2 | sum f) over this wave's rows:
+// `own` lanes hold a row's candidates x[c], cnt rows in all
+__device__ __forceinline__ void cand_record(int kind, int norm, bool own, double cnt, const double (&x)[3],
+                                            double (&rec)[kPartStride]) {
+    const bool sharpe = kind == PMENV_REWARD_SHARPE;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        rec[3 + 4 * c + 0] = 0.0;
+        rec[3 + 4 * c + 1] = 0.0;
+        rec[3 + 4 * c + 2] = 0.0;
+        rec[3 + 4 * c + 3] = 0.0;
+        if (!cand_used(norm, c)) continue;                   // uniform
+        if (sharpe) {
+            const double mean = cnt > 0.0 ? wave_sum(own ? x[c] : 0.0) / cnt : 0.0;
+            const double d = own ? x[c] - mean : 0.0;
+            rec[3 + 4 * c + 0] = cnt;
+            rec[3 + 4 * c + 1] = mean;
+            rec[3 + 4 * c + 2] = wave_sum(d * d);
+        } else {
+            rec[3 + 4 * c + 3] = wave_sum(own ? (kind == PMENV_REWARD_LOG_RETURN ? log(x[c]) : x[c]) : 0.0);
+        }
+    }
+    rec[15] = 0.0;
+}
+
+// fold record q into acc (fields the kind / norm mode use only)
+__device__ __forceinline__ void fold_record(int kind, int norm, double (&acc)[kPartStride], const double* q) {
+    acc[0] += q[0];
+    acc[1] = fmin(acc[1], q[1]);
+    acc[2] += q[2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        if (!cand_used(norm, c)) continue;
+        if (kind == PMENV_REWARD_SHARPE)
+            chan_merge(acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], q[3 + 4 * c], q[4 + 4 * c], q[5 + 4 * c]);
+        else
+            acc[6 + 4 * c] += q[6 + 4 * c];
+    }
+}
+
 // one wave per row (4 rows per wave, 16 per block). EPL > 0 (N <= 64*EPL): the wave
 // loads all four rows' elements into registers up front (lane l holds elements
 // l + 64k: coalesced 256-B rows, every load in flight before the first reduction) and
@@ -56,8 +113,8 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
 // log-return reward).
 template <int EPL>
 __device__ __forceinline__ void rows_wave_partial(const float* a, const float* v_prev, const float* p, int B, int N,
-                                                  int kind, double* work, double (*sh)[kRowsPerBlock], int blk,
-                                                  int nblk) {
+                                                  int kind, int norm, double* work, double (*sh)[kRowsPerBlock],
+                                                  int blk, int nblk) {
     constexpr int RPW = kRowsPerBlock / 4;        // rows per wave
     constexpr int E = EPL > 0 ? EPL : 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -163,18 +220,7 @@ __device__ __forceinline__ void rows_wave_partial(const float* a, const float* v
     rec[0] = s_all;
     rec[1] = mn_all;
     rec[2] = has_nan ? 1.0 : 0.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double mean = wave_sum(ok ? x[c] : 0.0) / cnt;
-        const double d = ok ? x[c] - mean : 0.0;
-        const double m2 = wave_sum(d * d);
-        const double f = wave_sum(ok ? (kind == PMENV_REWARD_LOG_RETURN ? log(x[c]) : x[c]) : 0.0);
-        rec[3 + 4 * c + 0] = cnt;
-        rec[3 + 4 * c + 1] = mean;
-        rec[3 + 4 * c + 2] = m2;
-        rec[3 + 4 * c + 3] = f;
-    }
-    rec[15] = 0.0;
+    cand_record(kind, norm, ok, cnt, x, rec);
     if (lane < kPartStride) {
         double val = rec[0];
 #pragma unroll
@@ -186,9 +232,9 @@ __device__ __forceinline__ void rows_wave_partial(const float* a, const float* v
 template <int EPL>
 __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_kernel(const float* a, const float* v_prev,
                                                                         const float* p, int B, int N, int kind,
-                                                                        double* work) {
+                                                                        int norm, double* work) {
     __shared__ double sh[4][kRowsPerBlock];       // row sum, row min, raw, softmax
-    rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, (int)blockIdx.x, (int)gridDim.x);
+    rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, norm, work, sh, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------- N <= 64: a quad per row
@@ -224,8 +270,8 @@ __device__ __forceinline__ RowQuad<EPL> load_row_quad(const float* a, const floa
 
 template <int EPL>
 __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v_prev, const float* p, int B, int N,
-                                                  int kind, double* work, double (*rec_w)[kPartStride], int blk,
-                                                  int nblk) {
+                                                  int kind, int norm, double* work, double (*rec_w)[kPartStride],
+                                                  int blk, int nblk) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid & 3;
     const int r0 = blk * kQuadRows;
     const int nrows = min(kQuadRows, B - r0);
@@ -283,16 +329,7 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
     rec[0] = wave_sum(own ? s : 0.0);
     rec[1] = wave_min(own && !isnan(mn) ? mn : INFINITY);
     rec[2] = __any(own && isnan(mn)) ? 1.0 : 0.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double mean = cnt > 0.0 ? wave_sum(x[c]) / cnt : 0.0;
-        const double d = own ? x[c] - mean : 0.0;
-        rec[3 + 4 * c + 0] = cnt;
-        rec[3 + 4 * c + 1] = mean;
-        rec[3 + 4 * c + 2] = wave_sum(d * d);
-        rec[3 + 4 * c + 3] = wave_sum(own ? (kind == PMENV_REWARD_LOG_RETURN ? log(x[c]) : x[c]) : 0.0);
-    }
-    rec[15] = 0.0;
+    cand_record(kind, norm, own, cnt, x, rec);
     if (lane < kPartStride) {
         double val = rec[0];
 #pragma unroll
@@ -303,16 +340,7 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
     if (tid != 0) return;
     double acc[kPartStride];
     for (int i = 0; i < kPartStride; ++i) acc[i] = rec_w[0][i];
-    for (int w = 1; w < 4; ++w) {
-        const double* r = rec_w[w];
-        acc[0] += r[0];
-        acc[1] = fmin(acc[1], r[1]);
-        acc[2] += r[2];
-        for (int c = 0; c < 3; ++c) {
-            chan_merge(acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], r[3 + 4 * c], r[4 + 4 * c], r[5 + 4 * c]);
-            acc[6 + 4 * c] += r[6 + 4 * c];
-        }
-    }
+    for (int w = 1; w < 4; ++w) fold_record(kind, norm, acc, rec_w[w]);
     double* part = work + (size_t)6 * B + 8 + blk;        // field-major: coalesced final fold
     for (int i = 0; i < kPartStride; ++i) part[(size_t)i * nblk] = acc[i];
 }
@@ -320,9 +348,9 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
 template <int EPL>
 __global__ __launch_bounds__(kTrainBlock) void batch_reward_rows_quad_kernel(const float* a, const float* v_prev,
                                                                              const float* p, int B, int N, int kind,
-                                                                             double* work) {
+                                                                             int norm, double* work) {
     __shared__ double rec_w[4][kPartStride];
-    rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, (int)blockIdx.x, (int)gridDim.x);
+    rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, norm, work, rec_w, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // backward, N <= 64, a quad per row: dR/da through the (optional) softmax. The
@@ -411,16 +439,7 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
     acc[0] = 0.0; acc[1] = INFINITY; acc[2] = 0.0;
     for (int c = 0; c < 3; ++c) { acc[3 + 4 * c] = 0.0; acc[4 + 4 * c] = 0.0; acc[5 + 4 * c] = 0.0; acc[6 + 4 * c] = 0.0; }
     acc[15] = 0.0;
-    auto fold = [&](const double* q) {
-        acc[0] += q[0];
-        acc[1] = fmin(acc[1], q[1]);
-        acc[2] += q[2];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            chan_merge(acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], q[3 + 4 * c], q[4 + 4 * c], q[5 + 4 * c]);
-            acc[6 + 4 * c] += q[6 + 4 * c];
-        }
-    };
+    auto fold = [&](const double* q) { fold_record(kind, norm, acc, q); };
     // thread t folds partials t, t + 256, ... in order; then a shift-down tree inside
     // each wave (lane i takes lane i + o) and the four wave records in wave order
     // partials are field-major (field i of block k at parts[i * nparts + k]): every
@@ -432,7 +451,8 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
         for (int j = 0; j < 4; ++j) {
             const size_t k = k0 + (size_t)j * kTrainBlock;
 #pragma unroll
-            for (int i = 0; i < kPartStride; ++i) q[j][i] = k < nblk ? parts[(size_t)i * nblk + k] : 0.0;
+            for (int i = 0; i < kPartStride; ++i)
+                q[j][i] = k < nblk && field_used(kind, norm, i) ? parts[(size_t)i * nblk + k] : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -442,7 +462,9 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
         double q[kPartStride];
 #pragma unroll
         for (int i = 0; i < kPartStride; ++i)
-            q[i] = __hiloint2double(__shfl_down(__double2hiint(acc[i]), o, 64), __shfl_down(__double2loint(acc[i]), o, 64));
+            q[i] = field_used(kind, norm, i) ? __hiloint2double(__shfl_down(__double2hiint(acc[i]), o, 64),
+                                                                __shfl_down(__double2loint(acc[i]), o, 64))
+                                             : 0.0;
         if (lane < o) fold(q);
     }
     if (lane == 0)
@@ -459,13 +481,14 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
     const double mean = c == kCandRaw ? acc[4] : c == kCandSoftmax ? acc[8] : acc[12];
     const double m2 = c == kCandRaw ? acc[5] : c == kCandSoftmax ? acc[9] : acc[13];
     const double fsum = c == kCandRaw ? acc[6] : c == kCandSoftmax ? acc[10] : acc[14];
+    const bool sharpe = kind == PMENV_REWARD_SHARPE;
     const double sd = B > 1 ? sqrt(m2 / (B - 1)) : NAN;                  // torch.std: unbiased
     double R;
-    if (kind == PMENV_REWARD_SHARPE) R = mean / sd * scale;               // pg.py:80
+    if (sharpe) R = mean / sd * scale;                                    // pg.py:80
     else R = fsum / B * scale;                                            // pg.py:76, :78
     work[6 * (size_t)B + 0] = glob ? 1.0 : 0.0;
-    work[6 * (size_t)B + 1] = mean;
-    work[6 * (size_t)B + 2] = sd;
+    work[6 * (size_t)B + 1] = sharpe ? mean : 0.0;                        // only the Sharpe backward reads them
+    work[6 * (size_t)B + 2] = sharpe ? sd : 0.0;
     work[6 * (size_t)B + 3] = R;
     work[6 * (size_t)B + 4] = (double)norm;
     *reward_out = (float)R;

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(cons
                                                                             float* reward_out, int nblk) {
     __shared__ double rec_w[4][kPartStride];
     for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, work, rec_w, blk, nblk);
+        rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, norm, work, rec_w, blk, nblk);
         __syncthreads();                                          // rec_w is reused
     }
     if (drew_last_ticket<FENCE>(batch_reward_ticket(work, B)))
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(cons
                                                                             float* reward_out, int nblk) {
     __shared__ double sh[4][kRowsPerBlock];
     for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, work, sh, blk, nblk);
+        rows_wave_partial<EPL>(a, v_prev, p, B, N, kind, norm, work, sh, blk, nblk);
         __syncthreads();
     }
     if (drew_last_ticket<FENCE == 1 ? 0 : FENCE>(batch_reward_ticket(work, B)))   // several writer lanes
