@@ -307,6 +307,29 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // wide_r03wide.err). AUTO gives it in-place windows > 1 GiB at N <= 128 without commission.
     if (h->flat1_ok && c.num_assets > 64 && c.num_assets <= 128 && win > (1ll << 30) && !(c.commission > 0.0))
         h->flat1_auto |= PMENV_FUSE_INPLACE;
+    // In place, 24-100 MiB: a one-launch step beats the two-launch stream there (round 3,
+    // in-process interleaved, profiles/ab_r03/band_r03u.err, band_r03w.err; µs per step,
+    // two launches / one WG per env / flat step): N = 30 at 2,048 envs 27.2 / 24.7 / 25.9,
+    // 3,072 36.3 / 34.7 / 36.3; N = 16 at 4,096 28.8 / 28.1 / 26.8, 6,144 38.1 / 39.8 / 36.9;
+    // N = 8 at 4,096 19.4 / 18.9 / 16.3, 8,192 29.1 / 30.5 / 27.2; N = 32 at 3,072 37.9 /
+    // 38.4 / 36.7; N = 64 at 1,024 28.6 / - / 26.8. From ~115 MiB the two-launch stream
+    // leads (N = 30 at 4,096 44.8 / 45.7 / 47.2, N = 32 / 16 / 8 at 125 MiB, N = 48 at 188).
+    // Which one-launch form: the one-WG-per-env step where its waves' chunk slots hold the
+    // env with >= 90 % occupancy (N = 30: 1,875 of 2,048; it wins by 5-8 % there), else
+    // the flat step (N = 8 / 16 / 32: 65 / 78 / 87 %, the flat step wins by 4-14 %) — the
+    // same rule from 24 MiB, where the flat step also wins at N = 8 and 16 (4,096 x 8:
+    // 16.3 vs 18.9 us; 3,072 x 16: 21.6 vs 22.6).
+    if (win > (24ll << 20) && win <= (100ll << 20)) {
+        const double one_fill = h->one_ok ? (double)h->per4 / (256.0 * h->one_waves) : 0.0;
+        if (h->one_ok && one_fill >= 0.9) {
+            h->one_auto |= PMENV_FUSE_INPLACE;
+        } else if (h->flat1_ok && c.num_assets <= 64) {
+            h->flat1_auto |= PMENV_FUSE_INPLACE;
+            h->one_auto &= ~PMENV_FUSE_INPLACE;
+        } else if (h->one_ok) {
+            h->one_auto |= PMENV_FUSE_INPLACE;
+        }
+    }
 
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {

@@ -264,22 +264,38 @@ def test_gpu_flat_inplace_shapes(N, W, B):
 
 
 def test_gpu_auto_path_rule():
-    """AUTO: windows up to 48 MiB take the one-workgroup-per-env step (launch-latency
-    bound: it wins there at every asset count measured); above, env windows of >= 1,000
-    chunks take the flat one-launch step (step_flat_kernel) — double-buffered from 48 MiB,
-    in place from 256 MiB (in place, cache-resident windows are faster on the two-launch
-    stream), with or without commission — and the rest the two-launch stream; wide envs
-    (64 < N <= 128) take step_flat_vec_kernel in place above 1 GiB. Checked against the
-    oracle just above the 48 MiB threshold (1,700 envs x 30 x 50: 51 MB)."""
+    """AUTO: windows up to 24 MiB take the one-workgroup-per-env step (launch-latency
+    bound); in place from 24 to 100 MiB a one-launch step too — that one where its waves'
+    chunk slots hold the env with >= 90 % occupancy (N = 30), the flat step otherwise —
+    and from 100 to 256 MiB the two-launch stream (cache-resident windows); above, env
+    windows of >= 1,000 chunks take the flat one-launch step (step_flat_kernel) —
+    double-buffered from 48 MiB, in place from 256 MiB, with or without commission — and
+    the rest the two-launch stream; wide envs (64 < N <= 128) take step_flat_vec_kernel in
+    place above 1 GiB. Checked against the oracle at the band's shapes."""
     from pmenv import TradingEnv
-    small = TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV)          # 45 MB
+
+    def parts(e):
+        db, ip = e.step_path.split(" | ")
+        return db, ip
+    small = TradingEnv(num_envs=800, num_assets=8, window=50, device=DEV)            # 6 MB
     assert small.step_path.count("step_env_kernel") == 2
-    big = TradingEnv(num_envs=1700, num_assets=30, window=50, device=DEV)            # 51 MB
-    db, ip = big.step_path.split(" | ")
+    db, ip = parts(TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV))   # 45 MB
+    assert db.startswith("step_env_kernel") and ip.startswith("step_env_kernel")
+    db, ip = parts(TradingEnv(num_envs=1700, num_assets=30, window=50, device=DEV))   # 51 MB
+    assert db.startswith("step_flat_kernel") and ip.startswith("step_env_kernel")
+    db, ip = parts(TradingEnv(num_envs=3000, num_assets=30, window=50, device=DEV))   # 90 MB
+    assert db.startswith("step_flat_kernel") and ip.startswith("step_env_kernel")
+    db, ip = parts(TradingEnv(num_envs=4096, num_assets=30, window=50, device=DEV))   # 123 MB: config 2
     assert db.startswith("step_flat_kernel") and "advance_flat_inplace_kernel" in ip
+    db, ip = parts(TradingEnv(num_envs=4096, num_assets=16, window=50, device=DEV))   # 66 MB, 78 % fill
+    assert ip.startswith("step_flat_kernel")
+    db, ip = parts(TradingEnv(num_envs=4096, num_assets=8, window=50, device=DEV))    # 33 MB, 65 % fill
+    assert ip.startswith("step_flat_kernel") and db.startswith("step_env_kernel")
     huge = TradingEnv(num_envs=9000, num_assets=30, window=50, device=DEV)           # 270 MB
     assert huge.step_path.count("step_flat_kernel") == 2
-    thin = TradingEnv(num_envs=9000, num_assets=8, window=50, device=DEV)            # 500 chunks per env
+    db, ip = parts(TradingEnv(num_envs=9000, num_assets=8, window=50, device=DEV))    # 72 MB, 500 chunks per env
+    assert "step_flat_kernel" not in db and "step_env_kernel" not in db and ip.startswith("step_flat_kernel")
+    thin = TradingEnv(num_envs=18000, num_assets=8, window=50, device=DEV)           # 144 MB
     assert "step_flat_kernel" not in thin.step_path and "step_env_kernel" not in thin.step_path
     wide = TradingEnv(num_envs=2000, num_assets=65, window=50, device=DEV)           # N > 64
     assert "step_flat_kernel" not in wide.step_path
@@ -294,6 +310,8 @@ def test_gpu_auto_path_rule():
     assert "step_flat" not in wide_500.step_path
     _run_both({}, B=1700, N=30, W=50, T=9, kind="mixed", seed=31)
     _run_both({"ring": "chrono"}, B=1700, N=30, W=50, T=5, kind="simplex", seed=32, double_buffer=True)
+    _run_both({}, B=4096, N=8, W=50, T=53, kind="mixed", seed=34)
+    _run_both({"ring": "chrono", "commission": 0.0025}, B=4096, N=16, W=50, T=6, kind="rawpos", seed=35)
     _run_both({}, B=9000, N=30, W=50, T=7, kind="mixed", seed=33)
 
 
