@@ -557,11 +557,52 @@ __device__ __forceinline__ float scalar_finish(const StepParams& p, int b, int l
     return m.wp;
 }
 
+// The in-place flat advance's halo (copy_halo in env_step.h) in two halves: the
+// loads go out with the step's own loads, the stores after its compute, so the copy
+// costs the wave no extra memory round trip. Items past two per thread (grids
+// smaller than half the halo) take the plain loop at the end.
+struct HaloRegs {
+    f4 v[4];
+    bool d0, d1;
+};
+
+__device__ __forceinline__ HaloRegs halo_load(const StepParams& p) {
+    HaloRegs h;
+    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
+    h.d0 = p.halo && gid < p.halo_wgs;
+    h.d1 = p.halo && gid + nthr < p.halo_wgs;
+    const f4* src = reinterpret_cast<const f4*>(p.obs);
+    const f4 z = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const bool d = t ? h.d1 : h.d0;
+        const uint32_t q = (gid + t * nthr + 1) * p.halo_block;
+        h.v[2 * t] = d && q < p.halo_qtot ? src[q] : z;
+        h.v[2 * t + 1] = d && q + 1 < p.halo_qtot ? src[q + 1] : z;
+    }
+    return h;
+}
+
+__device__ __forceinline__ void halo_store(const StepParams& p, const HaloRegs& h) {
+    if (!p.halo) return;
+    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
+    f4* dst = reinterpret_cast<f4*>(p.halo);
+    if (h.d0) { dst[2 * gid] = h.v[0]; dst[2 * gid + 1] = h.v[1]; }
+    if (h.d1) { dst[2 * (gid + nthr)] = h.v[2]; dst[2 * (gid + nthr) + 1] = h.v[3]; }
+    const f4* src = reinterpret_cast<const f4*>(p.obs);
+    for (uint32_t i = gid + 2 * nthr; i < p.halo_wgs; i += nthr) {
+        const uint32_t q = (i + 1) * p.halo_block;
+        dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
+        dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
 // P env groups per wave in sequence, all their loads issued first: P times the
-// bytes in flight per wave for a latency-bound kernel
+// bytes in flight per wave for a latency-bound kernel; the in-place stream's halo copy
+// loads with them and stores at the end (HaloRegs)
 template <int L, int P>
 __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
-    copy_halo(p);
+    const HaloRegs halo = halo_load(p);
     constexpr int EPW = 64 / L;                   // envs per wave and group
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
@@ -573,6 +614,7 @@ __global__ __launch_bounds__(256) void scalar_step_reg_kernel(StepParams p) {
         int32_t k;
         (void)scalar_finish<L>(p, (w * P + j) * EPW + lane / L, lane, in[j], k);
     }
+    halo_store(p, halo);
 }
 
 // ---------------------------------------------------------------- K2: window advance

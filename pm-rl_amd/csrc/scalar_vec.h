@@ -62,45 +62,6 @@ __device__ __forceinline__ void load_packed(const float* base, uint32_t bytes, s
     }
 }
 
-// The in-place flat advance's halo (copy_halo in env_step.h) in two halves: the
-// loads go out with the step's own loads, the stores after its compute, so the copy
-// costs the wave no extra memory round trip. Items past two per thread (grids
-// smaller than half the halo) take the plain loop at the end.
-struct HaloRegs {
-    f4 v[4];
-    bool d0, d1;
-};
-
-__device__ __forceinline__ HaloRegs halo_load(const StepParams& p) {
-    HaloRegs h;
-    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
-    h.d0 = p.halo && gid < p.halo_wgs;
-    h.d1 = p.halo && gid + nthr < p.halo_wgs;
-    const f4* src = reinterpret_cast<const f4*>(p.obs);
-    const f4 z = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const bool d = t ? h.d1 : h.d0;
-        const uint32_t q = (gid + t * nthr + 1) * p.halo_block;
-        h.v[2 * t] = d && q < p.halo_qtot ? src[q] : z;
-        h.v[2 * t + 1] = d && q + 1 < p.halo_qtot ? src[q + 1] : z;
-    }
-    return h;
-}
-
-__device__ __forceinline__ void halo_store(const StepParams& p, const HaloRegs& h) {
-    if (!p.halo) return;
-    const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
-    f4* dst = reinterpret_cast<f4*>(p.halo);
-    if (h.d0) { dst[2 * gid] = h.v[0]; dst[2 * gid + 1] = h.v[1]; }
-    if (h.d1) { dst[2 * (gid + nthr)] = h.v[2]; dst[2 * (gid + nthr) + 1] = h.v[3]; }
-    const f4* src = reinterpret_cast<const f4*>(p.obs);
-    for (uint32_t i = gid + 2 * nthr; i < p.halo_wgs; i += nthr) {
-        const uint32_t q = (i + 1) * p.halo_block;
-        dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
-        dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
-    }
-}
 
 // The packed scalar step in three parts, so the one-launch walk step (step_walk.h) can
 // put its window loads between the loads and the compute and run the state writes

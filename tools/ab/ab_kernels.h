@@ -2,6 +2,7 @@
 // alternatives the product measured against and replaced. Moved out of
 // pm-rl_amd/csrc/replay.h and trainer.h, whose device helpers they use.
 #pragma once
+#include "../../pm-rl_amd/csrc/env_step.h"
 #include "../../pm-rl_amd/csrc/replay.h"
 #include "../../pm-rl_amd/csrc/trainer.h"
 
@@ -141,6 +142,66 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(cons
     }
     if (drew_last_ticket<FENCE == 1 ? 0 : FENCE>(batch_reward_ticket(work, B)))   // several writer lanes
         final_fold(B, kind, norm, scale, work, reward_out, nblk);
+}
+
+
+// The in-place flat stream without the LDS image (PMENV_FLAT_DIRECT): each lane loads its
+// own chunk and its shifted source (floats 4j+5 .. 4j+8) straight from memory with a
+// dword-aligned 16-B load; the workgroup's last two chunks take theirs from the next chunk
+// and the halo. One barrier (every load of the workgroup before any store), then compose
+// and store. ABL: flat_side_load's SKIP bits (timing only).
+template <int BLOCK, int V, int POL, int ABL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_direct_kernel(StepParams p, uint32_t qtot) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = blockIdx.x * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? min(2u, qtot - c0 - nblk) : 0u;
+    const auto rh = make_rsrc(p.halo + (size_t)blockIdx.x * 8, nh * 16u);
+    f4 own[V], shf[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t j = (uint32_t)(64 * V * wave + 64 * v + lane);
+        own[v] = buf_load4<kAux>(rs, j * 16u);
+        // floats 4j+5 .. 4j+8 lie inside the workgroup's range for j + 3 <= nblk
+        shf[v] = buf_load4<kAux>(rs, j + 3u <= nblk ? j * 16u + 20u : 0xFFFFFFF0u);
+    }
+    // the last two chunks' sources: chunk j+1 (in range) or the halo
+    const uint32_t je = nblk >= 2 ? nblk - 2u : 0u;
+    const bool edge = tid < 2 && nblk >= 2;
+    f4 ea = f4{0.f, 0.f, 0.f, 0.f}, eb = f4{0.f, 0.f, 0.f, 0.f};
+    if (edge) {
+        const uint32_t j = je + (uint32_t)tid;                        // nblk - 2, nblk - 1
+        ea = j + 1u < nblk ? buf_load4<0>(rs, (j + 1u) * 16u) : buf_load4<0>(rh, 0u);
+        eb = j + 1u < nblk ? buf_load4<0>(rh, 0u) : buf_load4<0>(rh, 16u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t qw = __builtin_amdgcn_readfirstlane(c0 + (uint32_t)(64 * V * wave));
+    WaveSide ws;
+    ws.ok = false;
+    ws = wave_side_load(p, qw, 64u * V, qtot);
+    FlatSide sd[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) sd[v] = flat_side_from_wave<ABL & 15>(p, ws, min(qw + 64u * v + lane, qtot - 1u));
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    __shared__ f4 sh_edge[2][2];
+    if (edge) { sh_edge[tid][0] = ea; sh_edge[tid][1] = eb; }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t j = (uint32_t)(64 * V * wave + 64 * v + lane);
+        float sh[4] = {shf[v].x, shf[v].y, shf[v].z, shf[v].w};
+        if (j + 3u > nblk && j < nblk) {
+            const int k = (int)(j - je);
+            const f4 a = sh_edge[k][0], b = sh_edge[k][1];
+            sh[0] = a.y; sh[1] = a.z; sh[2] = a.w; sh[3] = b.x;
+        }
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        buf_store4<kAux>(rs, j * 16u, flat_compose(p, sd[v], un, sh));
+    }
 }
 
 }  // namespace pmenv_dev

@@ -110,6 +110,11 @@ bool flat_inplace(const pmenv* h, const Tools* t, StepParams p, hipStream_t stre
     const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
     const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
     const int pol = h->flat_ip_pol;
+    if (t->ablate == 64 + 15 && key == 2562) {    // the product's cache-resident geometry, side data skipped
+        advance_flat_inplace_kernel<256, 2, 0, 15><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        return true;
+    }
+    if (t->ablate >= 64 && t->ablate < 128 && cpw != 512) return false;   // its 512 x 1 tiles need the 512-chunk halo
     if (t->ablate >= 64 && t->ablate < 128) {     // PMENV_ABLATE = 64 + SKIP bits
         const unsigned g1 = (unsigned)((h->flat_qtot + 511) / 512);
 #define PMENV_ABL(X) case 64 + X: advance_flat_inplace_kernel<512, 1, 1, X><<<g1, 512, 0, stream>>>(p, h->flat_qtot); break;
@@ -408,6 +413,24 @@ bool launch_advance(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const Tools* t = tools(h);
     if (!t) return false;
     const bool db = p.obs_out != p.obs;
+    if (!db && h->flat_inplace && knob("PMENV_FLAT_DIRECT")) {      // the stream without the LDS image
+        StepParams q = p;
+        const pmenv_cfg& c = h->cfg;
+        q.div_units = make_fastdiv((uint32_t)((int64_t)c.num_assets * c.window * c.features / 4));
+        q.halo = h->halo;
+        const int cpw = h->flat_ip_block * h->flat_ip_vec;
+        const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
+        const int abl = knob_int("PMENV_FLAT_DIRECT_ABL", 0);
+        if (h->flat_ip_block == 256) {
+            if (abl == 15) advance_flat_direct_kernel<256, 2, 0, 15><<<grid, 256, 0, stream>>>(q, h->flat_qtot);
+            else advance_flat_direct_kernel<256, 2, 0, 0><<<grid, 256, 0, stream>>>(q, h->flat_qtot);
+        } else if (h->flat_ip_pol == 1) {
+            advance_flat_direct_kernel<512, 2, 1, 0><<<grid, 512, 0, stream>>>(q, h->flat_qtot);
+        } else {
+            advance_flat_direct_kernel<512, 2, 0, 0><<<grid, 512, 0, stream>>>(q, h->flat_qtot);
+        }
+        return true;
+    }
     if (db && h->flat && !t->ablate) return flat_db(h, t, p, stream);
     if (!db && h->flat_inplace && (!t->ablate || (t->ablate >= 64 && t->ablate < 128)))
         return flat_inplace(h, t, p, stream);
