@@ -110,8 +110,13 @@ bool flat_inplace(const pmenv* h, const Tools* t, StepParams p, hipStream_t stre
     const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
     const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
     const int pol = h->flat_ip_pol;
-    if (t->ablate == 64 + 15 && key == 2562) {    // the product's cache-resident geometry, side data skipped
-        advance_flat_inplace_kernel<256, 2, 0, 15><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+    if (key == 2562 && t->ablate > 64 && t->ablate < 80) {   // the product's cache-resident geometry, side data skipped
+        switch (t->ablate - 64) {
+            case 1: advance_flat_inplace_kernel<256, 2, 0, 1><<<grid, 256, 0, stream>>>(p, h->flat_qtot); break;
+            case 2: advance_flat_inplace_kernel<256, 2, 0, 2><<<grid, 256, 0, stream>>>(p, h->flat_qtot); break;
+            case 4: advance_flat_inplace_kernel<256, 2, 0, 4><<<grid, 256, 0, stream>>>(p, h->flat_qtot); break;
+            default: advance_flat_inplace_kernel<256, 2, 0, 15><<<grid, 256, 0, stream>>>(p, h->flat_qtot); break;
+        }
         return true;
     }
     if (t->ablate >= 64 && t->ablate < 128 && cpw != 512) return false;   // its 512 x 1 tiles need the 512-chunk halo
@@ -400,7 +405,11 @@ bool launch_scalar(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const bool groups = t->k1_groups != 1 && h->cfg.num_assets <= 64 && h->k1_vec == 0;
     if (!t->ablate && !ab_vec && !groups) return false;
     StepParams q = p;
-    if (t->ablate) q.halo = nullptr;              // the ablations of the stream skip its halo too
+    // the ablations of the stream skip its halo copy too, except the side-data-only ones
+    // at the product's cache-resident geometry (PMENV_ABLATE = 64 + 1 / 2 / 4 / 15, 256 x 2)
+    const bool side_only = t->ablate > 64 && t->ablate < 80 && h->flat_ip_block * h->flat_ip_vec == 512 &&
+                           h->flat_ip_block == 256;
+    if (t->ablate && !side_only) q.halo = nullptr;
     if (ab_vec) scalar_vec_ab(h->k1_vec, q, stream);
     else if (groups) {
         if (h->cfg.num_assets <= 32) scalar_reg_groups<32>(t->k1_groups, q, stream);
