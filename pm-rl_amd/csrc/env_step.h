@@ -958,6 +958,27 @@ __device__ __forceinline__ FlatSide flat_side_from_wave(const StepParams& p, con
     return sd;
 }
 
+// flat_side_from_wave without the bar row and w' (bar-batch mode, the wave's rows in one
+// 4-row window): `ri` = the chunk's row in that window (0 .. 3), for a stream that reads
+// the row's bar and w' from LDS after its barrier (flat_wg_body<..., LSIDE>, tools A/B)
+__device__ __forceinline__ FlatSide flat_side_rows(const StepParams& p, const WaveSide& ws, uint32_t q, int& ri) {
+    constexpr int F = 5;
+    const int N = p.N, WF = p.W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    FlatSide sd;
+    const uint32_t b = fdiv(q, p.div_units);
+    const uint32_t j0 = 4u * (q - b * per4);
+    const uint32_t row = fdiv(j0, p.div_wf);
+    sd.kk = (int)(j0 - row * (uint32_t)WF);
+    ri = (int)(b * (uint32_t)N + row - ws.g0);
+    sd.bar_nan = false;
+    sd.xb = f4{0.f, 0.f, 0.f, 0.f};
+    sd.xwp = 0.f;
+    const int mk = -(int)(b != ws.b0);
+    sd.k = ((ws.k2[1] & mk) | (ws.k2[0] & ~mk)) - 1;   // scalar_step_kernel counted this step
+    return sd;
+}
+
 // the output chunk from the unshifted input un (chunk q) and the shifted source sh
 // (floats 4q+5 .. 4q+8), per element at row position pos = kk + e (pos >= WF: the
 // chunk has wrapped into the next row, whose positions 0..2 are never a last day or
@@ -1044,11 +1065,13 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint3
 // the wave's side data is one scalar window.
 // ABL (timing-only ablation, PMENV_ABLATE = 64 + ABL with the flat path; 0 in the
 // product): flat_side_load's SKIP bits (1 bar, 2 w', 4 counter, 8 day), 16 = no halo,
-// 32 = per-lane side loads instead of the wave's scalar loads
+// 32 = per-lane side loads instead of the wave's scalar loads, 128 = no compose (the
+// shifted chunk stored as it is: PMENV_STREAM_BARE)
 // OUT = true: the same workgroup body double-buffered (obs -> obs_out); the two
 // chunks past the workgroup are then read straight from obs (no halo copy).
-template <int BLOCK, int V, int POL, bool OUT, int ABL>
+template <int BLOCK, int V, int POL, bool OUT, int ABL, bool LSIDE = false>
 __device__ __forceinline__ void flat_wg_body(StepParams& p, uint32_t qtot, f4* sh4) {
+    __shared__ f4 sh_side[LSIDE ? BLOCK / 64 : 1][5];   // LSIDE: per wave its 4 bar rows, then their w'
     constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
     constexpr int CPW = BLOCK * V;                  // chunks per workgroup
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1070,9 +1093,23 @@ __device__ __forceinline__ void flat_wg_body(StepParams& p, uint32_t qtot, f4* s
     WaveSide ws;
     ws.ok = false;
     if (!(ABL & 32)) ws = wave_side_load(p, qw, 64u * V, qtot);
-    FlatSide sd[V];
+    const bool lside = LSIDE && ABL == 0 && ws.ok && !p.day;
+    if (lside && lane == 0) {
 #pragma unroll
-    for (int v = 0; v < V; ++v) sd[v] = flat_side_from_wave<ABL & 15>(p, ws, min(qw + 64u * v + lane, qtot - 1u));
+        for (int r = 0; r < 4; ++r)
+            sh_side[wave][r] = f4{__int_as_float(ws.bar16[4 * r]), __int_as_float(ws.bar16[4 * r + 1]),
+                                  __int_as_float(ws.bar16[4 * r + 2]), __int_as_float(ws.bar16[4 * r + 3])};
+        sh_side[wave][4] = f4{__int_as_float(ws.w4[0]), __int_as_float(ws.w4[1]), __int_as_float(ws.w4[2]),
+                              __int_as_float(ws.w4[3])};
+    }
+    FlatSide sd[V];
+    int ri[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t q = min(qw + 64u * v + lane, qtot - 1u);
+        if (lside) sd[v] = flat_side_rows(p, ws, q, ri[v]);
+        else sd[v] = flat_side_from_wave<ABL & 15>(p, ws, q);
+    }
 #pragma unroll
     for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
     if (tid < 2) sh4[CPW + tid] = hal;
@@ -1081,10 +1118,15 @@ __device__ __forceinline__ void flat_wg_body(StepParams& p, uint32_t qtot, f4* s
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int j = 64 * V * wave + 64 * v + lane;
+        if (lside) {
+            sd[v].xb = sh_side[wave][ri[v]];
+            sd[v].xwp = reinterpret_cast<const float*>(&sh_side[wave][4])[ri[v]];
+        }
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, flat_compose(p, sd[v], un, sh));
+        if (ABL & 128) buf_store4<kAux>(rd, (uint32_t)j * 16u, f4{sh[0], sh[1], sh[2], sh[3]});   // timing only
+        else buf_store4<kAux>(rd, (uint32_t)j * 16u, flat_compose(p, sd[v], un, sh));
     }
 }
 
@@ -1092,6 +1134,13 @@ template <int BLOCK, int V, int POL, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams p, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
     flat_wg_body<BLOCK, V, POL, false, ABL>(p, qtot, sh4);
+}
+
+// tools A/B: the stream reading each chunk's bar and w' from LDS rows staged per wave
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_inplace_lside_kernel(StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, false, 0, true>(p, qtot, sh4);
 }
 
 // the same kernel held to 80 SGPRs (8 waves per SIMD instead of 7; tools A/B)

@@ -46,6 +46,11 @@ struct Tools {
     bool flat_db_wg = true;     // PMENV_FLAT_DB_WG=0: the ds_bpermute double-buffered stream
     int k1_groups = 1;          // PMENV_K1_GROUPS: env groups per wave of scalar_step_reg_kernel
     int one_v = kOneV;          // PMENV_ONE_V: step_env_kernel chunks per lane
+    // in-place stream variants, read at create like every knob here (ab_libs.py sets them
+    // only while it creates the handle): PMENV_FLAT_DIRECT (+ _ABL SKIP bits), PMENV_STREAM_BARE
+    // (1: no compose, no side data; 2: no compose), PMENV_FLAT_LSIDE (bar rows / w' via LDS)
+    int flat_direct = 0, flat_direct_abl = 0, stream_bare = 0;
+    bool flat_lside = false;
 };
 
 Tools* tools(const pmenv* h) { return static_cast<Tools*>(h->tools); }
@@ -110,6 +115,15 @@ bool flat_inplace(const pmenv* h, const Tools* t, StepParams p, hipStream_t stre
     const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
     const int key = h->flat_ip_block * 10 + h->flat_ip_vec;
     const int pol = h->flat_ip_pol;
+    if (key == 2562 && t->stream_bare) {                      // timing only: no compose (and no side data)
+        if (t->stream_bare == 2) advance_flat_inplace_kernel<256, 2, 0, 128><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        else advance_flat_inplace_kernel<256, 2, 0, 128 + 15><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        return true;
+    }
+    if (key == 2562 && t->flat_lside) {                       // bar rows and w' staged in LDS per wave
+        advance_flat_inplace_lside_kernel<256, 2, 0><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        return true;
+    }
     if (key == 2562 && t->ablate > 64 && t->ablate < 80) {   // the product's cache-resident geometry, side data skipped
         switch (t->ablate - 64) {
             case 1: advance_flat_inplace_kernel<256, 2, 0, 1><<<grid, 256, 0, stream>>>(p, h->flat_qtot); break;
@@ -345,6 +359,10 @@ void plan(pmenv* h) {
     const int one_rule = [&] {
         return h->one_ok && (win <= (48ll << 20) || !h->flat_inplace) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }();
+    t->flat_direct = knob_int("PMENV_FLAT_DIRECT", 0);
+    t->flat_direct_abl = knob_int("PMENV_FLAT_DIRECT_ABL", 0);
+    t->stream_bare = knob_int("PMENV_STREAM_BARE", 0);
+    t->flat_lside = knob_int("PMENV_FLAT_LSIDE", 0) != 0;
     t->one_v = knob_int("PMENV_ONE_V", kOneV);
     if (t->one_v != 1 && t->one_v != 2 && t->one_v != 3 && t->one_v != 6 && t->one_v != 8) t->one_v = kOneV;
     if (t->one_v != kOneV) {
@@ -422,14 +440,14 @@ bool launch_advance(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const Tools* t = tools(h);
     if (!t) return false;
     const bool db = p.obs_out != p.obs;
-    if (!db && h->flat_inplace && knob("PMENV_FLAT_DIRECT")) {      // the stream without the LDS image
+    if (!db && h->flat_inplace && t->flat_direct) {                 // the stream without the LDS image
         StepParams q = p;
         const pmenv_cfg& c = h->cfg;
         q.div_units = make_fastdiv((uint32_t)((int64_t)c.num_assets * c.window * c.features / 4));
         q.halo = h->halo;
         const int cpw = h->flat_ip_block * h->flat_ip_vec;
         const unsigned grid = (unsigned)((h->flat_qtot + cpw - 1) / cpw);
-        const int abl = knob_int("PMENV_FLAT_DIRECT_ABL", 0);
+        const int abl = t->flat_direct_abl;
         if (h->flat_ip_block == 256) {
             if (abl == 15) advance_flat_direct_kernel<256, 2, 0, 15><<<grid, 256, 0, stream>>>(q, h->flat_qtot);
             else advance_flat_direct_kernel<256, 2, 0, 0><<<grid, 256, 0, stream>>>(q, h->flat_qtot);
