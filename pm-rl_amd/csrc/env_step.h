@@ -1130,10 +1130,121 @@ __device__ __forceinline__ void flat_wg_body(StepParams& p, uint32_t qtot, f4* s
     }
 }
 
+// The same workgroup body with a two-level compose. Every chunk takes the common form —
+// its shifted source, or (storage order, ring full) its own weight dwords — and only the
+// chunks holding a row's last day or its ring slot patch those elements from the row's bar
+// and w' (a divergent branch a few lanes per wave instruction take). The workgroup's rows'
+// bar, w' and counter come into LDS before the barrier, one row per thread (per-lane
+// loads: no scalar window, no per-chunk selects). The same values as flat_compose, element
+// by element: the common form is flat_compose's result wherever neither a last day nor the
+// slot is involved, and the patch applies flat_compose's rule to exactly those elements.
+// Needs at most BLOCK rows per workgroup: 4 V <= W F (W >= 2 at V = 2: the flat stream's
+// shape rule, pmenv.hip).
+template <int BLOCK, int V, int POL, bool OUT>
+__device__ __forceinline__ void flat_wg_body_patch(StepParams& p, uint32_t qtot, f4* sh4) {
+    constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
+    constexpr int CPW = BLOCK * V, F = 5;
+    __shared__ f4 sh_bar[BLOCK];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = blockIdx.x * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    f4 own[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : p.halo + (size_t)blockIdx.x * 8;
+    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    __builtin_amdgcn_sched_barrier(0);
+    // the workgroup's rows g_lo .. g_hi (global row = b N + n): thread t stages row g_lo + t
+    const int N = p.N, W = p.W, WF = W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    const uint32_t b_lo = fdiv(c0, p.div_units);
+    const uint32_t g_lo = b_lo * (uint32_t)N + fdiv(4u * (c0 - b_lo * per4), p.div_wf);
+    const uint32_t ql = c0 + nblk - 1u;
+    const uint32_t b_hi = fdiv(ql, p.div_units);
+    const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
+    if ((uint32_t)tid <= g_hi - g_lo) {
+        const uint32_t g = g_lo + (uint32_t)tid;
+        const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
+        const float* barb = env_bar(p, (int)b);                     // null: a day outside the series
+        const float nanv = __int_as_float(0x7fc00000);
+        sh_bar[tid] = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
+        sh_wp[tid] = p.w_new[g];
+        sh_kc[tid] = p.k[b] - 1;                                     // scalar_step_kernel counted this step
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
+    __syncthreads();
+    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
+    const bool storage = p.ring_mode == PMENV_RING_STORAGE;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
+        const uint32_t b = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - b * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const int kk = (int)(j0 - row * (uint32_t)WF);
+        const int t = (int)(b * (uint32_t)N + row - g_lo);
+        const int32_t k = sh_kc[t];
+        const bool shift_w = !(storage && k >= W - 1);
+        const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+            o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
+        }
+        const int slot_w =
+            (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
+        if (kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u)) {   // a last day or the slot
+            const f4 xb = sh_bar[t];
+            const float xwp = sh_wp[t];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int pos = kk + e;
+                const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+                const bool in_row = pos < WF;
+                const bool lastday = in_row && pos >= WF - F;
+                const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
+                o[e] = pick(lastday && f < F - 1, bsel, o[e]);
+                o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
+            }
+        }
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, f4{o[0], o[1], o[2], o[3]});
+    }
+}
+
+// The in-place flat stream: the two-level compose in the product (ABL = 0); the tools
+// build's timing-only ablations run the per-element compose with their SKIP bits.
+// Round 3, in-process interleaved against the per-element compose, the same bits:
+// 8,192 x 30 81.5 vs 82.8 us, 65,536 x 30 637.0 vs 646.5, double-buffered 84.6 vs 87.1 and
+// 641.8 vs 648.5; 4,096 x 30, 8,192 x 16, 16,384 x 8, 4,096 x 48 within 0.3 %
+// (profiles/ab_r03/patch_r03p.err)
 template <int BLOCK, int V, int POL, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) void advance_flat_inplace_kernel(StepParams p, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
-    flat_wg_body<BLOCK, V, POL, false, ABL>(p, qtot, sh4);
+    if constexpr (ABL == 0) flat_wg_body_patch<BLOCK, V, POL, false>(p, qtot, sh4);
+    else flat_wg_body<BLOCK, V, POL, false, ABL>(p, qtot, sh4);
+}
+
+// tools A/B: the in-place / double-buffered stream with the per-element compose
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_inplace_perelem_kernel(StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, false, 0>(p, qtot, sh4);
+}
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) void advance_flat_wg_perelem_kernel(StepParams p, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    flat_wg_body<BLOCK, V, POL, true, 0>(p, qtot, sh4);
 }
 
 // tools A/B: the stream reading each chunk's bar and w' from LDS rows staged per wave
@@ -1155,7 +1266,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void ad
 template <int BLOCK, int V, int POL>
 __global__ __launch_bounds__(BLOCK) void advance_flat_wg_kernel(StepParams p, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
-    flat_wg_body<BLOCK, V, POL, true, 0>(p, qtot, sh4);
+    flat_wg_body_patch<BLOCK, V, POL, true>(p, qtot, sh4);
 }
 
 // Taken by the scalar step kernels before the in-place flat advance of the same step:

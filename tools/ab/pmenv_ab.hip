@@ -51,6 +51,7 @@ struct Tools {
     // (1: no compose, no side data; 2: no compose), PMENV_FLAT_LSIDE (bar rows / w' via LDS)
     int flat_direct = 0, flat_direct_abl = 0, stream_bare = 0;
     bool flat_lside = false;
+    bool flat_perelem = false;  // PMENV_FLAT_PERELEM: the stream's per-element compose (flat_wg_body)
 };
 
 Tools* tools(const pmenv* h) { return static_cast<Tools*>(h->tools); }
@@ -85,6 +86,12 @@ bool flat_db(const pmenv* h, const Tools* t, StepParams p, hipStream_t stream) {
     const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
     const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
     p.div_units = make_fastdiv(per4);
+    if (t->flat_perelem) {                        // the per-element compose, the product's 512 x 2 geometry
+        const unsigned gp = (unsigned)((qtot + 1023) / 1024);
+        if (h->flat_pol == 1) advance_flat_wg_perelem_kernel<512, 2, 1><<<gp, 512, 0, stream>>>(p, qtot);
+        else advance_flat_wg_perelem_kernel<512, 2, 0><<<gp, 512, 0, stream>>>(p, qtot);
+        return true;
+    }
     if (!t->flat_db_wg) {
         const int bk = t->flat_block;
         const unsigned grid = (unsigned)((qtot + bk - 1) / bk);
@@ -118,6 +125,12 @@ bool flat_inplace(const pmenv* h, const Tools* t, StepParams p, hipStream_t stre
     if (key == 2562 && t->stream_bare) {                      // timing only: no compose (and no side data)
         if (t->stream_bare == 2) advance_flat_inplace_kernel<256, 2, 0, 128><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
         else advance_flat_inplace_kernel<256, 2, 0, 128 + 15><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        return true;
+    }
+    if (t->flat_perelem && (key == 2562 || key == 5122)) {     // the per-element compose (before round 3)
+        if (key == 2562) advance_flat_inplace_perelem_kernel<256, 2, 0><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        else if (pol == 1) advance_flat_inplace_perelem_kernel<512, 2, 1><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
+        else advance_flat_inplace_perelem_kernel<512, 2, 0><<<grid, 512, 0, stream>>>(p, h->flat_qtot);
         return true;
     }
     if (key == 2562 && t->flat_lside) {                       // bar rows and w' staged in LDS per wave
@@ -363,6 +376,7 @@ void plan(pmenv* h) {
     t->flat_direct_abl = knob_int("PMENV_FLAT_DIRECT_ABL", 0);
     t->stream_bare = knob_int("PMENV_STREAM_BARE", 0);
     t->flat_lside = knob_int("PMENV_FLAT_LSIDE", 0) != 0;
+    t->flat_perelem = knob_int("PMENV_FLAT_PERELEM", 0) != 0;
     t->one_v = knob_int("PMENV_ONE_V", kOneV);
     if (t->one_v != 1 && t->one_v != 2 && t->one_v != 3 && t->one_v != 6 && t->one_v != 8) t->one_v = kOneV;
     if (t->one_v != kOneV) {
