@@ -1009,6 +1009,43 @@ __device__ __forceinline__ f4 flat_compose(const StepParams& p, const FlatSide& 
     return f4{v[0], v[1], v[2], v[3]};
 }
 
+// flat_compose in two levels, the same values element by element: every chunk takes the
+// common form — the shifted source, or (storage order, ring full) its own weight dwords —
+// and only a chunk holding a row's last day or its ring slot (a divergent branch: a few
+// lanes per wave instruction) fetches the row's bar and w' (`side(xb, xwp)`, NaN bar for a
+// day outside the series) and patches those elements. k: the counter before the step.
+template <typename Side>
+__device__ __forceinline__ f4 compose2(const StepParams& p, int kk, int32_t k, const float (&un)[4],
+                                       const float (&sh)[4], Side side) {
+    constexpr int F = 5;
+    const int W = p.W, WF = W * F;
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
+    const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+        o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
+    }
+    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
+    if (kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u)) {   // a last day or the slot
+        f4 xb;
+        float xwp;
+        side(xb, xwp);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int pos = kk + e;
+            const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+            const bool in_row = pos < WF;
+            const bool lastday = in_row && pos >= WF - F;
+            const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
+            o[e] = pick(lastday && f < F - 1, bsel, o[e]);
+            o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
+        }
+    }
+    return f4{o[0], o[1], o[2], o[3]};
+}
+
 template <int BLOCK, int POL>
 __global__ __launch_bounds__(BLOCK) void advance_flat_kernel(StepParams p, uint32_t qtot) {
     constexpr int kAux = POL == 1 ? 2 : POL == 2 ? 3 : 0;
@@ -1180,7 +1217,6 @@ __device__ __forceinline__ void flat_wg_body_patch(StepParams& p, uint32_t qtot,
     if (tid < 2) sh4[CPW + tid] = hal;
     __syncthreads();
     const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
-    const bool storage = p.ring_mode == PMENV_RING_STORAGE;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int j = 64 * V * wave + 64 * v + lane;
@@ -1190,35 +1226,14 @@ __device__ __forceinline__ void flat_wg_body_patch(StepParams& p, uint32_t qtot,
         const uint32_t row = fdiv(j0, p.div_wf);
         const int kk = (int)(j0 - row * (uint32_t)WF);
         const int t = (int)(b * (uint32_t)N + row - g_lo);
-        const int32_t k = sh_kc[t];
-        const bool shift_w = !(storage && k >= W - 1);
-        const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int f = f0 + e >= F ? f0 + e - F : f0 + e;
-            o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
-        }
-        const int slot_w =
-            (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
-        if (kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u)) {   // a last day or the slot
-            const f4 xb = sh_bar[t];
-            const float xwp = sh_wp[t];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int pos = kk + e;
-                const int f = f0 + e >= F ? f0 + e - F : f0 + e;
-                const bool in_row = pos < WF;
-                const bool lastday = in_row && pos >= WF - F;
-                const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
-                o[e] = pick(lastday && f < F - 1, bsel, o[e]);
-                o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
-            }
-        }
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, f4{o[0], o[1], o[2], o[3]});
+        const f4 o = compose2(p, kk, sh_kc[t], un, sh, [&](f4& xb, float& xwp) {
+            xb = sh_bar[t];
+            xwp = sh_wp[t];
+        });
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);
     }
 }
 

@@ -134,24 +134,16 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
         const int le = (int)(e - t.e_lo);
         const uint32_t j0 = 4u * (q - e * per4);
         const uint32_t row = fdiv(j0, p.div_wf);
-        FlatSide sd;
-        sd.kk = (int)(j0 - row * (uint32_t)WF);
-        sd.bar_nan = false;
-        sd.k = sh_k[le];
-        const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && sd.k >= p.W - 1);
-        const int slot_w =
-            (int)(((uint32_t)(1 + sd.k) - fdiv((uint32_t)(1 + sd.k), p.div_w) * (uint32_t)p.W) * F + (F - 1));
-        const bool need = sd.kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - sd.kk) <= 3u);
-        sd.xb = f4{0.f, 0.f, 0.f, 0.f};
-        sd.xwp = 0.f;
-        if (need) {
-            sd.xb = sh_bar[le][row];
-            sd.xwp = sh_wp[le][row];
-        }
+        const int kk = (int)(j0 - row * (uint32_t)WF);
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {t.own[v].x, t.own[v].y, t.own[v].z, t.own[v].w};
-        const f4 o = flat_compose(p, sd, un, sh);
+        // the two-level compose: only chunks holding a row's last day or ring slot read the
+        // env's bar / w' from LDS
+        const f4 o = compose2(p, kk, sh_k[le], un, sh, [&](f4& xb, float& xwp) {
+            xb = sh_bar[le][row];
+            xwp = sh_wp[le][row];
+        });
         buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                     // past the end: dropped
         if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
     }
@@ -297,25 +289,15 @@ __global__ __launch_bounds__(BLOCK) void step_flat_vec_kernel(StepParams p, uint
         const int le = (int)(e - e_lo);
         const uint32_t j0 = 4u * (q - e * per4);
         const uint32_t row = fdiv(j0, p.div_wf);
-        FlatSide sd;
-        sd.kk = (int)(j0 - row * (uint32_t)WF);
-        sd.bar_nan = false;
-        sd.k = sh_k[le];
-        const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && sd.k >= p.W - 1);
-        const int slot_w =
-            (int)(((uint32_t)(1 + sd.k) - fdiv((uint32_t)(1 + sd.k), p.div_w) * (uint32_t)p.W) * F + (F - 1));
-        const bool need = sd.kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - sd.kk) <= 3u);
-        sd.xb = f4{0.f, 0.f, 0.f, 0.f};
-        sd.xwp = 0.f;
-        if (need) {
-            const int r = (int)row - sh_rlo[le];
-            sd.xb = sh_bar[le][r];
-            sd.xwp = sh_wp[le][r];
-        }
+        const int kk = (int)(j0 - row * (uint32_t)WF);
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        const f4 o = flat_compose(p, sd, un, sh);
+        const f4 o = compose2(p, kk, sh_k[le], un, sh, [&](f4& xb, float& xwp) {
+            const int r = (int)row - sh_rlo[le];
+            xb = sh_bar[le][r];
+            xwp = sh_wp[le][r];
+        });
         buf_store4<kAuxS>(rd, (uint32_t)j * 16u, o);                    // past the end: dropped
         if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
     }
