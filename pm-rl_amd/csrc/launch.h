@@ -69,8 +69,9 @@ inline void launch_advance(const pmenv* h, const StepParams& p, hipStream_t stre
     else launch_advance_rows(h, p, stream);
 }
 
-// the first launch: the register form (N <= 64, one asset per lane, L = 32 / 64 lanes per
-// env), the packed strided form (64 < N <= 512), the LDS form (N > 512)
+// the first launch: the packed one-asset-per-lane form (N <= 16, L = 8 / 16 lanes per env),
+// the register form (16 < N <= 64, L = 32 / 64), the packed strided form (64 < N <= 512),
+// the LDS form (N > 512)
 template <int L, int A>
 inline void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
     const unsigned waves = (unsigned)((p.B + 64 / L - 1) / (64 / L));
@@ -79,7 +80,9 @@ inline void launch_scalar_vec_la(const StepParams& p, hipStream_t stream) {
 
 inline void launch_scalar_kernels(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const int N = h->cfg.num_assets;
-    if (h->k1_vec == kK1Str + 6402) launch_scalar_vec_la<64, 2>(p, stream);
+    if (h->k1_vec == kK1Str + 801) launch_scalar_vec_la<8, 1>(p, stream);
+    else if (h->k1_vec == kK1Str + 1601) launch_scalar_vec_la<16, 1>(p, stream);
+    else if (h->k1_vec == kK1Str + 6402) launch_scalar_vec_la<64, 2>(p, stream);
     else if (h->k1_vec == kK1Str + 6404) launch_scalar_vec_la<64, 4>(p, stream);
     else if (h->k1_vec == kK1Str + 6408) launch_scalar_vec_la<64, 8>(p, stream);
     else if (N <= 64) {

@@ -34,15 +34,20 @@ namespace {
 
 thread_local char g_create_err[512] = "";
 
-// K1 shape per asset count: N <= 64 takes the register form (one asset per lane; its
-// reductions — DPP row shifts, the fixed-order row combine — are bitwise those of the
-// one-launch steps' scalar part, so the paths, and sharded and unsharded runs whose
-// path can differ by env count, give the same bits); 64 < N <= 512 the packed strided
-// form (64 lanes x A assets, every dword load a coalesced run; step_flat_vec_kernel
-// shares it); N > 512 the LDS form.
+// K1 shape per asset count: N <= 64 keeps one asset per lane, with reductions bitwise
+// those of the one-launch steps' scalar part (so the paths, and sharded and unsharded
+// runs whose path can differ by env count, give the same bits): N <= 16 the packed form
+// with 8 / 16 lanes per env (8 / 4 envs per wave instead of 2; its butterfly pairs the
+// lanes as the row shifts do, every pair sum commutes bitwise, and the all-zero padding
+// lanes of the register form only add +0.0, which the packed form's 0.0 + x seed
+// reproduces), 16 < N <= 64 the register form; 64 < N <= 512 the packed strided form
+// (64 lanes x A assets, every dword load a coalesced run; step_flat_vec_kernel shares
+// it); N > 512 the LDS form.
 int pick_k1_vec(const pmenv_cfg& c) {
     const int N = c.num_assets;
     if ((int64_t)c.num_envs * N * 4 >= (1ll << 32)) return 0;     // descriptors span the [B*N] arrays
+    if (N <= 8) return kK1Str + 801;
+    if (N <= 16) return kK1Str + 1601;
     if (N <= 64) return 0;
     if (N <= 128) return kK1Str + 6402;
     if (N <= 256) return kK1Str + 6404;

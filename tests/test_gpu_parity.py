@@ -390,6 +390,47 @@ def test_gpu_one_and_two_launch_agree(db, kw):
         assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
 
 
+@pytest.mark.parametrize("N", [1, 5, 8, 9, 16])
+@pytest.mark.parametrize("kw", [MODES[0], MODES[2], MODES[6], MODES[8], MODES[9]],
+                         ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
+def test_gpu_small_n_paths_agree(N, kw):
+    """N <= 16: the two-launch step's packed scalar step (8 / 16 lanes per env) gives the
+    bits of the one-launch steps' register-form scalar part (flat, per-env) in every
+    path, including the signed-zero corners — all-zero and all -0.0 action rows, whose
+    sums the register form's padding lanes turn into +0.0."""
+    from pmenv import TradingEnv, synth
+    B = 41
+    W = -(-max(8, -(-592 // (5 * N))) // 4) * 4             # flat: >= 148 16-B chunks per env window
+    T = W + 4                                                  # through the storage-ring wrap
+    ser = synth.series(W + T, B, N, seed=zlib.crc32(f"small{N}{kw}".encode()), device=DEV)
+    act = synth.actions(T, B, N, seed=N + 3, device=DEV).clone()
+    act[:, 1::3] = act[:, 1::3] * 3.0 - 0.4                  # off-simplex rows, some negative weights
+    act[:, 3] = 0.0
+    act[:, 5] = -0.0
+    act[2:, 7] = -0.0
+    act[::2, 9, : (N + 1) // 2] = -0.0
+    impls = ("flat", "one_launch", "two_launch")
+    envs, obs = [], []
+    for impl in impls:
+        e = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl=impl, **kw)
+        o = synth.window_from_series(ser, W)
+        e.reset(o)
+        envs.append(e)
+        obs.append(o)
+    assert "scalar_step_vec_kernel" in envs[2].step_path
+    for t in range(T):
+        rs = []
+        for i, e in enumerate(envs):
+            r, _ = e.step(act[t], obs[i], bar=ser[W + t])
+            rs.append(r)
+        for i in (1, 2):
+            # bit patterns: the zero rows' w' is 0 / 0 (NaN), the same NaN in every path
+            assert torch.equal(obs[0].view(torch.int32), obs[i].view(torch.int32)), f"step {t} {impls[i]}: windows"
+            assert torch.equal(rs[0].view(torch.int32), rs[i].view(torch.int32)), f"step {t} {impls[i]}: rewards"
+            assert torch.equal(envs[0].value.view(torch.int64), envs[i].value.view(torch.int64)), \
+                f"step {t} {impls[i]}: values"
+
+
 @pytest.mark.parametrize("kind", ["simplex", "mixed", "rawpos"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 @pytest.mark.parametrize("kw", MODES, ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")

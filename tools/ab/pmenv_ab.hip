@@ -56,7 +56,7 @@ struct Tools {
 
 Tools* tools(const pmenv* h) { return static_cast<Tools*>(h->tools); }
 
-bool is_product_k1(int v) { return v == 0 || v == kK1Str + 6402 || v == kK1Str + 6404 || v == kK1Str + 6408; }
+bool is_product_k1(int v) { return v == 0 || v == kK1Str + 801 || v == kK1Str + 1601 || v == kK1Str + 6402 || v == kK1Str + 6404 || v == kK1Str + 6408; }
 
 // ---------------------------------------------------------------- the two-launch stream
 template <int BLOCK, int V, int ABL, int POL>
