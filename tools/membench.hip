@@ -183,6 +183,36 @@ __global__ __launch_bounds__(BLOCK) void inplace_unit_wc(float* x, int unit) {
     }
 }
 
+// 9. in-place shifted copy through an LDS image (the product stream's structure, no side
+// data, no halo): aligned own chunks -> LDS, barrier, two 16-B LDS reads, shift, store
+template <int BLOCK, int V>
+__global__ __launch_bounds__(BLOCK) void inplace_lds(float* x, int unit) {
+    __shared__ f4 img[BLOCK * V + 2];
+    f4* e = reinterpret_cast<f4*>(x) + (size_t)blockIdx.x * unit;
+    f4 r[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int q = threadIdx.x + i * BLOCK;
+        r[i] = q < unit ? e[q] : f4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) img[threadIdx.x + i * BLOCK] = r[i];
+    if (threadIdx.x < 2) img[BLOCK * V + threadIdx.x] = f4{0, 0, 0, 0};
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int q = threadIdx.x + i * BLOCK;
+        const f4 a = img[q + 1], b = img[q + 2];
+        if (q < unit) e[q] = f4{a.y, a.z, a.w, b.x};
+    }
+}
+
+// fills the buffer with non-zero data (the product's windows are prices, not zeros)
+__global__ void fill(float* x, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        x[i] = 100.0f + (float)(i % 977) * 0.013f;
+}
+
 template <typename F>
 double timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -213,6 +243,21 @@ int main(int argc, char** argv) {
     CK(hipMemset(a, 0, n4 * 16 + 256));
     CK(hipMemset(b, 0, n4 * 16 + 256));
     int reps = 20;
+    if (argc > 2 && atoi(argv[2]) == 1) {    // the LDS-image probe only, on non-zero data
+        fill<<<4096, 256>>>((float*)a, n4 * 4);
+        CK(hipDeviceSynchronize());
+        auto rep2 = [&](const char* name, double s) { printf("%-40s %8.1f us  %7.1f GB/s\n", name, s * 1e6, bytes / s / 1e9); };
+        char nm[80];
+#define RUNL(BL, V, UNIT) snprintf(nm, sizeof nm, "inplace lds  %4d f4 %4dx%d", UNIT, BL, V); \
+        rep2(nm, timeit([&] { inplace_lds<BL, V><<<(unsigned)(n4 / UNIT), BL>>>((float*)a, UNIT); }, reps));
+#define RUNU(BL, V, UNIT) snprintf(nm, sizeof nm, "inplace unit %4d f4 %4dx%d", UNIT, BL, V); \
+        rep2(nm, timeit([&] { inplace_unit<BL, V><<<(unsigned)(n4 / UNIT), BL>>>((float*)a, UNIT); }, reps));
+        RUNU(256, 2, 500) RUNU(512, 1, 500) RUNU(512, 4, 1875) RUNU(1024, 2, 1875)
+        RUNL(256, 2, 512) RUNL(512, 1, 512) RUNL(512, 2, 1024) RUNL(256, 4, 1024) RUNL(1024, 2, 2048)
+        RUNL(256, 2, 500) RUNL(512, 4, 1875) RUNL(1024, 2, 1875)
+        CK(hipFree(a)); CK(hipFree(b));
+        return 0;
+    }
     auto rep = [&](const char* name, double s) { printf("%-40s %8.1f us  %7.1f GB/s\n", name, s * 1e6, bytes / s / 1e9); };
     float* dummy; CK(hipMalloc(&dummy, 64));
     {
