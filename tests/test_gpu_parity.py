@@ -393,11 +393,12 @@ def test_gpu_one_and_two_launch_agree(db, kw):
 @pytest.mark.parametrize("N", [1, 5, 8, 9, 16])
 @pytest.mark.parametrize("kw", [MODES[0], MODES[2], MODES[6], MODES[8], MODES[9]],
                          ids=lambda k: "-".join(f"{a}={b}" for a, b in k.items()) or "reference")
-def test_gpu_small_n_paths_agree(N, kw):
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_small_n_paths_agree(N, kw, db):
     """N <= 16: the two-launch step's packed scalar step (8 / 16 lanes per env) gives the
     bits of the one-launch steps' register-form scalar part (flat, per-env) in every
-    path, including the signed-zero corners — all-zero and all -0.0 action rows, whose
-    sums the register form's padding lanes turn into +0.0."""
+    path, in place and double-buffered, including the signed-zero corners — all-zero and
+    all -0.0 action rows, whose sums the register form's padding lanes turn into +0.0."""
     from pmenv import TradingEnv, synth
     B = 41
     W = -(-max(8, -(-592 // (5 * N))) // 4) * 4             # flat: >= 148 16-B chunks per env window
@@ -421,7 +422,10 @@ def test_gpu_small_n_paths_agree(N, kw):
     for t in range(T):
         rs = []
         for i, e in enumerate(envs):
-            r, _ = e.step(act[t], obs[i], bar=ser[W + t])
+            if db:
+                r, obs[i] = e.step(act[t], obs[i], bar=ser[W + t], out=torch.empty_like(obs[i]))
+            else:
+                r, _ = e.step(act[t], obs[i], bar=ser[W + t])
             rs.append(r)
         for i in (1, 2):
             # bit patterns: the zero rows' w' is 0 / 0 (NaN), the same NaN in every path

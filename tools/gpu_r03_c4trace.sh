@@ -4,6 +4,9 @@ set -u
 export TMPDIR=/tmp
 TAG=${1:-r03c4}
 mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py \
+  -k small_n_paths_agree > gpurun_out/smalln_tests_$TAG.log 2>&1 || { tail -30 gpurun_out/smalln_tests_$TAG.log; exit 1; }
+tail -1 gpurun_out/smalln_tests_$TAG.log
 for B in 8192 4096; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$B -o run --output-format csv -- \
     python3 bench.py --envs-per-gpu $B --steps 200 --warmup 20 --cpu-baseline 0 --alt-steps 0 > gpurun_out/prof_${TAG}_$B.log 2>&1 || exit $?
