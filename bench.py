@@ -275,6 +275,15 @@ def weak_leg(args, rank, world, dev, lib, _abi, synth, TradingEnv, torch, dist):
     return out
 
 
+def lib_source_sha256():
+    """sha256 of the product library's sources and build script (tools/libfp.py), or None."""
+    try:
+        from tools.libfp import source_sha256
+    except ImportError:
+        return None
+    return source_sha256(ROOT)
+
+
 def sha256_file(path):
     import hashlib
     h = hashlib.sha256()
@@ -487,16 +496,21 @@ def main():
     window_bytes = B * N * W * F * 4
     traffic, traffic_src = None, None
     lib_sha = sha256_file(_abi.LIB_PATH)
+    src_sha = lib_source_sha256()
     try:
         pmc = json.load(open(args.pmc_file))
         # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py) of the same kernel at
-        # the same workload, measured on THIS library build (its sha256 recorded on the box):
-        # anything else reports null rather than a stale figure
+        # the same workload, measured on THIS library — the same binary, or (hipcc output is
+        # not byte-reproducible) a build of the same sources and build script: anything else
+        # reports null rather than a stale figure
         same = pmc.get("workload") == [B, N, W, F] and f"::{kernel}<" in pmc.get("dominant_kernel", "")
+        same_bin = pmc.get("lib_sha256") == lib_sha
+        same_src = src_sha is not None and pmc.get("lib_src_sha256") == src_sha
         traffic_src = {"file": os.path.relpath(args.pmc_file, ROOT), "tag": pmc.get("tag"),
                        "lib_sha256": pmc.get("lib_sha256"), "running_lib_sha256": lib_sha,
-                       "same_workload_and_kernel": same,
-                       "same_library": pmc.get("lib_sha256") == lib_sha}
+                       "lib_src_sha256": pmc.get("lib_src_sha256"), "running_lib_src_sha256": src_sha,
+                       "same_workload_and_kernel": same, "same_binary": same_bin, "same_sources": same_src,
+                       "same_library": same_bin or same_src}
         if same and traffic_src["same_library"]:
             traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):

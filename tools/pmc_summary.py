@@ -59,6 +59,10 @@ if main:
 import hashlib  # noqa: E402
 lib = os.path.join(ROOT, "pm-rl_amd", "pmenv", "libpmenv.so")
 res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
+# ... or a build of the same sources (hipcc output is not byte-reproducible: tools/libfp.py)
+sys.path.insert(0, ROOT)
+from tools.libfp import source_sha256  # noqa: E402
+res["lib_src_sha256"] = source_sha256(ROOT)
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
 json.dump(res, open(os.path.join(ROOT, "profiles", f"pmc_{tag}.json"), "w"), indent=1)
