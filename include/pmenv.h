@@ -178,6 +178,11 @@ typedef struct pmenv_step_args {
  *    at t = W-1, and if prices == NULL the relatives are
  *    bar[close] / obs[W-1, close] (instrument.py:79), with obs[W-1, close]
  *    taken from the env's last_close state (equal to it by construction).
+ *    The window's channel F-1 is the ring itself here: the step shifts it with
+ *    the window (or, storage order with the ring full, rewrites only the slot),
+ *    so an edit the caller makes to that channel persists, where surface mode
+ *    rewrites the whole channel from the ring; market-channel edits are honoured
+ *    in both modes (announce in-place edits with pmenv_window_written).
  * Portfolio value (f64, env-owned) is readable through pmenv_value(). */
 int pmenv_step_ex(pmenv* h, const pmenv_step_args* args, hipStream_t stream);
 int pmenv_step(pmenv* h, const float* action, const float* prices, const float* bar,
