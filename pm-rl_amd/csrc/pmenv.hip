@@ -698,12 +698,17 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     // SIMD, so a 65,536-env rollout's 1,024 workgroups are resident at once; the same bits):
     // 56.7 vs 58.5 us at 256 x 65,536, 110.1 vs 114.7 at 512 x 65,536; slower below 65,536
     // envs or 256 days (profiles/ab_r02/gae_occ8_r02zl.json)
+    // adv / ret are written once and read by the learner later: nt stores where they measured
+    // faster (the same bits): 62.3 -> 45.7 us at 256 x 65,536, 9.0 -> 8.4 at 256 x 4,096,
+    // 80.2 -> 58.9 at 2,048 x 8,192 on the tile; at 256 x 16,384 (the U = 8 tile, a cache-
+    // resident rollout) 14.1 vs 14.5, so that form keeps plain stores
+    // (profiles/rows_r03ad/rows_nt2.json)
     if (tile && U == 8 && B >= 65536 && T >= 256)
-        gae_tile_kernel<8, 8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
-                                                                   lam);
+        gae_tile_kernel<8, 8, 8, 2><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                      lam);
     else if (tile && U == 16)
-        gae_tile_kernel<8, 16><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
-                                                                 lam);
+        gae_tile_kernel<8, 16, 1, 2><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                       lam);
     else if (tile)
         gae_tile_kernel<8, 8><<<(B + 63) / 64, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
                                                                 lam);
@@ -853,8 +858,11 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     // 16-B aligned series / s (C callers may pass sliced views: those take the row form)
     const bool al16 = (((uintptr_t)series | (uintptr_t)s) & 15u) == 0;
     const bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && al16;
+    // the windows are written once and read by the learner later: nt stores (the tile's
+    // bits unchanged), per call 29.0 -> 27.5 us at 4,096 samples, 235.1 -> 196.9 at 32,768,
+    // 74.4 -> 54.3 at 8,192 from a 65,536 x 64 buffer (profiles/rows_r03ad/rows_nt.json)
     if (tile) {                                            // one workgroup per sample, staged in LDS
-        rollout_gather_tile_kernel<<<(unsigned)S, 256, lds, stream>>>(
+        rollout_gather_tile_kernel<2><<<(unsigned)S, 256, lds, stream>>>(
             series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N),
             make_fastdiv((uint32_t)(W * F)), make_fastdiv((uint32_t)F));
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;

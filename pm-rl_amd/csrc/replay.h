@@ -116,7 +116,10 @@ static __global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const f
 // contiguous run of [T_rec, B, N] — and the [N, W, 5] window is written as 16-B chunks
 // from LDS (a lane's four floats walk (asset, day, channel) incrementally). Every weight
 // line is fetched once per sample, where the per-row form fetches it per asset row.
-static __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
+// NT: cache-policy bits of the window stores (0: plain stores; 2: nt, the product; the tools
+// build A/Bs the others through the same buffer stores)
+template <int NT = 0>
+__global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
                                                                   const int32_t* start, const float* weights, int B,
                                                                   int ring_mode, const int32_t* t_idx,
                                                                   const int32_t* env, float* s, FastDiv div_n,
@@ -183,7 +186,8 @@ static __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const f
                 }
             }
         }
-        out[q] = f4{v[0], v[1], v[2], v[3]};
+        if constexpr (NT == 0) out[q] = f4{v[0], v[1], v[2], v[3]};
+        else buf_store4<NT>(make_rsrc(out, (uint32_t)nq * 16u), (uint32_t)q * 16u, f4{v[0], v[1], v[2], v[3]});
     }
 }
 

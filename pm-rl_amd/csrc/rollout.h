@@ -83,7 +83,8 @@ static __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, co
 // Loads are buffer loads with the lane's env as the (only) VGPR offset and the
 // wave-uniform row as the SGPR offset, so U rows in flight cost no address VGPRs.
 // Needs every array below 2 GiB (the host checks).
-template <int NW, int U, int OCC = 1>
+// SP: cache-policy bits of the adv / ret stores (0 in the product; tools A/B)
+template <int NW, int U, int OCC = 1, int SP = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) void gae_tile_kernel(
     const float* r, const float* v, const uint8_t* dones, float* adv, float* ret, int T, int B, float gamma,
     float lam) {
@@ -155,9 +156,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) 
                 const double d = RECOMP ? (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u] : dl[RECOMP ? 0 : u];
                 a = d + gl * n * a;
                 // lanes past B: voff is out of range for the store descriptors -> dropped
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, SP);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret, voff_st,
-                                                      (uint32_t)t * row, 0);
+                                                      (uint32_t)t * row, SP);
             }
         }
         for (int j = NW - 1; j >= 0; --j) carry = shD[j][lane] + shC[j][lane] * carry;

@@ -562,6 +562,22 @@ bool launch_flat1(const pmenv* h, const StepParams& p, unsigned grid, bool out, 
 bool gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
          int32_t B, float gamma, float lam, hipStream_t stream, int* rc) {
     const char* k = knob("PMENV_GAE");
+    if (const char* sp = knob("PMENV_GAE_SP")) {   // the product's tile choice, stores with policy 2 (nt) / 16 (sc1)
+        const int a = atoi(sp);
+        const bool big = B >= 65536 && T >= 256;
+        const unsigned g = (unsigned)((B + 63) / 64);
+#define PMENV_GAESP(A_)                                                                                        \
+    do {                                                                                                       \
+        if (big) gae_tile_kernel<8, 8, 8, A_><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam); \
+        else if (B < 16384) gae_tile_kernel<8, 16, 1, A_><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam); \
+        else gae_tile_kernel<8, 8, 1, A_><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam); \
+    } while (0)
+        if (a == 2) PMENV_GAESP(2);
+        else PMENV_GAESP(16);
+#undef PMENV_GAESP
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (!k && !knob("PMENV_GAE_U") && !knob("PMENV_GAE_E")) return false;
     const bool fits = (size_t)(T + 1) * (size_t)B * 4u < (1ull << 31);
     const bool scan = k ? !strcmp(k, "scan") : (B < 64 && T >= 256);
@@ -676,7 +692,8 @@ bool replay_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t
 }
 
 // rollout gather: PMENV_RGATHER_ELEM (one thread per output float), PMENV_RGATHER_ROWS (the
-// wave-per-row form)
+// wave-per-row form), PMENV_RGATHER_NT=2|16|18 (the product's tile, window stores with those
+// cache-policy bits)
 bool rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_t W, const int32_t* start,
                     const float* weights, int32_t T_rec, int32_t B, int32_t ring_mode, const int32_t* t_idx,
                     const int32_t* env, int32_t S, float* s, hipStream_t stream, int* rc) {
@@ -684,6 +701,17 @@ bool rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, int32_
         const int64_t threads = (int64_t)S * N * W * F;
         rollout_gather_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(
             series, T, N, F, W, start, weights, T_rec, B, ring_mode, t_idx, env, S, s);
+    } else if (const char* nt = knob("PMENV_RGATHER_NT")) {      // the tile with nt (2) / sc1 (16) stores
+        const size_t lds = (size_t)W * N * F * sizeof(float);
+        const int aux = atoi(nt);
+        auto go = [&](auto kern) {
+            kern<<<(unsigned)S, 256, lds, stream>>>(series, T, N, W, start, weights, B, ring_mode, t_idx, env, s,
+                                                   make_fastdiv((uint32_t)N), make_fastdiv((uint32_t)(W * F)),
+                                                   make_fastdiv((uint32_t)F));
+        };
+        if (aux == 2) go(rollout_gather_tile_kernel<2>);
+        else if (aux == 16) go(rollout_gather_tile_kernel<16>);
+        else go(rollout_gather_tile_kernel<18>);
     } else if (knob("PMENV_RGATHER_ROWS")) {
         const int64_t rows = (int64_t)S * N;
         rollout_gather_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(

@@ -93,10 +93,12 @@ def main():
                           "stream8": {"PMENV_GAE": "stream", "PMENV_GAE_P": "8"},
                           "stream16": {"PMENV_GAE": "stream", "PMENV_GAE_P": "16"},
                           "stream32": {"PMENV_GAE": "stream", "PMENV_GAE_P": "32"},
+                          "tile_nt": {"PMENV_GAE_SP": "2"},
+                          "tile_sc1": {"PMENV_GAE_SP": "16"},
                           "auto": {}})
             nbytes = lib.pmenv_gae_workspace(T, B)
             work = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=dev)
-            gk = ("PMENV_GAE", "PMENV_GAE_U", "PMENV_GAE_P")
+            gk = ("PMENV_GAE", "PMENV_GAE_U", "PMENV_GAE_P", "PMENV_GAE_SP")
             outs = {}
             for mode, env in modes.items():
                 for k in gk:
@@ -132,17 +134,21 @@ def main():
                                                        P(tix), P(eix), S, P(out_c), st), "rollout_gather")
             outs = {}
             # the product's LDS-staged tile, the wave-per-row and float-per-thread forms (tools)
-            for form, knob in (("tile", None), ("rows", "PMENV_RGATHER_ROWS"), ("elem", "PMENV_RGATHER_ELEM")):
-                os.environ.pop("PMENV_RGATHER_ELEM", None)
-                os.environ.pop("PMENV_RGATHER_ROWS", None)
+            forms = (("tile", None), ("rows", "PMENV_RGATHER_ROWS"), ("elem", "PMENV_RGATHER_ELEM"),
+                     ("tile_nt", "PMENV_RGATHER_NT=2"), ("tile_sc1", "PMENV_RGATHER_NT=16"),
+                     ("tile_nt_sc1", "PMENV_RGATHER_NT=18"))
+            for form, knob in forms:
+                for k in ("PMENV_RGATHER_ELEM", "PMENV_RGATHER_ROWS", "PMENV_RGATHER_NT"):
+                    os.environ.pop(k, None)
                 if knob:
-                    os.environ[knob] = "1"
+                    k, _, val = knob.partition("=")
+                    os.environ[k] = val or "1"
                 call()
                 outs[form] = out_c.clone()
                 res.append(row(f"rollout_gather_{form}", timeit(call, a.reps), S * N_ * W_ * 5 * 4, B=Bc, T=Tr, S=S,
                                N=N_, W=W_, same_bits=bool(torch.equal(outs[form], outs["tile"]))))
-            os.environ.pop("PMENV_RGATHER_ELEM", None)
-            os.environ.pop("PMENV_RGATHER_ROWS", None)
+            for k in ("PMENV_RGATHER_ELEM", "PMENV_RGATHER_ROWS", "PMENV_RGATHER_NT"):
+                os.environ.pop(k, None)
             del outs
             del ser_c, wts, out_c
         # advantage moments (the 24-byte all-reduce's input)
