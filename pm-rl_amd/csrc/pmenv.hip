@@ -726,7 +726,10 @@ namespace {
 constexpr int kGaeSeg = 8 * 16;
 int gae_chunks(int32_t T, int32_t B, int* Lc) {
     const int blocks = (B + 63) / 64;
-    if (B >= 16384 || T < 4 * kGaeSeg) return 0;
+    // from 8,192 envs (128 workgroups) the one-pass tile with nt stores wins: 2,048 x 8,192
+    // 59.0 vs 74.2 us split (profiles/rows_r03af/rows_r03af.json); the split keeps 512 envs
+    // x 4,096 days at 16.4 against the tile's 102
+    if (B >= 8192 || T < 4 * kGaeSeg) return 0;
     if ((size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
     int want = (1024 + blocks - 1) / blocks;                    // chunks for ~1024 workgroups
     int lc = (T + want - 1) / want;
@@ -757,7 +760,7 @@ int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones
     const dim3 grid((unsigned)((B + 63) / 64), (unsigned)n);
     gae_chunk_kernel<8, 16, true><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
                                                             work);
-    gae_chunk_kernel<8, 16, false><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
+    gae_chunk_kernel<8, 16, false, 2><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
                                                              work);
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const fl
 //               carry-in, then runs the tiled scan over its chunk writing adv / ret.
 // The inputs are read twice (26 B per element instead of 17) in exchange for
 // chunks x the workgroups; selected by the host only where B / 64 leaves the CUs idle.
-template <int NW, int U, bool MAPS>
+// SP: cache-policy bits of the apply pass's adv / ret stores
+template <int NW, int U, bool MAPS, int SP = 0>
 __global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, const float* v, const uint8_t* dones,
                                                            float* adv, float* ret, int T, int B, float gamma,
                                                            float lam, int Lc, double* maps) {
@@ -314,9 +315,9 @@ __global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, cons
                     const double n = (alive >> u) & 1u ? 1.0 : 0.0;
                     a = dl[u] + gl * n * a;
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st,
-                                                          (uint32_t)t * row, 0);
+                                                          (uint32_t)t * row, SP);
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret,
-                                                          voff_st, (uint32_t)t * row, 0);
+                                                          voff_st, (uint32_t)t * row, SP);
                 }
             }
         }

@@ -599,6 +599,8 @@ def test_gpu_synth_matches_oracle():
                                         # tiled: T below / across / not a multiple of the segment, ragged B
                                         (37, 100, "tile16"), (64, 64, "tile16"), (129, 4099, "tile16"),
                                         (300, 130, "tile16"), (256, 65536, "tile8"), (37, 16385, "tile8"),
+                                        # from 8,192 envs long horizons take the tile, not the split
+                                        (2048, 8192, "tile16"),
                                         # the 64-VGPR tile (B >= 65,536, T >= 256): ragged B, T past a segment
                                         (300, 70001, "tile8_occ8"), (256, 65600, "tile8_occ8")])
 def test_gpu_gae_kernels_match_oracle(T, B, kernel):
@@ -641,7 +643,7 @@ def test_gpu_gae_per_env_loop_beyond_tile_offsets():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 8192), (700, 4099),
+@pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 4096), (700, 4099),
                                  (16384, 64)])
 def test_gpu_gae_horizon_split_matches_oracle(T, B):
     """The default wrapper path (pmenv_gae_ex): few envs x long horizons split the
