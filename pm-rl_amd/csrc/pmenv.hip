@@ -863,11 +863,18 @@ int pmenv_rollout_gather(const float* series, int32_t T, int32_t N, int32_t F, i
     const bool tile = F == 5 && (N * W * F) % 4 == 0 && lds <= 64 * 1024 && al16;
     // the windows are written once and read by the learner later: nt stores (the tile's
     // bits unchanged), per call 29.0 -> 27.5 us at 4,096 samples, 235.1 -> 196.9 at 32,768,
-    // 74.4 -> 54.3 at 8,192 from a 65,536 x 64 buffer (profiles/rows_r03ad/rows_nt.json)
+    // 74.4 -> 54.3 at 8,192 from a 65,536 x 64 buffer; windows that fit well inside the
+    // Infinity Cache (<= 128 MiB) take sc1 stores instead: 24.1-24.5 us at 4,096 samples
+    // (123 MB), which lose 1.5-2x from 245 MB up (profiles/rows_r03ad/, rows_r03ae/)
     if (tile) {                                            // one workgroup per sample, staged in LDS
-        rollout_gather_tile_kernel<2><<<(unsigned)S, 256, lds, stream>>>(
-            series, T, N, W, start, weights, B, ring_mode, t_idx, env, s, make_fastdiv((uint32_t)N),
-            make_fastdiv((uint32_t)(W * F)), make_fastdiv((uint32_t)F));
+        const bool small = (size_t)S * N * W * F * sizeof(float) <= ((size_t)128 << 20);
+        auto go = [&](auto kern) {
+            kern<<<(unsigned)S, 256, lds, stream>>>(series, T, N, W, start, weights, B, ring_mode, t_idx, env, s,
+                                                   make_fastdiv((uint32_t)N), make_fastdiv((uint32_t)(W * F)),
+                                                   make_fastdiv((uint32_t)F));
+        };
+        if (small) go(rollout_gather_tile_kernel<16>);
+        else go(rollout_gather_tile_kernel<2>);
         return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
     }
     const int64_t rows = (int64_t)S * N;                 // one wave per (sample, asset) row

@@ -116,8 +116,8 @@ static __global__ __launch_bounds__(256) void rollout_gather_rows_kernel(const f
 // contiguous run of [T_rec, B, N] — and the [N, W, 5] window is written as 16-B chunks
 // from LDS (a lane's four floats walk (asset, day, channel) incrementally). Every weight
 // line is fetched once per sample, where the per-row form fetches it per asset row.
-// NT: cache-policy bits of the window stores (0: plain stores; 2: nt, the product; the tools
-// build A/Bs the others through the same buffer stores)
+// NT: cache-policy bits of the window stores (0: plain stores; the product: 16, sc1, for
+// windows <= 128 MiB, else 2, nt; the tools build A/Bs the others)
 template <int NT = 0>
 __global__ __launch_bounds__(256) void rollout_gather_tile_kernel(const float* series, int T, int N, int W,
                                                                   const int32_t* start, const float* weights, int B,
