@@ -26,9 +26,10 @@ Legs, in order (one process per GPU):
   3. the other window mode (alt), the collective (N > 1), then on rank 0 at N = 1
      the CPU baseline and the replay of the reference's own recorded outputs.
 
-Multi-GPU runs are weak-scaled by default (65,536 envs per rank, envs sharded by
-global id, no collective in the step); --global-envs G runs G envs in total sharded
-over the ranks (strong scaling; BASELINE config 4 is 65,536 over 8 GPUs):
+Multi-GPU runs are strong-scaled by default: the north star's 65,536 envs in total,
+sharded over the ranks by global id (BASELINE config 4: 8,192 per GPU at N = 8; no
+collective in the step); --global-envs G sets the total, --weak keeps 65,536 envs per
+rank instead:
 
     python bench.py                                   # N = 1
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \

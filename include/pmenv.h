@@ -32,7 +32,9 @@
 extern "C" {
 #endif
 
-#define PMENV_ABI_VERSION 1
+/* 2: pmenv_window_written / pmenv_state_written added; pmenv_cfg_default's ret_mode is
+ *    PMENV_RET_GROSS (trading_env.py:88 for every reward kind; was AUTO in 1) */
+#define PMENV_ABI_VERSION 2
 
 /* Opaque HIP stream (identical to HIP's own typedef); NULL = default stream. */
 typedef struct ihipStream_t* hipStream_t;

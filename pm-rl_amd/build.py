@@ -89,4 +89,7 @@ def build_all(force=False):
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if "--ab-only" in sys.argv:      # the tools library alone (an A/B run on the GPU box builds it there)
+        build_pmenv("--force" in sys.argv, ab=True)
+    else:
+        build_all(force="--force" in sys.argv)

@@ -77,10 +77,9 @@ struct FlatTile {
     ScalarIn sin;
 };
 
-template <int BLOCK, int V, int POL, bool OUT>
+// AUX: the window loads' buffer cache-policy bits (0 default, 2 nt)
+template <int BLOCK, int V, int AUX, bool OUT>
 __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, uint32_t tile, FlatTile<V>& t) {
-    // window loads: nt for POL 1, 3 (tools A/B: 5 sc0 nt, 6 sc1 nt, 7 nt)
-    constexpr int kAux = (POL == 1 || POL == 3 || POL == 7) ? 2 : POL == 5 ? 3 : POL == 6 ? 18 : 0;
     constexpr int CPW = BLOCK * V;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     t.c0 = tile * (uint32_t)CPW;
@@ -92,7 +91,7 @@ __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, u
     __builtin_amdgcn_sched_barrier(0);
     const auto rs = make_rsrc(p.obs + (size_t)t.c0 * 4, t.nblk * 16u);
 #pragma unroll
-    for (int v = 0; v < V; ++v) t.own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    for (int v = 0; v < V; ++v) t.own[v] = buf_load4<AUX>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
     const uint32_t ntiles = (qtot + CPW - 1) / CPW;
     const uint32_t nh = tile + 1 < ntiles ? min(2u, qtot - t.c0 - t.nblk) : 0u;
     const float* hsrc = OUT ? p.obs + (size_t)(t.c0 + t.nblk) * 4 : p.halo_in + (size_t)tile * 8;
@@ -100,11 +99,10 @@ __device__ __forceinline__ void flat1_load(const StepParams& p, uint32_t qtot, u
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BLOCK, int V, int POL, bool OUT>
+// AUX: the window stores' buffer cache-policy bits (0 default, 2 nt)
+template <int BLOCK, int V, int AUX, bool OUT>
 __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot, uint32_t tile, const FlatTile<V>& t,
                                               f4* sh4, f4 (*sh_bar)[64], float (*sh_wp)[64], int32_t* sh_k) {
-    // window stores: nt for POL 1, 4 (tools A/B: 5 sc0 nt, 6 and 7 sc1 nt)
-    constexpr int kAux = (POL == 1 || POL == 4) ? 2 : POL == 5 ? 3 : (POL == 6 || POL == 7) ? 18 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t per4 = p.per4;
@@ -144,7 +142,7 @@ __device__ __forceinline__ void flat1_process(const StepParams& p, uint32_t qtot
             xb = sh_bar[le][row];
             xwp = sh_wp[le][row];
         });
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                     // past the end: dropped
+        buf_store4<AUX>(rd, (uint32_t)j * 16u, o);                     // past the end: dropped
         if (first_out && j < 2) reinterpret_cast<f4*>(p.halo_out)[2 * (tile - 1) + j] = o;
     }
     // 6. the scalar steps' tails: state, ring slot, snapshot and reward (the owner only)
@@ -179,28 +177,24 @@ __device__ __forceinline__ void flat_seq_enter(StepParams& p) {
     }
 }
 
-// POL: cache policy of the window stream (0 default, 1 nt; tools A/B: 3 nt loads only,
-// 4 nt stores only); OUT: double-buffered (the
-// two chunks past a tile are read straight from obs, no halo). BLOCK x V: 256 x 4 (env
-// windows of >= 511 chunks) or 512 x 2 (148 .. 510), host-chosen. Held to 80 SGPRs where
-// the compiler can (512 x 2: 8 waves per SIMD instead of 7).
-template <int BLOCK, int V, int POL, bool OUT, bool XCD = false>
+// POL: cache policy of the window stream, loads and stores (0 default, 1 nt); OUT:
+// double-buffered (the two chunks past a tile are read straight from obs, no halo).
+// BLOCK x V: 128 x 8 / 256 x 4 (env windows of >= 511 chunks) or 512 x 2 (148 .. 510),
+// host-chosen. Held to 80 SGPRs where the compiler can (512 x 2: 8 waves per SIMD
+// instead of 7). (The tile orders and per-direction policies measured against it are
+// the tools build's step_flat_ab_kernel, tools/ab/ab_kernels.h.)
+template <int BLOCK, int V, int POL, bool OUT>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void step_flat_kernel(StepParams p,
                                                                                               uint32_t qtot) {
-    constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64;
+    constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64, AUX = POL == 1 ? 2 : 0;
     __shared__ f4 sh4[CPW + 2];
     __shared__ f4 sh_bar[WAVES][64];
     __shared__ float sh_wp[WAVES][64];
     __shared__ int32_t sh_k[WAVES];
-    uint32_t tile = blockIdx.x;
-    if (XCD) {   // tools A/B: XCD x (workgroups x, x + 8, ...) takes a contiguous range of tiles
-        const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = tile & 7, i = tile >> 3;
-        tile = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-    }
     flat_seq_enter<OUT>(p);
     FlatTile<V> t;
-    flat1_load<BLOCK, V, POL, OUT>(p, qtot, tile, t);
-    flat1_process<BLOCK, V, POL, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
+    flat1_load<BLOCK, V, AUX, OUT>(p, qtot, blockIdx.x, t);
+    flat1_process<BLOCK, V, AUX, OUT>(p, qtot, blockIdx.x, t, sh4, sh_bar, sh_wp, sh_k);
 }
 
 // ---------------------------------------------------------------- wide envs (64 < N <= 512)

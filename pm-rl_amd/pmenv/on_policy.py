@@ -72,6 +72,7 @@ class OnPolicy:
         self.explore_std = float(explore_std)
         self.explore_seed = int(explore_seed)
         self.env_offset = int(env_offset)
+        self._u = None                 # [T, B, N] centred logits the last exploring rollout sampled
 
     def act(self, s, t=None):
         """agent.act (pg.py:29-38): the policy's scores, softmaxed over assets; with
@@ -81,6 +82,9 @@ class OnPolicy:
             mu = self.policy(s.to(dtype)).squeeze(-1).float()
             if self.explore_std > 0.0 and t is not None:
                 mu = mu + self.explore_std * self._noise[t - 1]
+                # the sampled centred logits, scored later by log_prob: recovering them from
+                # the softmax action loses them where the softmax underflows
+                self._u[t - 1] = mu - mu.mean(dim=-1, keepdim=True)
             return torch.softmax(mu, dim=-1)
 
     def _draw_noise(self):
@@ -91,6 +95,7 @@ class OnPolicy:
         la = torch.log(synth.actions(buf.T, buf.B, buf.N, env_offset=self.env_offset, seed=self.explore_seed,
                                      device=self.env.device))
         self._noise = la - la.mean(dim=-1, keepdim=True)
+        self._u = torch.empty_like(self._noise)          # [T, B, N] sampled centred logits (act)
 
     def rollout(self, obs0=None, bars=None, start=None):
         """train/on_policy.py:59-67 for every env at once. Slab form: obs0 [B, N, W, F] is
@@ -152,16 +157,24 @@ class OnPolicy:
         adv, ret = self.buf.returns(values, gamma, lam)
         return parallel.normalize(adv, group=group, eps=eps), ret, values
 
-    def log_prob(self, s, a):
+    def log_prob(self, s, a, u=None):
         """log pi(a | s) of the exploring policy, up to a constant: the action's centred
-        log-weights u against the centred scores mu under N(mu, explore_std^2) on the
-        simplex's logit plane (softmax is shift-invariant, so only centred logits matter).
-        s [S, N, W, F], a [S, N] -> [S]."""
+        logits u against the centred scores mu under N(mu, explore_std^2) on the simplex's
+        logit plane (softmax is shift-invariant, so only centred logits matter).
+        s [S, N, W, F], a [S, N] -> [S]. u [S, N]: the centred logits act() sampled (exact);
+        None recovers them as the centred log of a, which is biased where the softmax
+        underflowed (a warning names how many actions hold such weights)."""
         mu = self.policy(s).squeeze(-1)
         mu = mu - mu.mean(dim=-1, keepdim=True)
-        la = torch.log(a.to(mu.dtype).clamp(min=torch.finfo(torch.float32).tiny))
-        u = la - la.mean(dim=-1, keepdim=True)
-        return -((u - mu) ** 2).sum(dim=-1) / (2.0 * self.explore_std ** 2)
+        if u is None:
+            tiny = torch.finfo(torch.float32).tiny
+            if bool((a < 1e-30).any()):
+                import warnings
+                warnings.warn(f"log_prob: {int((a < 1e-30).any(dim=-1).sum())} actions hold softmax weights "
+                              "below 1e-30; their logits are not recoverable from the action (pass u)")
+            la = torch.log(a.to(mu.dtype).clamp(min=tiny))
+            u = la - la.mean(dim=-1, keepdim=True)
+        return -((u.to(mu.dtype) - mu) ** 2).sum(dim=-1) / (2.0 * self.explore_std ** 2)
 
     def update_actor_critic(self, adv, group=None, chunk=None):
         """One actor-critic policy step on the normalised advantages advantages() returns
@@ -190,7 +203,8 @@ class OnPolicy:
             idx = torch.arange(i, min(i + cs, n), device=adv.device)
             t, env = idx // B + 1, idx % B
             s, a, _r, _v, _a, _p = buf.gather(t, env)
-            lp = self.log_prob(s.to(dtype), a.reshape(-1, buf.N))
+            u = None if self._u is None else self._u[t - 1, env]      # None: a buffer filled without act()
+            lp = self.log_prob(s.to(dtype), a.reshape(-1, buf.N), u=u)
             loss = -(adv[t - 1, env].to(dtype) * lp).sum()
             loss.backward()
             loss_sum += loss.detach().double()

@@ -62,9 +62,16 @@ def allreduce_grads(params, loss_sum, count, group=None):
     f64 bucket: the gradients of a small policy are a few hundred KB, one latency-bound
     exchange over xGMI), then every gradient is divided by the global count. Returns
     (global loss sum, global count) as python floats."""
-    ps = [p for p in params if p.grad is not None]
-    dev = ps[0].grad.device if ps else torch.device("cpu")
-    parts = [p.grad.detach().reshape(-1).to(torch.float64) for p in ps]
+    # every parameter, in order, on every rank: a parameter without a gradient (a rank with
+    # no envs, a branch unused there) contributes zeros, so the buckets line up over ranks
+    ps = list(params)
+    if not ps:
+        raise ValueError("allreduce_grads needs the replicated parameters")
+    dev = ps[0].device
+    for p in ps:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    parts = [p.grad.detach().reshape(-1).to(device=dev, dtype=torch.float64) for p in ps]
     extra = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64).reshape(()).to(dev),
                          torch.tensor(float(count), dtype=torch.float64, device=dev)])
     bucket = torch.cat(parts + [extra])
@@ -74,6 +81,6 @@ def allreduce_grads(params, loss_sum, count, group=None):
     off = 0
     for p in ps:
         k = p.grad.numel()
-        p.grad.copy_((bucket[off:off + k] / n).reshape(p.grad.shape).to(p.grad.dtype))
+        p.grad.copy_((bucket[off:off + k] / n).reshape(p.grad.shape).to(device=p.grad.device, dtype=p.grad.dtype))
         off += k
     return total, n

@@ -4,13 +4,23 @@ Mirrors zachramsey/pm-rl env/sim/trading_env.py (`TradingEnv`, :7-115) call for
 call, with a leading batch dimension B of lockstep envs:
 
     reference                                  here
-    TradingEnv()                      :8-18    TradingEnv(num_envs=B, num_assets=N, window=W)
+    TradingEnv()                      :8-18    TradingEnv()  (shape bound by the first reset / step)
+                                               TradingEnv(num_envs=B, num_assets=N, window=W, features=F)
     reset(features) -> features       :21-41   reset(features[, mask]) -> features  (in place)
     step(action, features, prices)    :44-105  step(action, features, prices) -> (r, features)
       -> (r, features)                         step(action, features, bar=bar)  (fused window advance)
-    .value                            :9,89    .value  (f64 [B], device view)
+    .value                            :9,89    .value  (f64 [B], device view; host 0-dim with host I/O)
     .weights (ActionBuffer)           :10      .weights (RingView: get_last / get_all)
-    .info values/actions/rewards/returns       .info (opt-in, track_info=True)
+    .info values/actions/rewards/returns       .info (kept by default for one env, as the reference)
+
+`TradingEnv()` with no arguments is the reference's constructor (`train/on_policy.py:35`):
+the reference sizes its ring from config/base.py's NUM_ASSETS / WINDOW_SIZE and takes
+whatever feature count the data pool carries (`data/data_loader.py:48`), so here every
+dimension that is not given — envs, assets, window, features — is taken from the first
+`reset(features)` (or `step`) tensor: `[N, W, F]` for one env, `[B, N, W, F]` for B.
+Dimensions that are given are checked against it (ValueError, as a ring of the wrong
+shape fails in the reference). `info` is kept by default when the env holds one env
+(the reference always keeps it, :13-18, :34-39); pass `track_info=` to choose.
 
 Every compute call goes through libpmenv.so (include/pmenv.h); there is no CPU
 path. `features` must be a float32, contiguous tensor: it is written in place and
@@ -18,7 +28,7 @@ returned, exactly as trading_env.py:32,103 mutate the caller's tensor. A caller 
 keeps the reference's CPU tensors (train/on_policy.py:59-67 hands the env host
 tensors) may pass them unchanged: they are staged to the env's GPU and back (a PCIe
 round trip per call — the slow path; keep tensors on the GPU for throughput), and
-the reward and `.value` come back on the host as the reference returns them.
+the reward, `.value` and `.info` come back on the host with the reference's types.
 """
 import ctypes
 import weakref
@@ -26,7 +36,7 @@ import weakref
 import torch
 
 from . import _abi
-from .config import EnvConfig
+from .config import EnvConfig, NUM_ASSETS, WINDOW_SIZE
 
 _CPU = torch.device("cpu")
 
@@ -88,21 +98,16 @@ class RingView:
 
 
 class TradingEnv:
-    def __init__(self, num_envs=1, num_assets=None, window=None, features=5, device=None,
-                 config=None, track_info=False, step_impl="auto", **overrides):
+    _DIMS = ("num_envs", "num_assets", "window", "features")
+
+    def __init__(self, num_envs=None, num_assets=None, window=None, features=None, device=None,
+                 config=None, track_info=None, step_impl="auto", **overrides):
         """step_impl: "auto" (per shape), "one_launch" (step_env_kernel, one workgroup per
         env), "flat" (step_flat_kernel, one launch over 16 KiB window tiles) or
-        "two_launch" (scalar-step kernel + window stream); see set_step_impl."""
-        if config is None:
-            kw = dict(num_envs=num_envs, features=features)
-            if num_assets is not None:
-                kw["num_assets"] = num_assets
-            if window is not None:
-                kw["window"] = window
-            kw.update(overrides)
-            config = EnvConfig(**kw)
-        self.cfg = config.validate()
-        self._lib = _abi.load()
+        "two_launch" (scalar-step kernel + window stream); see set_step_impl.
+        Dimensions left as None are bound by the first reset / step tensor (until then
+        the handle holds config/base.py's shape: one env, 32 assets, window 32, F = 5).
+        track_info: None keeps `info` when the env holds one env (the reference's case)."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -110,6 +115,32 @@ class TradingEnv:
             raise ValueError("pmenv runs on a GPU device only (no CPU fallback)")
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
+        self._lib = _abi.load()
+        given = dict(num_envs=num_envs, num_assets=num_assets, window=window, features=features)
+        if config is None:
+            self._free = {k for k, v in given.items() if v is None}     # bound by the first tensor
+            self._overrides = dict(overrides)
+            config = self._config(dict(num_envs=1, num_assets=NUM_ASSETS, window=WINDOW_SIZE, features=5))
+        else:
+            self._free = set()
+        self._given = given
+        self._track_info_arg = track_info
+        self.step_impl = step_impl
+        self._h = None
+        self._build(config)
+
+    def _config(self, dims):
+        """EnvConfig of the given dims with the constructor's explicit values and overrides;
+        a close channel not given is the OHLC close (3), or the last market channel below F = 5."""
+        kw = {k: (self._given[k] if self._given[k] is not None else dims[k]) for k in self._DIMS}
+        kw.update(self._overrides)
+        if "close_channel" not in self._overrides:
+            kw["close_channel"] = min(3, kw["features"] - 2)
+        return EnvConfig(**kw)
+
+    def _build(self, config):
+        """Create the handle (and its state views) for `config`."""
+        self.cfg = config.validate()
         self._c = self.cfg.to_c()
         nbytes = self._lib.pmenv_state_bytes_for(ctypes.byref(self._c))
         if nbytes == 0:
@@ -137,9 +168,10 @@ class TradingEnv:
         self.weights = RingView(self)
         self._obs_shape = (B, N, W, self.cfg.features)
         self._args = _abi.PmenvStepArgs()          # reused: every field is set on every step
-        self.track_info = track_info
-        self._unbatched = False
-        self._host_io = False               # the last reset/step came with CPU tensors
+        self.track_info = (B == 1) if self._track_info_arg is None else bool(self._track_info_arg)
+        # the last reset/step came unbatched / with CPU tensors; a TradingEnv() whose shape
+        # the first call binds looks like the reference's (host, one env) until then
+        self._unbatched = self._host_io = bool(self._free) and B == 1
         # caller edits between steps (trading_env.py:102-105: the features are the caller's):
         # the version counters of the state blob (shared by .value and every other view)
         # and of the last in-place window, as this wrapper left them; a change tells the
@@ -147,24 +179,91 @@ class TradingEnv:
         self._state_ver = _version(self._state)
         self._win = None
         self._win_ver = -1
-        self.set_step_impl(step_impl)
-        self.info = None
+        self.set_step_impl(self.step_impl)
         self._reset_info()
+
+    def _fit(self, features):
+        """Bind the dimensions the constructor left open to the first tensor the env sees
+        (trading_env.py sizes nothing itself: config/base.py and the data pool do)."""
+        if not self._free:
+            return
+        shape = tuple(features.shape)
+        if len(shape) == 4:
+            dims = dict(zip(self._DIMS, shape))
+        elif len(shape) == 3:
+            dims = dict(zip(self._DIMS[1:], shape), num_envs=1)
+        else:
+            raise ValueError(f"features must be [N, W, F] or [B, N, W, F], got {shape}")
+        self._free = set()
+        cfg = self._config(dims)
+        if tuple(getattr(cfg, k) for k in self._DIMS) != tuple(getattr(self.cfg, k) for k in self._DIMS) or \
+                cfg.close_channel != self.cfg.close_channel:
+            self.close()
+            self._build(cfg)
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _reset_info(self):
+        """trading_env.py:13-18 / :34-39 (dict order is relied on by util/plot.py:61). With
+        host I/O and one env the entries have the reference's types: the seed entries are
+        Python 0s, INITIAL_CASH and the all-cash get_last() tensor; each step appends the
+        value as a 0-dim tensor (:80) and w', the return and the reward as numpy arrays
+        (:85, :90, :100; value and return in f64, the precision the env computes in)."""
+        self._info = None
+        self._pending = []
         if not self.track_info:
-            self.info = None
             return
         B, N = self.cfg.num_envs, self.cfg.num_assets
-        e0 = torch.zeros(B, N, device=self.device)
+        if self._host_io and self._unbatched:
+            e0 = torch.zeros(N)
+            e0[0] = 1
+            ic = self.cfg.init_cash
+            self._info = {"values": [int(ic) if float(ic).is_integer() else ic], "actions": [e0],
+                          "rewards": [0], "returns": [0]}
+            return
+        dev = _CPU if self._host_io else self.device
+        e0 = torch.zeros(B, N, device=dev)
         e0[:, 0] = 1
-        # trading_env.py:13-18 / :34-39 (dict order is relied on by util/plot.py:61)
-        self.info = {"values": [self._value.clone()], "actions": [e0], "rewards": [torch.zeros(B, device=self.device)],
-                     "returns": [torch.zeros(B, device=self.device, dtype=torch.float64)]}
+        self._info = {"values": [self._value.to(dev, copy=True)], "actions": [e0],
+                      "rewards": [torch.zeros(B, device=dev)],
+                      "returns": [torch.zeros(B, device=dev, dtype=torch.float64)]}
+
+    @property
+    def info(self):
+        """The reference's per-step history (values, actions, rewards, returns), or None when
+        not tracked. Host-I/O records are copied to the host when `info` is read (one copy
+        per array for all steps since the last read), not on every step."""
+        if self._info is None:
+            return None
+        if self._pending:
+            self._flush_info()
+        return self._info
+
+    @info.setter
+    def info(self, value):
+        self._pending = []
+        self._info = value
+
+    def _flush_info(self):
+        pend, self._pending = self._pending, []
+        vals = torch.stack([p[0] for p in pend]).cpu()
+        acts = torch.stack([p[1] for p in pend]).cpu().numpy()
+        rets = torch.stack([p[2] for p in pend]).cpu().numpy()
+        rews = torch.stack([p[3] for p in pend]).cpu().numpy()
+        inf = self._info
+        for i in range(len(pend)):
+            if self._unbatched:
+                inf["values"].append(vals[i, 0])
+                inf["actions"].append(acts[i, 0])
+                inf["returns"].append(rets[i, 0, ...])        # 0-dim arrays, as .cpu().numpy()
+                inf["rewards"].append(rews[i, 0, ...])
+            else:
+                inf["values"].append(vals[i])
+                inf["actions"].append(acts[i])
+                inf["returns"].append(rets[i])
+                inf["rewards"].append(rews[i])
 
     def _obs_check(self, features, name="features"):
         cfg = self.cfg
@@ -219,6 +318,7 @@ class TradingEnv:
         unb = False
         dev_features = features
         if features is not None:
+            self._fit(features)
             unb = self._obs_check(features)
             self._unbatched = unb
             self._host_io = features.device.type == "cpu"
@@ -259,22 +359,33 @@ class TradingEnv:
         weights_out            : a float32 [B, N] GPU tensor that receives the
                                  post-drift weights w' (info["actions"], :83-85)
         Returns (r, features); r is f32 [B] (0-dim for unbatched single-env input).
+
+        Caller edits between fused in-place steps are honoured (the reference keeps no copy
+        of the features): the wrapper compares torch's version counters of the window and
+        of the state before each step. Writes those counters miss — `.data`, DLPack, raw
+        kernels, or edits between replays of a captured hipGraph, where this check ran
+        once at capture — must be announced with window_written(features) /
+        state_written(), or the next flat step composes tile seams from stale copies.
         """
-        cfg = self.cfg
-        B, N = cfg.num_envs, cfg.num_assets
+        self._fit(features)
         unb = self._obs_check(features)
-        host = features.device.type == "cpu"
-        if out is not None and (out.device.type == "cpu") != host:
-            raise ValueError("out must live where features does")
-        if host:                                   # the reference's CPU tensors: staged through the GPU
-            r, res = self.step(action, features.to(self.device), prices=prices, bar=bar,
-                               out=None if out is None else torch.empty(out.shape, dtype=out.dtype,
-                                                                        device=self.device),
-                               series=series, day=day, weights_out=weights_out)
+        if features.device.type == "cpu":           # the reference's CPU tensors: staged through the GPU
+            if out is not None and out.device.type != "cpu":
+                raise ValueError("out must live where features does")
+            dev_out = None if out is None else torch.empty(out.shape, dtype=out.dtype, device=self.device)
+            r, res = self._step(action, features.to(self.device), prices, bar, dev_out, series, day,
+                                weights_out, unb, host=True)
             (features if out is None else out).copy_(res)
             self._host_io = True
             return r.cpu(), (features if out is None else out)
+        if out is not None and out.device.type == "cpu":
+            raise ValueError("out must live where features does")
         self._host_io = False
+        return self._step(action, features, prices, bar, out, series, day, weights_out, unb, host=False)
+
+    def _step(self, action, features, prices, bar, out, series, day, weights_out, unb, host):
+        cfg = self.cfg
+        B, N = cfg.num_envs, cfg.num_assets
         a = self._vec(action, N, "action")
         p = self._vec(prices, N, "prices") if prices is not None else None
         br = dy = None
@@ -320,7 +431,8 @@ class TradingEnv:
                     weights_out.device != self.device or weights_out.numel() != B * N:
                 raise ValueError(f"weights_out must be a contiguous float32 [{B}, {N}] tensor on {self.device}")
             args.weights = weights_out.data_ptr()
-        if self.track_info:
+        track = self.track_info and self._info is not None
+        if track:
             ret = torch.empty(B, dtype=torch.float64, device=self.device)
             args.ret = ret.data_ptr()
             if weights_out is None:
@@ -329,12 +441,16 @@ class TradingEnv:
         _abi.check(self._lib.pmenv_step_ex(self._h, ctypes.byref(args), stream), self._h, "pmenv_step")
         if out is None and br is not None:
             self._watch(features)
-        if self.track_info:
+        if track:
             # trading_env.py:80,85,90,100
-            self.info["values"].append(self._value.clone())
-            self.info["actions"].append(w if weights_out is None else weights_out.reshape(B, N).clone())
-            self.info["returns"].append(ret)
-            self.info["rewards"].append(r)
+            wv = w if weights_out is None else weights_out.reshape(B, N).clone()
+            if host:
+                self._pending.append((self._value.clone(), wv, ret, r))
+            else:
+                self._info["values"].append(self._value.clone())
+                self._info["actions"].append(wv)
+                self._info["returns"].append(ret)
+                self._info["rewards"].append(r)
         self._unbatched = unb
         return (r[0] if unb else r), (features if out is None else out)
 
@@ -355,6 +471,26 @@ class TradingEnv:
                                      self._win_ver is None or _version(window) != self._win_ver):
             _abi.check(self._lib.pmenv_window_written(self._h, _ptr(window), stream), self._h,
                        "pmenv_window_written")
+
+    def window_written(self, features):
+        """Announce that `features` — the window the next fused step advances in place — was
+        written in a way torch's version counter does not see: through `.data`, DLPack /
+        CuPy, a raw kernel on `data_ptr()`, or between replays of a captured hipGraph (the
+        wrapper's own check runs once, at capture). The next flat step re-reads its tile
+        halo from the window (pmenv_window_written)."""
+        self._obs_check(features)
+        if features.device.type == "cpu":
+            return
+        _abi.check(self._lib.pmenv_window_written(self._h, _ptr(features), self._stream()), self._h,
+                   "pmenv_window_written")
+        self._watch(features)
+
+    def state_written(self):
+        """Announce a write of the env state (value, ring, counters, statistics) that
+        bypassed torch's version counter (see window_written); the next flat step
+        re-reads its snapshot from the canonical state (pmenv_state_written)."""
+        _abi.check(self._lib.pmenv_state_written(self._h, self._stream()), self._h, "pmenv_state_written")
+        self._state_ver = _version(self._state)
 
     def advance(self, action, features, bar, prices=None, out=None):
         """Fused step: window advance + bar append (see step)."""

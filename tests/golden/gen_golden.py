@@ -53,9 +53,17 @@ def load_reference(W, N, commission=0.0):
     return mod.TradingEnv
 
 
+def close_channel(F):
+    """The close's channel: OHLC's 3 from F = 5 up, else the last market channel."""
+    return min(3, F - 2)
+
+
 def make_series(rng, N, D, F=5, sigma=0.01):
     """OHLC random walk [N, D, F] fp32; channel F-1 is a zero placeholder that
-    trading_env.py:103 overwrites with the weight history."""
+    trading_env.py:103 overwrites with the weight history. F = 5 is [open, high, low,
+    close, weight]; F > 5 adds indicator-like channels (the reference's pool carries
+    len(pool.features) channels, data/data_loader.py:48); F < 5 keeps [open, close][-F+1:]
+    with the close in close_channel(F)."""
     z = rng.standard_normal((N, D + 1, 4))
     close = np.empty((N, D + 1))
     close[:, 0] = 100.0 * np.exp(0.2 * rng.standard_normal(N))
@@ -67,7 +75,16 @@ def make_series(rng, N, D, F=5, sigma=0.01):
     h = np.maximum(o, c) * np.exp(np.abs(0.5 * sigma * z[:, 1:, 2]))
     lo = np.minimum(o, c) * np.exp(-np.abs(0.5 * sigma * z[:, 1:, 3]))
     s = np.zeros((N, D, F), np.float32)
-    s[:, :, 0], s[:, :, 1], s[:, :, 2], s[:, :, 3] = o, h, lo, c
+    if F >= 5:
+        s[:, :, 0], s[:, :, 1], s[:, :, 2], s[:, :, 3] = o, h, lo, c
+        for f in range(4, F - 1):                   # scaled indicator-like channels in [0, 1]
+            s[:, :, f] = rng.uniform(0.0, 1.0, (N, D))
+    elif F == 4:
+        s[:, :, 0], s[:, :, 1], s[:, :, 2] = o, h, c
+    elif F == 3:
+        s[:, :, 0], s[:, :, 1] = o, c
+    else:
+        s[:, :, 0] = c
     return s
 
 
@@ -92,18 +109,18 @@ def make_actions(rng, kind, T, N):
     return a
 
 
-def run_case(name, N, W, T, dtype, kind, resets=(), chan_steps=None, seed=0):
+def run_case(name, N, W, T, dtype, kind, resets=(), chan_steps=None, seed=0, F=5):
     import torch
     torch.set_default_dtype(torch.float64 if dtype == "f64" else torch.float32)
     tdt = torch.get_default_dtype()
     TradingEnv = load_reference(W, N)
     rng = np.random.default_rng(seed)
-    F = 5
+    cc = close_channel(F)
     series = make_series(rng, N, T + W, F)
     actions = make_actions(rng, kind, T, N)
     # instrument.py:79 divides float32 close tensors, so the relatives the env sees
     # are fp32-rounded even when the env itself runs in f64
-    close = series[:, :, 3]
+    close = series[:, :, cc]
     prices = np.zeros((T + 1, N), np.float64 if dtype == "f64" else np.float32)
     for i in range(1, T + 1):
         prices[i] = (close[:, i + W - 1] / close[:, i + W - 2]).astype(np.float32)
@@ -137,7 +154,7 @@ def run_case(name, N, W, T, dtype, kind, resets=(), chan_steps=None, seed=0):
             chans.append(obs[:, :, -1].numpy().astype(np.float64))
         # market channels are returned untouched (in-place write of channel F-1 only)
         assert np.array_equal(obs[:, :, :-1].numpy().astype(np.float32), series[:, i:i + W, :-1])
-    meta = dict(name=name, N=N, W=W, F=F, T=T, dtype=dtype, kind=kind, resets=list(resets),
+    meta = dict(name=name, N=N, W=W, F=F, close_channel=cc, T=T, dtype=dtype, kind=kind, resets=list(resets),
                 seed=seed, reference="zachramsey/pm-rl @ 2025-03-04 env/sim/trading_env.py",
                 torch=torch.__version__)
     np.savez_compressed(
@@ -210,6 +227,86 @@ def trainer_vectors():
     np.savez_compressed(os.path.join(OUT, "trainer_reward.npz"), **out)
 
 
+def driver_vectors(T_eval=40, T_roll=48, F=8, seed=77):
+    """train/on_policy.py's env call sequence, run on the reference env: `TradingEnv()` with
+    no arguments (:35, config/base.py's NUM_ASSETS / WINDOW_SIZE), then _evaluate(0)
+    (:76-90), _rollout (:56-67, recording what buffer.add receives: np.array(env.value)),
+    and _evaluate(1) — one env object throughout, as Metrics / Visualizer hold it
+    (:39-40). The windows carry F feature channels (len(pool.features), not 5), the agent's
+    actions are [N, 1] (simplex, with every 7th step mixed-sign to reach the normalisation
+    branch). After each phase the info lists are recorded as util/eval.py:14-37 and
+    util/plot.py:61,74-75 read them, plus each entry's type (trading_env.py:13-18, :80-100)."""
+    import torch
+    torch.set_default_dtype(torch.float32)
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import config.base as cb
+    N, W = cb.NUM_ASSETS, cb.WINDOW_SIZE             # the constructor's shape: config/base.py:28-29
+    TradingEnv = load_reference(W, N)
+    rng = np.random.default_rng(seed)
+    cc = close_channel(F)
+    test = make_series(rng, N, T_eval + W, F)
+    train = make_series(rng, N, T_roll + W, F)
+    out = {"test_series": test, "train_series": train}
+
+    def actions(T):
+        a = make_actions(rng, "simplex", T, N)
+        mixed = make_actions(rng, "mixed", T, N)
+        a[7::7] = mixed[7::7]
+        return a
+
+    def prices_of(series, T):
+        c = series[:, :, cc]
+        p = np.zeros((T + 1, N), np.float32)
+        for i in range(1, T + 1):
+            p[i] = c[:, i + W - 1] / c[:, i + W - 2]
+        return p
+
+    def tname(x):
+        return type(x).__name__ + ("" if not hasattr(x, "dtype") else ":" + str(x.dtype).replace("torch.", "")) + \
+            ("" if not hasattr(x, "shape") else ":" + "x".join(map(str, tuple(x.shape))))
+
+    env = TradingEnv()
+    out["init_info_types"] = np.array(json.dumps({k: [tname(x) for x in v] for k, v in env.info.items()}))
+    out["init_value"] = np.array(float(env.value))
+    for phase, series, T in (("eval0", test, T_eval), ("rollout", train, T_roll), ("eval1", test, T_eval)):
+        acts, prices = actions(T), prices_of(series, T)
+        rewards = np.full(T + 1, np.nan)
+        values = np.zeros(T + 1)
+        buf_v = np.full(T + 1, np.nan)
+        s = None
+        for step in range(T + 1):
+            data = torch.tensor(series[:, step:step + W, :])
+            if step == 0:
+                s = env.reset(data)
+                assert s is data
+            else:
+                a = torch.tensor(acts[step]).reshape(N, 1)
+                r, s_ = env.step(a, data, torch.tensor(prices[step]))
+                assert s_ is data
+                rewards[step] = float(r)
+                if phase == "rollout":
+                    buf_v[step] = float(np.array(env.value))     # RolloutBuffer.add: np.array(v)
+                s = s_
+            values[step] = float(env.value)
+        info = env.info
+        assert list(info.keys()) == ["values", "actions", "rewards", "returns"]
+        out[f"{phase}_actions_in"], out[f"{phase}_prices"] = acts, prices
+        out[f"{phase}_rewards"], out[f"{phase}_values"], out[f"{phase}_buffer_value"] = rewards, values, buf_v
+        out[f"{phase}_info_values"] = np.array([float(x) for x in info["values"]])
+        out[f"{phase}_info_actions"] = np.array(info["actions"], dtype=np.float64)   # eval.py:33
+        out[f"{phase}_info_rewards"] = np.array([float(x) for x in info["rewards"]])
+        out[f"{phase}_info_returns"] = np.array([float(x) for x in info["returns"]])
+        out[f"{phase}_info_types"] = np.array(json.dumps({k: [tname(x) for x in v[:2]] for k, v in info.items()}))
+        out[f"{phase}_chan"] = s[:, :, -1].numpy().astype(np.float64)
+        assert np.array_equal(s[:, :, :-1].numpy(), series[:, T:T + W, :-1])
+    meta = dict(N=N, W=W, F=F, close_channel=cc, T_eval=T_eval, T_roll=T_roll, seed=seed, dtype="f32",
+                reference="zachramsey/pm-rl @ 2025-03-04 train/on_policy.py + env/sim/trading_env.py",
+                torch=torch.__version__)
+    out["meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(OUT, "onpolicy_driver.npz"), **out)
+
+
 CASES = [
     # name, N, W, T, dtype, kind, resets, chan_steps
     ("simplex_n5_w50_t64_f64", 5, 50, 64, "f64", "simplex", (), None),
@@ -229,15 +326,38 @@ CASES = [
     ("simplex_n129_w50_t16_f64", 129, 50, 16, "f64", "simplex", (), [0, 1, 16]),
 ]
 
+# F != 5: the reference's windows carry len(pool.features) channels (data/data_loader.py:48)
+FEAT_CASES = [
+    # name, N, W, T, dtype, kind, resets, chan_steps, F
+    ("feat12_n30_w50_t64_f64", 30, 50, 64, "f64", "simplex", (), [0, 1, 49, 50, 64], 12),
+    ("feat12_n30_w50_t64_f32", 30, 50, 64, "f32", "mixed", (), [0, 1, 49, 50, 64], 12),
+    ("feat3_n7_w10_t30_f32", 7, 10, 30, "f32", "mixed", (11,), None, 3),
+    ("feat8_n32_w32_t80_f64", 32, 32, 80, "f64", "simplex", (40,), [0, 1, 31, 32, 33, 40, 41, 80], 8),
+]
+
 
 def main():
-    for i, (name, N, W, T, dt, kind, resets, cs) in enumerate(CASES):
-        m = run_case(name, N, W, T, dt, kind, resets, cs, seed=1000 + i)
-        print("wrote", m["name"])
-    reward_module_vectors()
-    print("wrote reward_module")
-    trainer_vectors()
-    print("wrote trainer_reward")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma list: env (F = 5 cases), feat, driver, reward, trainer")
+    only = set(filter(None, ap.parse_args().only.split(","))) or {"env", "feat", "driver", "reward", "trainer"}
+    if "env" in only:
+        for i, (name, N, W, T, dt, kind, resets, cs) in enumerate(CASES):
+            m = run_case(name, N, W, T, dt, kind, resets, cs, seed=1000 + i)
+            print("wrote", m["name"])
+    if "feat" in only:
+        for i, (name, N, W, T, dt, kind, resets, cs, F) in enumerate(FEAT_CASES):
+            m = run_case(name, N, W, T, dt, kind, resets, cs, seed=2000 + i, F=F)
+            print("wrote", m["name"])
+    if "driver" in only:
+        driver_vectors()
+        print("wrote onpolicy_driver")
+    if "reward" in only:
+        reward_module_vectors()
+        print("wrote reward_module")
+    if "trainer" in only:
+        trainer_vectors()
+        print("wrote trainer_reward")
 
 
 if __name__ == "__main__":

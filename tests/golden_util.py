@@ -11,13 +11,29 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def cases():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not p.endswith(("reward_module.npz", "trainer_reward.npz")))
+                  if not p.endswith(("reward_module.npz", "trainer_reward.npz", "onpolicy_driver.npz")))
 
 
 def load(name):
     d = np.load(os.path.join(GOLDEN_DIR, name + ".npz"))
     g = {k: d[k] for k in d.files}
     g["meta"] = json.loads(str(g["meta"]))
+    return g
+
+
+def close_channel(g):
+    """The series' close channel (the F = 5 cases predate the meta field: OHLC's 3)."""
+    return g["meta"].get("close_channel", 3)
+
+
+def load_driver():
+    """tests/golden/onpolicy_driver.npz: train/on_policy.py's env call sequence on the
+    reference (gen_golden.driver_vectors)."""
+    d = np.load(os.path.join(GOLDEN_DIR, "onpolicy_driver.npz"))
+    g = {k: d[k] for k in d.files}
+    for k in list(g):
+        if k == "meta" or k.endswith("info_types"):
+            g[k] = json.loads(str(g[k]))
     return g
 
 

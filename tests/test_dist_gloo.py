@@ -163,3 +163,45 @@ def test_actor_critic_sharded_update_equals_unsharded():
             scale = max(float(g.abs().max()) for g in group)   # (the last bias's gradient is 0: a
             np.testing.assert_allclose(x, y.numpy(), rtol=1e-12, atol=1e-13 * scale,   # shift of every score)
                                        err_msg=f"rank {rank} tensor {i}")
+
+
+def _grads_worker(rank, world, port, root, q):
+    import sys
+    sys.path.insert(0, os.path.join(root, "pm-rl_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pmenv.parallel import allreduce_grads
+    torch.manual_seed(0)
+    a, b = torch.nn.Linear(3, 2).double(), torch.nn.Linear(3, 1).double()
+    x = torch.arange(6, dtype=torch.float64).reshape(2, 3) * (rank + 1)
+    # rank 0 uses both heads; rank 1 (say, a shard without envs of one kind) only the first:
+    # its second head's grads stay None
+    loss = a(x).sum() + (b(x).sum() if rank == 0 else 0.0)
+    loss.backward()
+    params = list(a.parameters()) + list(b.parameters())
+    total, n = allreduce_grads(params, loss.detach(), 2.0)
+    q.put((rank, total, n, [p.grad.clone().numpy() for p in params]))
+    dist.destroy_process_group()
+
+
+def test_allreduce_grads_aligns_buckets_when_a_rank_has_no_grad():
+    """A parameter without a gradient on one rank contributes zeros: the ranks' buckets keep
+    the same length and order (a mismatch would hang or mix gradients), and every rank ends
+    with the same averaged gradients."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grads_worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, t0, n0, g0), (_, t1, n1, g1) = res
+    assert n0 == n1 == 4.0 and t0 == t1
+    for x, y in zip(g0, g1):
+        assert np.array_equal(x, y)
+    # the second head's bias: rank 0's sum d/db = 2 rows, rank 1 none -> 2 / 4
+    assert np.allclose(g0[-1], [0.5])

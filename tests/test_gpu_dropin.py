@@ -1,0 +1,169 @@
+"""The reference's own training driver swaps pmenv's TradingEnv in unchanged.
+
+train/on_policy.py:35 builds `TradingEnv()` with no arguments, hands the same object to
+Metrics and Visualizer (:39-40), and drives it with the data loader's CPU tensors:
+_evaluate (:76-90), _rollout (:56-67, RolloutBuffer.add(s, a, np.array(env.value), r)),
+_evaluate again. Metrics reads env.info["returns" / "values" / "actions"]
+(util/eval.py:14-37) and Visualizer unpacks env.info.values() in order (util/plot.py:61,
+74-75). tests/golden/onpolicy_driver.npz records that sequence run on the reference
+itself with F = 8 feature channels (len(pool.features), data/data_loader.py:48) at
+config/base.py's NUM_ASSETS = WINDOW_SIZE = 32. Needs an MI355X.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+PHASES = (("eval0", "test_series", "T_eval"), ("rollout", "train_series", "T_roll"), ("eval1", "test_series", "T_eval"))
+# the reference stores the value and the return in the fp32 of its tensors; pmenv computes
+# them in f64 and keeps that precision (same container types and shapes)
+FLOAT_OK = {"float32", "float64"}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _tname(x):
+    kind = type(x).__name__
+    dt = str(x.dtype).replace("torch.", "") if hasattr(x, "dtype") else None
+    shape = "x".join(map(str, tuple(x.shape))) if hasattr(x, "shape") else None
+    return kind, dt, shape
+
+
+def _same_types(got, want):
+    """Entry types of one info list against the reference's ('int', 'Tensor:float32:32', ...)."""
+    assert len(got) >= len(want)
+    for x, w in zip(got, want):
+        parts = w.split(":")
+        kind, dt, shape = _tname(x)
+        assert kind == parts[0], (kind, w)
+        if len(parts) > 1:
+            assert dt == parts[1] or {dt, parts[1]} <= FLOAT_OK, (dt, w)
+            assert shape == parts[2], (shape, w)
+
+
+def test_gpu_onpolicy_driver_sequence_unchanged():
+    from pmenv import TradingEnv
+    g = gu.load_driver()
+    m = g["meta"]
+    N, W, F = m["N"], m["W"], m["F"]
+    env = TradingEnv()                                   # on_policy.py:35, no arguments
+    held = env                                           # Metrics(self.env, ...) / Visualizer(..., self.env, ...)
+    assert float(env.value) == g["init_value"]
+    _same_types([v[0] for v in env.info.values()], [t[0] for t in g["init_info_types"].values()])
+    for phase, skey, tkey in PHASES:
+        series, T = g[skey], m[tkey]
+        acts, prices = g[f"{phase}_actions_in"], g[f"{phase}_prices"]
+        rewards, values, buf_v = np.full(T + 1, np.nan), np.zeros(T + 1), np.full(T + 1, np.nan)
+        rew_tot = 0
+        s = None
+        for step in range(T + 1):                        # for step, (datetime, prices, data) in enumerate(dl)
+            data = torch.tensor(series[:, step:step + W, :])
+            if step == 0:
+                s = env.reset(data)
+                assert s is data
+            else:
+                a = torch.tensor(acts[step]).reshape(N, 1)          # agent.act(s): [N, 1]
+                r, s_ = env.step(a, data, torch.tensor(prices[step]))
+                assert s_ is data and r.dim() == 0 and r.device.type == "cpu"
+                rew_tot += r
+                rewards[step] = float(r)
+                if phase == "rollout":
+                    buf_v[step] = float(np.array(env.value))        # RolloutBuffer.add (rollout_buffer.py:55)
+                s = s_
+            values[step] = float(env.value)
+        assert env.cfg.features == F and env.cfg.num_assets == N and env.cfg.window == W
+        info = held.info
+        # util/plot.py:61 unpacks the dict in the reference's order; :74-75 np.array the lists
+        assert list(info.keys()) == ["values", "actions", "rewards", "returns"]
+        vals, wts, rews, rets = info.values()
+        for k, got in info.items():
+            _same_types(got[:2], g[f"{phase}_info_types"][k])
+        assert len(vals) == len(wts) == len(rews) == len(rets) == T + 1
+        # util/eval.py:14-30: DataFrames indexed by the last len(...) dates
+        dates = pd.date_range("2020-01-01", periods=T + 1, freq="D")
+        df_ret = pd.DataFrame(info["returns"], index=dates[-len(info["returns"]):])
+        df_val = pd.DataFrame(info["values"], index=dates[-len(info["values"]):])
+        weights = np.array(info["actions"])                          # eval.py:33
+        assert weights.shape == (T + 1, N)
+        # fp32 reference vs f64 pmenv (golden_util.tolerances for f32 cases)
+        np.testing.assert_allclose(df_val.to_numpy()[:, 0].astype(np.float64), g[f"{phase}_info_values"], rtol=2e-5)
+        np.testing.assert_allclose(df_ret.to_numpy()[:, 0].astype(np.float64), g[f"{phase}_info_returns"], rtol=2e-5)
+        np.testing.assert_allclose(np.array(rews, dtype=np.float64), g[f"{phase}_info_rewards"], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(weights, g[f"{phase}_info_actions"], rtol=1e-5, atol=2e-7)
+        np.testing.assert_allclose(rewards[1:], g[f"{phase}_rewards"][1:], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(values, g[f"{phase}_values"], rtol=2e-5)
+        if phase == "rollout":
+            np.testing.assert_allclose(buf_v[1:], g["rollout_buffer_value"][1:], rtol=2e-5)
+        # eval.py:32-37 average turnover and :50 the final value's format
+        turn = sum(np.sum(np.abs(weights[i] - weights[i - 1])) for i in range(1, len(weights))) / (len(weights) - 1)
+        wref = g[f"{phase}_info_actions"]
+        tref = sum(np.sum(np.abs(wref[i] - wref[i - 1])) for i in range(1, len(wref))) / (len(wref) - 1)
+        assert np.isclose(turn, tref, rtol=1e-5)
+        assert f"{info['values'][-1]:.2f}" == f"{g[f'{phase}_info_values'][-1]:.2f}"
+        np.testing.assert_allclose(s[:, :, -1].numpy(), g[f"{phase}_chan"], rtol=1e-5, atol=2e-7)
+        assert np.array_equal(s[:, :, :-1].numpy(), series[:, T:T + W, :-1])
+        assert np.isclose(float(rew_tot), np.nansum(g[f"{phase}_rewards"]), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", [n for n in gu.cases() if n.startswith("feat")])
+def test_gpu_feature_count_bound_by_first_reset(name):
+    """F != 5 windows through TradingEnv() with no arguments: the first reset binds N, W
+    and F (and the close channel), surface contract with host tensors, reference goldens."""
+    from pmenv import TradingEnv
+    from test_oracle_golden import compare
+    g = gu.load(name)
+    mt = g["meta"]
+    N, W, F, T = mt["N"], mt["W"], mt["F"], mt["T"]
+    env = TradingEnv()
+    out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
+           "wpost": np.full((T + 1, N), np.nan), "chans": {}, "market_ok": True}
+    for i in range(T + 1):
+        obs = torch.tensor(gu.window(g, i)[0])
+        if g["ops"][i]:
+            env.reset(obs)
+        else:
+            r, obs2 = env.step(torch.tensor(g["actions"][i]).reshape(N, 1), obs, torch.tensor(g["prices"][i]))
+            assert obs2 is obs
+            out["rewards"][i] = float(r)
+            out["rets"][i] = float(env.info["returns"][-1])
+            out["wpost"][i] = env.info["actions"][-1]
+        out["values"][i] = float(env.value)
+        out["chans"][i] = obs[:, :, -1].numpy()
+    assert (env.cfg.num_assets, env.cfg.window, env.cfg.features) == (N, W, F)
+    compare(g, out)
+
+
+def test_gpu_given_dims_are_checked_against_the_first_tensor():
+    """A dimension the constructor fixes is not rebound: a window of another shape raises
+    ValueError (as the reference's fixed-size ring fails on it)."""
+    from pmenv import TradingEnv
+    env = TradingEnv(num_assets=7)
+    with pytest.raises(ValueError):
+        env.reset(torch.zeros(5, 10, 3))
+    env = TradingEnv(num_assets=7)
+    env.reset(torch.zeros(7, 10, 3))
+    assert (env.cfg.num_assets, env.cfg.window, env.cfg.features, env.cfg.close_channel) == (7, 10, 3, 1)
+    with pytest.raises(ValueError):                      # bound now: a later window must match
+        env.step(torch.full((7, 1), 1 / 7), torch.zeros(7, 12, 3), torch.ones(7))
+
+
+def test_gpu_batched_shape_bound_by_first_device_window():
+    """TradingEnv(device=...) with a [B, N, W, F] device window binds B too; info is then
+    opt-in (not kept for B > 1 unless asked)."""
+    from pmenv import TradingEnv
+    env = TradingEnv(device="cuda:0")
+    obs = torch.rand(64, 30, 50, 5, device="cuda:0")
+    env.reset(obs)
+    assert env.num_envs == 64 and env.info is None
+    r, o = env.step(torch.full((64, 30), 1 / 30, device="cuda:0"), obs, torch.ones(64, 30, device="cuda:0"))
+    assert o is obs and r.shape == (64,)
+    torch.testing.assert_close(env.value, torch.full((64,), 25000.0, dtype=torch.float64, device="cuda:0"))

@@ -33,7 +33,8 @@ def replay_gpu(g, mode, host=False, impl="auto"):
     from pmenv import TradingEnv
     m = g["meta"]
     N, W, F, T = m["N"], m["W"], m["F"], m["T"]
-    env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True, step_impl=impl)
+    env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True, step_impl=impl,
+                     close_channel=gu.close_channel(g))
     _t = (lambda x, dtype=torch.float32: torch.as_tensor(np.ascontiguousarray(x), dtype=dtype)) if host else \
         globals()["_t"]
     out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
@@ -52,8 +53,12 @@ def replay_gpu(g, mode, host=False, impl="auto"):
                 out["market_ok"] &= np.array_equal(obs[..., :-1].cpu().numpy(), gu.window(g, i)[0, ..., :-1])
             assert obs2 is obs and r.dim() == 0 and r.device == obs.device
             out["rewards"][i] = float(r)
-            out["rets"][i] = float(env.info["returns"][-1][0])
-            out["wpost"][i] = env.info["actions"][-1][0].cpu().numpy()
+            if host:                   # the reference's entry types: 0-dim / [N] numpy arrays
+                out["rets"][i] = float(env.info["returns"][-1])
+                out["wpost"][i] = env.info["actions"][-1]
+            else:
+                out["rets"][i] = float(env.info["returns"][-1][0])
+                out["wpost"][i] = env.info["actions"][-1][0].cpu().numpy()
         out["values"][i] = float(env.value)
         out["chans"][i] = obs[:, :, -1].cpu().numpy()
     return out

@@ -12,7 +12,7 @@ from pmenv.config import EnvConfig
 def replay_oracle(g, mode):
     m = g["meta"]
     N, W, F, T = m["N"], m["W"], m["F"], m["T"]
-    env = OracleEnv(EnvConfig(num_envs=1, num_assets=N, window=W, features=F))
+    env = OracleEnv(EnvConfig(num_envs=1, num_assets=N, window=W, features=F, close_channel=gu.close_channel(g)))
     out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
            "wpost": np.full((T + 1, N), np.nan), "chans": {}, "market_ok": True}
     obs = None
@@ -56,6 +56,42 @@ def test_oracle_matches_reference(name, mode):
     out = replay_oracle(g, mode)
     assert out["market_ok"]
     compare(g, out)
+
+
+def test_golden_cases_cover_feature_counts():
+    """The reference's windows carry len(pool.features) channels (data/data_loader.py:48):
+    goldens exist for F != 5, below and above OHLC + weight."""
+    fs = {gu.load(n)["meta"]["F"] for n in gu.cases()}
+    assert {3, 5, 8, 12} <= fs
+
+
+PHASES = (("eval0", "test_series", "T_eval"), ("rollout", "train_series", "T_roll"), ("eval1", "test_series", "T_eval"))
+
+
+def test_oracle_matches_reference_driver_sequence():
+    """train/on_policy.py's call sequence (TradingEnv(), evaluate, rollout, evaluate: one env
+    object, resets between phases, F = 8 windows) replayed on the oracle."""
+    g = gu.load_driver()
+    m = g["meta"]
+    N, W, F = m["N"], m["W"], m["F"]
+    env = OracleEnv(EnvConfig(num_envs=1, num_assets=N, window=W, features=F, close_channel=m["close_channel"]))
+    for phase, skey, tkey in PHASES:
+        ser, T = g[skey], m[tkey]
+        rets, rews, vals = [0.0], [0.0], [env.value[0]]
+        for step in range(T + 1):
+            obs = np.ascontiguousarray(ser[None, :, step:step + W, :])
+            if step == 0:
+                env.reset(obs)
+                vals = [env.value[0]]
+            else:
+                r, ret, _ = env.step(g[f"{phase}_actions_in"][step], obs, prices=g[f"{phase}_prices"][step])
+                rews.append(r[0])
+                rets.append(ret[0])
+                vals.append(env.value[0])
+        np.testing.assert_allclose(vals, g[f"{phase}_info_values"], rtol=2e-5)
+        np.testing.assert_allclose(rets, g[f"{phase}_info_returns"], rtol=2e-5)
+        np.testing.assert_allclose(rews, g[f"{phase}_info_rewards"], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(obs[0, :, :, -1], g[f"{phase}_chan"], rtol=1e-5, atol=2e-7)
 
 
 def test_reference_reward_module():

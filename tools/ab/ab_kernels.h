@@ -204,4 +204,29 @@ __global__ __launch_bounds__(BLOCK) void advance_flat_direct_kernel(StepParams p
     }
 }
 
+// step_flat_kernel (csrc/step_flat.h) with the alternatives it was measured against:
+// per-direction cache policies (POL 3 nt loads only, 4 nt stores only, 5 sc0 nt, 6 sc1 nt,
+// 7 nt loads + sc1 nt stores) and XCD-contiguous tile ranges (XCD x takes workgroups
+// x, x + 8, ... as one contiguous range of tiles)
+template <int BLOCK, int V, int POL, bool OUT, bool XCD>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void step_flat_ab_kernel(StepParams p,
+                                                                                                 uint32_t qtot) {
+    constexpr int CPW = BLOCK * V, WAVES = BLOCK / 64;
+    constexpr int kAuxL = (POL == 1 || POL == 3 || POL == 7) ? 2 : POL == 5 ? 3 : POL == 6 ? 18 : 0;
+    constexpr int kAuxS = (POL == 1 || POL == 4) ? 2 : POL == 5 ? 3 : (POL == 6 || POL == 7) ? 18 : 0;
+    __shared__ f4 sh4[CPW + 2];
+    __shared__ f4 sh_bar[WAVES][64];
+    __shared__ float sh_wp[WAVES][64];
+    __shared__ int32_t sh_k[WAVES];
+    uint32_t tile = blockIdx.x;
+    if (XCD) {
+        const uint32_t G = gridDim.x, q = G >> 3, r = G & 7, x = tile & 7, i = tile >> 3;
+        tile = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+    }
+    flat_seq_enter<OUT>(p);
+    FlatTile<V> t;
+    flat1_load<BLOCK, V, kAuxL, OUT>(p, qtot, tile, t);
+    flat1_process<BLOCK, V, kAuxS, OUT>(p, qtot, tile, t, sh4, sh_bar, sh_wp, sh_k);
+}
+
 }  // namespace pmenv_dev

@@ -533,16 +533,16 @@ bool launch_flat1(const pmenv* h, const StepParams& p, unsigned grid, bool out, 
     if (key == 25604 && t->flat1_pol >= 3 && t->flat1_pol <= 7) {   // other cache policies
 #define PMENV_FLAT1_POLV(PV)                                                                      \
         if (t->flat1_pol == PV) {                                                                 \
-            if (out) step_flat_kernel<256, 4, PV, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);  \
-            else step_flat_kernel<256, 4, PV, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);     \
+            if (out) step_flat_ab_kernel<256, 4, PV, true, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);  \
+            else step_flat_ab_kernel<256, 4, PV, false, false><<<grid, 256, 0, stream>>>(p, h->flat_qtot);     \
         }
         PMENV_FLAT1_POLV(3) PMENV_FLAT1_POLV(4) PMENV_FLAT1_POLV(5) PMENV_FLAT1_POLV(6) PMENV_FLAT1_POLV(7)
 #undef PMENV_FLAT1_POLV
         return true;
     }
     if (key == 25604 && t->flat1_xcd) {
-        if (out) step_flat_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
-        else step_flat_kernel<256, 4, 1, false, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        if (out) step_flat_ab_kernel<256, 4, 1, true, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
+        else step_flat_ab_kernel<256, 4, 1, false, true><<<grid, 256, 0, stream>>>(p, h->flat_qtot);
         return true;
     }
     if (key == 51204) flat1_pad<512, 4>(h, p, grid, out, pol, pad, stream);

@@ -30,6 +30,9 @@ ap.add_argument("--path", default="auto", help="auto | one_launch | two_launch |
 ap.add_argument("--commission", type=float, default=0.0)
 ap.add_argument("--reward", default="log_returns")
 ap.add_argument("--out", action="store_true", help="double-buffered (obs -> obs_out)")
+ap.add_argument("--attribute", action="store_true",
+                help="synchronise after every step of the bits phase and name the build on stderr "
+                     "first (a fault is then reported against the build and step that raised it)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -117,12 +120,16 @@ kernels = [e.lib.pmenv_step_path(e.h).decode() for e in envs]
 # bits: the first 2 * W steps (past the ring wrap) from one reset, every build
 ref = None
 same = []
-for e in envs:
+for name, e in zip(names, envs):
+    if a.attribute:
+        print(f"# bits: {name} [{e.lib.pmenv_step_path(e.h).decode()}]", file=sys.stderr, flush=True)
     e.reset()
     rs = []
-    for _ in range(2 * W + 3):
+    for i in range(2 * W + 3):
         e.step()
         rs.append(e.rew.clone())
+        if a.attribute:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     got = (torch.stack(rs), e.obs.clone())
     if ref is None:
