@@ -117,13 +117,14 @@ class TradingEnv:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self._lib = _abi.load()
         given = dict(num_envs=num_envs, num_assets=num_assets, window=window, features=features)
+        self._given = given
         if config is None:
             self._free = {k for k, v in given.items() if v is None}     # bound by the first tensor
             self._overrides = dict(overrides)
             config = self._config(dict(num_envs=1, num_assets=NUM_ASSETS, window=WINDOW_SIZE, features=5))
         else:
             self._free = set()
-        self._given = given
+            self._overrides = {}
         self._track_info_arg = track_info
         self.step_impl = step_impl
         self._h = None

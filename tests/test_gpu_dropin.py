@@ -161,9 +161,9 @@ def test_gpu_batched_shape_bound_by_first_device_window():
     opt-in (not kept for B > 1 unless asked)."""
     from pmenv import TradingEnv
     env = TradingEnv(device="cuda:0")
-    obs = torch.rand(64, 30, 50, 5, device="cuda:0")
+    obs = torch.rand(64, 32, 50, 5, device="cuda:0")
     env.reset(obs)
     assert env.num_envs == 64 and env.info is None
-    r, o = env.step(torch.full((64, 30), 1 / 30, device="cuda:0"), obs, torch.ones(64, 30, device="cuda:0"))
+    r, o = env.step(torch.full((64, 32), 1 / 32, device="cuda:0"), obs, torch.ones(64, 32, device="cuda:0"))
     assert o is obs and r.shape == (64,)
     torch.testing.assert_close(env.value, torch.full((64,), 25000.0, dtype=torch.float64, device="cuda:0"))
