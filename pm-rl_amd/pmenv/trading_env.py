@@ -211,9 +211,15 @@ class TradingEnv:
         host I/O and one env the entries have the reference's types: the seed entries are
         Python 0s, INITIAL_CASH and the all-cash get_last() tensor; each step appends the
         value as a 0-dim tensor (:80) and w', the return and the reward as numpy arrays
-        (:85, :90, :100; value and return in f64, the precision the env computes in)."""
+        (:85, :90, :100; value and return in f64, the precision the env computes in).
+        The seed action is, in the reference, a VIEW of ring slot 0 (get_last() returns
+        `self.buffer[(idx - 1) % W]`, weight_buffer.py:28-30, and `.flatten()` of a 1-D
+        view is that view, :36): once the ring wraps it shows the w' last written there. The host-typed
+        seed entry follows it (refreshed from the device ring whenever `info` is read, and
+        frozen at the next reset, as the reference's reset swaps in a new buffer)."""
         self._info = None
         self._pending = []
+        self._slot0 = None
         if not self.track_info:
             return
         B, N = self.cfg.num_envs, self.cfg.num_assets
@@ -223,6 +229,8 @@ class TradingEnv:
             ic = self.cfg.init_cash
             self._info = {"values": [int(ic) if float(ic).is_integer() else ic], "actions": [e0],
                           "rewards": [0], "returns": [0]}
+            self._slot0 = e0
+            self._slot0_dirty = False
             return
         dev = _CPU if self._host_io else self.device
         e0 = torch.zeros(B, N, device=dev)
@@ -230,6 +238,12 @@ class TradingEnv:
         self._info = {"values": [self._value.to(dev, copy=True)], "actions": [e0],
                       "rewards": [torch.zeros(B, device=dev)],
                       "returns": [torch.zeros(B, device=dev, dtype=torch.float64)]}
+
+    def _sync_slot0(self):
+        """The host-typed seed action <- ring slot 0 of the env (the reference's alias)."""
+        if self._slot0 is not None and self._slot0_dirty:
+            self._slot0.copy_(self._ring[0, 0])
+            self._slot0_dirty = False
 
     @property
     def info(self):
@@ -240,11 +254,13 @@ class TradingEnv:
             return None
         if self._pending:
             self._flush_info()
+        self._sync_slot0()
         return self._info
 
     @info.setter
     def info(self, value):
         self._pending = []
+        self._slot0 = None
         self._info = value
 
     def _flush_info(self):
@@ -325,6 +341,8 @@ class TradingEnv:
             self._host_io = features.device.type == "cpu"
             if self._host_io:
                 dev_features = features.to(self.device)
+        if mask is None and self._info is not None:
+            _ = self.info                     # the old history, final (flushed, seed action frozen)
         m = None
         if mask is not None:
             m = torch.as_tensor(mask).to(self.device).reshape(-1).to(torch.uint8).contiguous()
@@ -447,6 +465,7 @@ class TradingEnv:
             wv = w if weights_out is None else weights_out.reshape(B, N).clone()
             if host:
                 self._pending.append((self._value.clone(), wv, ret, r))
+                self._slot0_dirty = True
             else:
                 self._info["values"].append(self._value.clone())
                 self._info["actions"].append(wv)
