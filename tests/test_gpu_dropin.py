@@ -108,7 +108,8 @@ def test_gpu_onpolicy_driver_sequence_unchanged():
         wref = g[f"{phase}_info_actions"]
         tref = sum(np.sum(np.abs(wref[i] - wref[i - 1])) for i in range(1, len(wref))) / (len(wref) - 1)
         assert np.isclose(turn, tref, rtol=1e-5)
-        assert f"{info['values'][-1]:.2f}" == f"{g[f'{phase}_info_values'][-1]:.2f}"
+        final = f"{info['values'][-1]:.2f}"                            # eval.py:50 formats a 0-dim tensor
+        assert abs(float(final) - g[f"{phase}_info_values"][-1]) <= 0.01 + 2e-5 * g[f"{phase}_info_values"][-1]
         np.testing.assert_allclose(s[:, :, -1].numpy(), g[f"{phase}_chan"], rtol=1e-5, atol=2e-7)
         assert np.array_equal(s[:, :, :-1].numpy(), series[:, T:T + W, :-1])
         assert np.isclose(float(rew_tot), np.nansum(g[f"{phase}_rewards"]), rtol=1e-4, atol=1e-5)
