@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-/* 2: pmenv_window_written / pmenv_state_written added; pmenv_cfg_default's ret_mode is
- *    PMENV_RET_GROSS (trading_env.py:88 for every reward kind; was AUTO in 1) */
+/* 2: pmenv_window_written / pmenv_state_written and PMENV_STEP_PATH_RELAY added;
+ *    pmenv_cfg_default's ret_mode is PMENV_RET_GROSS (trading_env.py:88 for every reward
+ *    kind; was AUTO in 1) */
 #define PMENV_ABI_VERSION 2
 
 /* Opaque HIP stream (identical to HIP's own typedef); NULL = default stream. */
@@ -220,12 +221,20 @@ const char* pmenv_step_path(const pmenv* h);
  * into a hipGraph on, the handle sequences its FLAT steps on the device (a small
  * flat_seq_kernel before each step_flat_kernel reads the parity and the snapshot's
  * validity from device memory, so graph replays and eager calls interleave freely;
- * pmenv_step_path then says "device-sequenced"). */
+ * pmenv_step_path then says "device-sequenced").
+ *
+ * RELAY forces step_relay_kernel: the two-launch path's scalar step and window stream in
+ * ONE launch — scalar workgroups (one run per env) relay w' and the counter to the stream
+ * tiles through epoch-tagged words in handle memory (F = 5, W >= 2, 16-B granular env
+ * windows, N <= 512; the same bits as TWO_LAUNCH). In place it keeps the tiles' halo from
+ * the previous step, under the same pmenv_window_written rule as FLAT. A RELAY step enqueued
+ * while `stream` is being captured runs as TWO_LAUNCH (its epoch is a host counter). */
 typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,
     PMENV_STEP_PATH_TWO_LAUNCH = 2,
-    PMENV_STEP_PATH_FLAT = 3
+    PMENV_STEP_PATH_FLAT = 3,
+    PMENV_STEP_PATH_RELAY = 4
 } pmenv_step_path_kind;
 int pmenv_set_step_path(pmenv* h, int32_t path);
 

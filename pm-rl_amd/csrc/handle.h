@@ -76,6 +76,24 @@ struct pmenv {
     bool device_seq;
     int32_t* seq;         // {D, C, V, pad, HOBS lo, HOBS hi} (step_flat.h)
     uint64_t snap_stride; // bytes between the two parities of the snapshot / halo
+    // one launch, scalar blocks relaying w' and the counter to the stream tiles (step_relay.h)
+    bool relay_ok;        // the shape fits step_relay_kernel
+    int relay_auto;       // PMENV_FUSE_* bits the automatic choice gives it
+    int relay;            // PMENV_FUSE_* bits: which windows take it now
+    int relay_kl, relay_ka;   // the scalar step's form: KL lanes per env, KA strided assets per lane (0: register)
+    int relay_epb;        // envs per scalar block
+    int relay_lead;       // tiles a scalar block goes ahead of the first tile that needs it
+    uint32_t relay_tiles, relay_scal;
+    void* relay_mem;      // role table | relay words | halo x 2
+    int32_t* relay_role;  // [relay_tiles + relay_scal]
+    uint64_t* relay_w;    // [B * N] {epoch, w'}
+    uint64_t* relay_k;    // [B] {epoch, counter before the step}
+    float* relay_halo[2]; // in place: [relay_tiles - 1][2] float4 per parity
+    int relay_par;        // parity of the halo the next relay step reads
+    const float* relay_obs;   // the window whose halo relay_halo[relay_par] holds (null: none)
+    uint32_t relay_epoch; // the last step's tag
+    bool relay_captured;  // a step / reset / state write of this handle was captured into a hipGraph:
+                          // replays write behind the host's back, so relay steps run as two launches
     int path;             // pmenv_step_path_kind
     void* tools;          // tools build: its knob state (null in the product library)
     char err[512];

@@ -8,6 +8,7 @@
 #include "scalar_vec.h"
 #include "step_env.h"
 #include "step_flat.h"
+#include "step_relay.h"
 
 namespace pmenv_host {
 
@@ -216,6 +217,64 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
     h->par = 1 - q;
     h->snap_ok = true;
     h->halo1_obs = out ? nullptr : p.obs;
+}
+
+// ---------------------------------------------------------------- one launch, relayed (step_relay.h)
+template <int BLOCK, int POL, bool OUT>
+inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
+                           hipStream_t stream) {
+    const uint32_t q = h->flat_qtot;
+    switch (h->relay_kl * 100 + h->relay_ka) {
+    case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 3200: step_relay_kernel<BLOCK, 2, POL, OUT, 32, 0><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    }
+}
+
+// prime the in-place halo when the last relay step's halo is not this window's, tag the
+// step with the next epoch (the words restart at 0 if the counter wraps), one launch
+inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
+    const bool out = p.obs_out != p.obs;
+    const int q = h->relay_par;
+    const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
+    p.per4 = h->per4;
+    p.div_units = make_fastdiv(h->per4);
+    if (!out && h->relay_obs != p.obs) {
+        StepParams pp = p;
+        pp.halo = h->relay_halo[q];
+        pp.halo_wgs = h->relay_tiles > 0 ? h->relay_tiles - 1 : 0;
+        pp.halo_block = cpw;
+        pp.halo_qtot = h->flat_qtot;
+        const unsigned g = (pp.halo_wgs + 255) / 256 < 2048 ? (pp.halo_wgs + 255) / 256 + 1 : 2048;
+        relay_prime_halo_kernel<<<g, 256, 0, stream>>>(pp);
+    }
+    if (++h->relay_epoch == 0) {
+        const size_t words = ((size_t)h->cfg.num_envs * h->cfg.num_assets + h->cfg.num_envs) * 8;
+        if (hipMemsetAsync(h->relay_w, 0, words, stream) != hipSuccess) return PMENV_ERR_HIP;
+        h->relay_epoch = 1;
+    }
+    RelayParams r;
+    r.role = h->relay_role;
+    r.w = h->relay_w;
+    r.k = h->relay_k;
+    r.halo_in = h->relay_halo[q];
+    r.halo_out = h->relay_halo[1 - q];
+    r.epoch = h->relay_epoch;
+    const unsigned grid = h->relay_tiles + h->relay_scal;
+    if (h->flat_ip_block == 256) {
+        if (out) launch_relay_g<256, 0, true>(h, p, r, grid, stream);
+        else launch_relay_g<256, 0, false>(h, p, r, grid, stream);
+    } else {
+        if (out) launch_relay_g<512, 1, true>(h, p, r, grid, stream);
+        else launch_relay_g<512, 1, false>(h, p, r, grid, stream);
+    }
+    if (!out) h->relay_par = 1 - q;
+    h->relay_obs = out ? nullptr : p.obs;
+    return PMENV_OK;
 }
 
 }  // namespace pmenv_host

@@ -75,9 +75,19 @@ bool capturing(hipStream_t stream) {
 // where host flags set once at capture time would let replay 2 on read the snapshot the
 // previous replay left (flat_seq_kernel then re-primes from the reset state).
 enum { kInvalSnap = 1, kInvalHalo = 2 };
-int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInvalHalo, bool host_only = false) {
+// The relay step keeps its in-place halo by a host flag: once anything of this handle is
+// captured into a hipGraph, replays may write the window or the state where the host does not
+// see it, so from then on its relay steps run as two launches.
+void note_capture(pmenv* h, hipStream_t stream) {
+    if (h->relay && !h->relay_captured && capturing(stream)) h->relay_captured = true;
+}
+
+int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInvalHalo, bool host_only = false,
+                     bool keep_relay = false) {
     if (what & kInvalSnap) h->snap_ok = false;
     h->halo1_obs = nullptr;
+    if (!keep_relay) h->relay_obs = nullptr;   // the relay step's halo
+    if (!host_only) note_capture(h, stream);
     if (host_only || !h->flat1_ok) return PMENV_OK;
     if (!h->device_seq && h->flat1 && capturing(stream)) h->device_seq = true;
     if (!h->device_seq) return PMENV_OK;
@@ -96,7 +106,13 @@ int one_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_ONE_LAUNCH) return h->one_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
     if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming ? 0 : -1;
     if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? 0 : -1;
+    if (path == PMENV_STEP_PATH_RELAY) return h->relay_ok ? 0 : -1;
     return h->one_auto;
+}
+int relay_bits(const pmenv* h, int path) {
+    if (path == PMENV_STEP_PATH_RELAY) return h->relay_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
+    if (path == PMENV_STEP_PATH_AUTO) return h->relay_auto;
+    return 0;
 }
 int flat1_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
@@ -181,6 +197,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         if (h->state && h->owns_state) (void)hipFree(h->state);
         if (h->halo) (void)hipFree(h->halo);
         if (h->snap) (void)hipFree(h->snap);
+        if (h->relay_mem) (void)hipFree(h->relay_mem);
         free(h);
         return code;
     };
@@ -336,6 +353,21 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
     }
 
+    // ---- the relayed one-launch step (step_relay_kernel): the flat stream's shapes (F = 5,
+    // W >= 2, 16-B granular env windows) with the two-launch path's scalar step forms
+    // (N <= 512, the packed forms' [B*N] descriptors under 2^32 bytes), the stream's tile
+    // geometry; at most BLOCK rows per tile (4 * 2 <= W * F). Forced only (RELAY) until
+    // measured against the other paths.
+    {
+        const int N = c.num_assets;
+        const int kv = h->k1_vec >= kK1Str ? h->k1_vec - kK1Str : h->k1_vec;
+        h->relay_ok = h->flat_ok && c.window >= 2 && N <= 512 && (N <= 64 || h->k1_vec != 0);
+        h->relay_kl = kv ? kv / 100 : (N <= 32 ? 32 : 64);
+        h->relay_ka = kv ? kv % 100 : 0;
+        h->relay_epb = (h->flat_ip_block / 64) * (64 / h->relay_kl);
+        h->relay_lead = 1024;
+        h->relay_auto = 0;
+    }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
@@ -344,6 +376,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->path = PMENV_STEP_PATH_AUTO;
     h->one = h->one_auto;
     h->flat1 = h->flat1_auto;
+    h->relay = h->relay_ok ? h->relay_auto : 0;
 
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
@@ -419,6 +452,52 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
             return fail(PMENV_ERR_HIP);
         }
     }
+    if (h->relay_ok) {
+        // the role table (scalar block s placed `lead` tiles ahead of the first tile that needs
+        // env s * EPB), the relay words (zero: no epoch yet) and the in-place halo's two parities
+        const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
+        const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
+        h->relay_tiles = (h->flat_qtot + cpw - 1) / cpw;
+        h->relay_scal = (uint32_t)((B + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
+        const size_t nrole = (size_t)h->relay_tiles + h->relay_scal;
+        auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
+        const size_t role_b = up16(nrole * 4), words_b = (BN + B) * 8;
+        const size_t hal = up16((size_t)h->relay_tiles * 32);
+        hipError_t ae = hipMalloc(&h->relay_mem, role_b + up16(words_b) + 2 * hal);
+        if (ae != hipSuccess) {
+            set_err(h, "hipMalloc(relay) failed: %s", hipGetErrorString(ae));
+            h->relay_mem = nullptr;
+            return fail(PMENV_ERR_HIP);
+        }
+        char* m = (char*)h->relay_mem;
+        h->relay_role = (int32_t*)m;
+        h->relay_w = (uint64_t*)(m + role_b);
+        h->relay_k = h->relay_w + BN;
+        h->relay_halo[0] = (float*)(m + role_b + up16(words_b));
+        h->relay_halo[1] = (float*)(m + role_b + up16(words_b) + hal);
+        int32_t* role = (int32_t*)malloc(nrole * 4);
+        if (!role) { set_err(h, "relay role table: out of host memory"); return fail(PMENV_ERR_ARG); }
+        size_t at = 0;
+        uint32_t s = 0;
+        const uint64_t per4 = h->per4, epb = (uint64_t)h->relay_epb;
+        for (uint32_t t = 0; t < h->relay_tiles; ++t) {
+            // the first tile holding a chunk of env s * EPB
+            while (s < h->relay_scal && (uint64_t)s * epb * per4 / cpw <= (uint64_t)t + (uint64_t)h->relay_lead)
+                role[at++] = -(int32_t)(s++) - 1;
+            role[at++] = (int32_t)t;
+        }
+        while (s < h->relay_scal) role[at++] = -(int32_t)(s++) - 1;
+        ae = hipMemcpy(h->relay_role, role, nrole * 4, hipMemcpyHostToDevice);
+        free(role);
+        if (ae == hipSuccess) ae = hipMemset(h->relay_w, 0, words_b);
+        if (ae != hipSuccess) {
+            set_err(h, "relay tables: %s", hipGetErrorString(ae));
+            return fail(PMENV_ERR_HIP);
+        }
+        h->relay_epoch = 0;
+        h->relay_par = 0;
+        h->relay_obs = nullptr;
+    }
     (void)flat1_invalidate(h, nullptr, kInvalSnap | kInvalHalo, true);   // no device sequencing yet
     char* base = (char*)h->state;
     h->value = (double*)(base + off[0]);
@@ -461,27 +540,31 @@ int pmenv_destroy(pmenv* h) {
     if (h->state && h->owns_state) (void)hipFree(h->state);
     if (h->halo) (void)hipFree(h->halo);
     if (h->snap) (void)hipFree(h->snap);
+    if (h->relay_mem) (void)hipFree(h->relay_mem);
     free(h);
     return PMENV_OK;
 }
 
 int pmenv_set_step_path(pmenv* h, int32_t path) {
     if (!h) return PMENV_ERR_ARG;
-    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_FLAT) {
+    if (path < PMENV_STEP_PATH_AUTO || path > PMENV_STEP_PATH_RELAY) {
         set_err(h, "unknown step path %d", path);
         return PMENV_ERR_ARG;
     }
     const int bits = one_bits(h, path);
     const int fbits = flat1_bits(h, path);
-    if (bits < 0 || fbits < 0) {
+    const int rbits = relay_bits(h, path);
+    if (bits < 0 || fbits < 0 || rbits < 0) {
         set_err(h, "step path %d does not fit this shape (one launch: F = 5, W >= 2, N <= 64, window <= 64 KiB "
                    "of LDS; two launches: F = 5, 16-B granular env windows; flat: F = 5, W >= 2, N <= 64, "
-                   "16-B granular env windows of >= 148 chunks, N > 64 up to 512 with W >= 14)", path);
+                   "16-B granular env windows of >= 148 chunks, N > 64 up to 512 with W >= 14; relay: F = 5, "
+                   "W >= 2, 16-B granular env windows, N <= 512)", path);
         return PMENV_ERR_ARG;
     }
     h->path = path;
     h->one = bits;
     h->flat1 = fbits;
+    h->relay = rbits;
     return PMENV_OK;
 }
 
@@ -534,8 +617,22 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         // a step captured into a hipGraph replays with frozen arguments: from then on this
         // handle sequences its flat steps on the device (flat_seq_kernel + the kernel)
         if (!h->device_seq && capturing(stream)) h->device_seq = true;
+        h->relay_obs = nullptr;
+        note_capture(h, stream);
         launch_flat1(h, p, stream);
         return check_launch(h, "step_flat_kernel");
+    }
+    if (a->bar && h->streaming && obs16 && (h->relay & fuse_bit) && !h->relay_captured && !capturing(stream)) {
+        // one launch, the scalar blocks relaying to the stream tiles (a captured step runs as
+        // two launches: the relay epoch is a host counter; note_capture marks the handle)
+        const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
+        if (const int rc = flat1_invalidate(h, stream, kInvalSnap | kInvalHalo, false, true)) return rc;
+        if (launch_relay(h, p, stream) != PMENV_OK) {
+            set_err(h, "relay step: hipMemsetAsync failed");
+            return PMENV_ERR_HIP;
+        }
+        return check_launch(h, "step_relay_kernel");
     }
     if (const int rc = flat1_invalidate(h, stream)) return rc;   // every other path skips the snapshot
     if (!a->bar) {
@@ -595,7 +692,8 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-        if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
+        if ((h->relay & bit) && !h->relay_captured) part[m] = "step_relay_kernel";
+        else if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
         else if (h->one & bit) part[m] = "step_env_kernel";
         else {
             snprintf(buf[m], sizeof buf[m], "%s+%s", k1, m ? ip2 : db2);

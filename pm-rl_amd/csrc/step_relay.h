@@ -1,0 +1,175 @@
+// step_relay.h — the advance step in ONE launch whose scalar steps run once per env, in
+// dedicated workgroups, and reach the window-stream tiles through relay words.
+//
+// The two-launch step (scalar-step kernel, then the flat window stream) pays a kernel
+// boundary: the stream cannot start before the last env's scalar step has ended. The flat
+// one-launch step (step_flat.h) removes the boundary but runs the scalar step inside every
+// tile an env straddles, which lengthens every tile's life. Here one launch carries both
+// roles, interleaved in dispatch order by a host-built role table:
+//   * a scalar block runs the two-launch path's own scalar step (the same code, so the same
+//     bits) for its envs and relays each lane's w' and the env's counter as 64-bit words
+//     {epoch, payload} — agent-scope relaxed atomic stores, coherent across the XCDs' L2s
+//     without an L2 write-back fence — then writes the state (scalar_tail);
+//   * a tile streams its 16-B chunks of the flat window exactly as the in-place stream does
+//     (the two-level compose of flat_wg_body_patch), staging its rows' bar, w' and counter
+//     from the relay words; a word whose epoch is not this step's is not yet written, and
+//     the lane re-reads it (s_sleep between tries). Each word validates itself, so no flag
+//     and no ordering between words is needed (the pattern rocPRIM's look-back scan state
+//     uses on gfx942 / gfx950: atomic loads / stores that bypass the non-coherent L2).
+// A tile only ever waits for scalar blocks placed before it in the role table (dispatched
+// earlier, and those never wait), so every wait ends. The scalar blocks go `lead` tiles
+// ahead of the first tile that needs them.
+//
+// In place, the two chunks past a tile belong to the next tile, which may already have
+// stored them: they come from a halo the next tile wrote in the previous step (its first
+// two output chunks, parity-buffered like step_flat_kernel's), primed from the window by
+// the host when anything else wrote it. Double-buffered tiles read them from obs.
+//
+// Reference semantics as the two-launch path (env_step.h scalar_core / scalar_tail,
+// scalar_vec.h vec_*, compose2): env/sim/trading_env.py:54-105, weight_buffer.py:13-44,
+// data/instrument.py:79, :339-356.
+#pragma once
+#include "env_step.h"
+#include "scalar_vec.h"
+
+namespace pmenv_dev {
+
+struct RelayParams {
+    const int32_t* role;     // [tiles + scalar blocks]: >= 0 a tile index, < 0 -(scalar block + 1)
+    uint64_t* w;             // [B * N] {epoch, w' bits}
+    uint64_t* k;             // [B]     {epoch, counter before the step}
+    const float* halo_in;    // in place: [tiles - 1][2] float4, this step's input chunks past each tile
+    float* halo_out;         // in place: the same for the next step (written by the tiles)
+    uint32_t epoch;          // this step's tag (never 0: the words start zeroed)
+};
+
+__device__ __forceinline__ void relay_put(uint64_t* w, uint32_t epoch, uint32_t bits) {
+    __hip_atomic_store(w, ((uint64_t)epoch << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t relay_get(const uint64_t* w) {
+    return __hip_atomic_load(const_cast<uint64_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The scalar role: the two-launch path's scalar step for envs [s * EPB, (s + 1) * EPB).
+// KA = 0: the register form, KL lanes per env (scalar_step_reg_kernel); KA > 0: the packed
+// form, KL lanes x KA strided assets (scalar_step_vec_kernel<KL, KA, true>).
+template <int BLOCK, int KL, int KA>
+__device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayParams& r, int s) {
+    constexpr int EPW = 64 / KL, EPB = (BLOCK / 64) * EPW;
+    const int lane = threadIdx.x & 63;
+    const int b = s * EPB + (int)(threadIdx.x >> 6) * EPW + lane / KL;
+    const int j = lane % KL;
+    const int N = p.N;
+    const bool env_ok = b < p.B;
+    if constexpr (KA == 0) {
+        const ScalarIn in = scalar_load<KL>(p, b, lane);
+        const ScalarMid m = scalar_core<KL>(p, b, lane, in);
+        if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, r.epoch, __float_as_uint(m.wp));
+        if (env_ok && j == 0) relay_put(r.k + b, r.epoch, (uint32_t)m.k);
+        scalar_tail<KL>(p, b, lane, in, m);
+    } else {
+        const VecIn<KA> in = vec_load<KL, KA, true>(p, b, lane);
+        const VecMid<KA> m = vec_core<KL, KA, true>(p, b, lane, in);
+#pragma unroll
+        for (int e = 0; e < KA; ++e) {
+            const int n = j + e * KL;
+            if (env_ok && n < N) relay_put(r.w + (size_t)b * N + n, r.epoch, __float_as_uint(m.wp[e]));
+        }
+        if (env_ok && j == 0) relay_put(r.k + b, r.epoch, (uint32_t)in.k);
+        vec_tail<KL, KA, true>(p, b, lane, in, m);
+    }
+}
+
+// The tile role: flat_wg_body_patch's stream of tile t, its rows' w' and counter from the
+// relay words. OUT: double-buffered (the chunks past the tile read straight from obs).
+template <int BLOCK, int V, int POL, bool OUT>
+__device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
+                                           f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V, F = 5;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = t * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    f4 own[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    const uint32_t ntiles = (qtot + CPW - 1) / CPW;
+    const uint32_t nh = t + 1 < ntiles ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : r.halo_in + (size_t)t * 8;
+    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    __builtin_amdgcn_sched_barrier(0);
+    // the tile's rows g_lo .. g_hi (global row = b N + n): thread i stages row g_lo + i
+    const int N = p.N, W = p.W, WF = W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    const uint32_t b_lo = fdiv(c0, p.div_units);
+    const uint32_t g_lo = b_lo * (uint32_t)N + fdiv(4u * (c0 - b_lo * per4), p.div_wf);
+    const uint32_t ql = c0 + nblk - 1u;
+    const uint32_t b_hi = fdiv(ql, p.div_units);
+    const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
+    const bool mine = (uint32_t)tid <= g_hi - g_lo;
+    const uint32_t g = g_lo + (mine ? (uint32_t)tid : 0u);
+    const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
+    const float* barb = env_bar(p, (int)b);                         // null: a day outside the series
+    const float nanv = __int_as_float(0x7fc00000);
+    const f4 xb = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
+    uint64_t ww = relay_get(r.w + g), kw = relay_get(r.k + b);
+    bool ready = !mine || ((uint32_t)(ww >> 32) == r.epoch && (uint32_t)(kw >> 32) == r.epoch);
+    while (!__all(ready)) {                     // a scalar block placed before this tile is still running
+        __builtin_amdgcn_s_sleep(2);
+        if (!ready) {
+            ww = relay_get(r.w + g);
+            kw = relay_get(r.k + b);
+            ready = (uint32_t)(ww >> 32) == r.epoch && (uint32_t)(kw >> 32) == r.epoch;
+        }
+    }
+    if (mine) {
+        sh_bar[tid] = xb;
+        sh_wp[tid] = __uint_as_float((uint32_t)ww);
+        sh_kc[tid] = (int32_t)(uint32_t)kw;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
+    __syncthreads();
+    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
+    const bool first_out = !OUT && t > 0;                           // feeds the previous tile's halo
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
+        const uint32_t bq = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - bq * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const int kk = (int)(j0 - row * (uint32_t)WF);
+        const int i = (int)(bq * (uint32_t)N + row - g_lo);
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        const f4 o = compose2(p, kk, sh_kc[i], un, sh, [&](f4& x, float& xwp) {
+            x = sh_bar[i];
+            xwp = sh_wp[i];
+        });
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
+        if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;
+    }
+}
+
+// BLOCK x V tiles (the flat stream's 256 x 2 / 512 x 2), POL the window stream's cache
+// policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar)
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA>
+__global__ __launch_bounds__(BLOCK) void step_relay_kernel(StepParams p, RelayParams r, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    __shared__ f4 sh_bar[BLOCK];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    const int role = __builtin_amdgcn_readfirstlane(r.role[blockIdx.x]);
+    if (role < 0) relay_scalar<BLOCK, KL, KA>(p, r, -role - 1);
+    else relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, (uint32_t)role, sh4, sh_bar, sh_wp, sh_kc);
+}
+
+// in place: relay halo[i] = chunks (i + 1) * CPW and + 1 of the window (primed by the host
+// when the halo of the last relay step does not belong to this window)
+static __global__ __launch_bounds__(256) void relay_prime_halo_kernel(StepParams p) { copy_halo(p); }
+
+}  // namespace pmenv_dev

@@ -47,7 +47,7 @@ class PmenvStepArgs(ctypes.Structure):
 
 PHASE_SCALAR = 1
 PHASE_ADVANCE = 2
-STEP_PATHS = {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3}
+STEP_PATHS = {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3, "relay": 4}
 
 
 # (name, restype, argtypes) for every symbol include/pmenv.h declares

@@ -134,7 +134,7 @@ def test_step_path_kinds_match_the_header():
     hdr = open(os.path.join(ROOT, "include", "pmenv.h")).read()
     kinds = dict((m.group(1).lower(), int(m.group(2)))
                  for m in re.finditer(r"PMENV_STEP_PATH_(\w+) = (\d+)", hdr))
-    assert kinds == {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3}
+    assert kinds == {"auto": 0, "one_launch": 1, "two_launch": 2, "flat": 3, "relay": 4}
     assert _abi.STEP_PATHS == kinds
 
 
