@@ -87,9 +87,10 @@ struct pmenv {
     void* relay_mem;      // role table | relay words | halo x 2
     int32_t* relay_role;  // [relay_tiles + relay_scal]
     uint64_t* relay_w;    // [B * N] {epoch, w'}
-    uint64_t* relay_k;    // [B] {epoch, counter before the step}
+    int32_t* relay_kp[2]; // [B] per parity: the counter before the step (kp_in), after it (kp_out)
+    bool relay_kp_ok;     // relay_kp[relay_par] equals the state's counter
     float* relay_halo[2]; // in place: [relay_tiles - 1][2] float4 per parity
-    int relay_par;        // parity of the halo the next relay step reads
+    int relay_par;        // parity of the counter copy / halo the next relay step reads
     const float* relay_obs;   // the window whose halo relay_halo[relay_par] holds (null: none)
     uint32_t relay_epoch; // the last step's tag
     bool relay_captured;  // a step / reset / state write of this handle was captured into a hipGraph:

@@ -231,36 +231,39 @@ inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParam
     case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     }
 }
 
-// prime the in-place halo when the last relay step's halo is not this window's, tag the
-// step with the next epoch (the words restart at 0 if the counter wraps), one launch
+// prime the counter copy and the in-place halo when the previous relay step's do not hold,
+// tag the step with the next epoch (the words restart at 0 if the counter wraps), one launch
 inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     const bool out = p.obs_out != p.obs;
     const int q = h->relay_par;
     const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
-    if (!out && h->relay_obs != p.obs) {
+    const bool need_halo = !out && h->relay_obs != p.obs;
+    if (need_halo || !h->relay_kp_ok) {
         StepParams pp = p;
-        pp.halo = h->relay_halo[q];
+        pp.halo = need_halo ? h->relay_halo[q] : nullptr;
         pp.halo_wgs = h->relay_tiles > 0 ? h->relay_tiles - 1 : 0;
         pp.halo_block = cpw;
         pp.halo_qtot = h->flat_qtot;
-        const unsigned g = (pp.halo_wgs + 255) / 256 < 2048 ? (pp.halo_wgs + 255) / 256 + 1 : 2048;
-        relay_prime_halo_kernel<<<g, 256, 0, stream>>>(pp);
+        const uint32_t work = pp.halo_wgs > (uint32_t)h->cfg.num_envs ? pp.halo_wgs : (uint32_t)h->cfg.num_envs;
+        const unsigned g = work / 256 + 1 < 2048 ? work / 256 + 1 : 2048;
+        relay_prime_kernel<<<g, 256, 0, stream>>>(pp, h->relay_kp_ok ? nullptr : h->relay_kp[q]);
     }
     if (++h->relay_epoch == 0) {
-        const size_t words = ((size_t)h->cfg.num_envs * h->cfg.num_assets + h->cfg.num_envs) * 8;
+        const size_t words = (size_t)h->cfg.num_envs * h->cfg.num_assets * 8;
         if (hipMemsetAsync(h->relay_w, 0, words, stream) != hipSuccess) return PMENV_ERR_HIP;
         h->relay_epoch = 1;
     }
     RelayParams r;
     r.role = h->relay_role;
     r.w = h->relay_w;
-    r.k = h->relay_k;
+    r.kp_in = h->relay_kp[q];
+    r.kp_out = h->relay_kp[1 - q];
     r.halo_in = h->relay_halo[q];
     r.halo_out = h->relay_halo[1 - q];
     r.epoch = h->relay_epoch;
@@ -272,7 +275,10 @@ inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
         if (out) launch_relay_g<512, 1, true>(h, p, r, grid, stream);
         else launch_relay_g<512, 1, false>(h, p, r, grid, stream);
     }
-    if (!out) h->relay_par = 1 - q;
+    // every relay step flips the parity; the halo of the next parity belongs to this window
+    // only when this step ran in place (and wrote it)
+    h->relay_par = 1 - q;
+    h->relay_kp_ok = true;
     h->relay_obs = out ? nullptr : p.obs;
     return PMENV_OK;
 }

@@ -86,7 +86,10 @@ int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInva
                      bool keep_relay = false) {
     if (what & kInvalSnap) h->snap_ok = false;
     h->halo1_obs = nullptr;
-    if (!keep_relay) h->relay_obs = nullptr;   // the relay step's halo
+    if (!keep_relay) {                         // the relay step's halo and counter copy
+        h->relay_obs = nullptr;
+        if (what & kInvalSnap) h->relay_kp_ok = false;
+    }
     if (!host_only) note_capture(h, stream);
     if (host_only || !h->flat1_ok) return PMENV_OK;
     if (!h->device_seq && h->flat1 && capturing(stream)) h->device_seq = true;
@@ -461,9 +464,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->relay_scal = (uint32_t)((B + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
         const size_t nrole = (size_t)h->relay_tiles + h->relay_scal;
         auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
-        const size_t role_b = up16(nrole * 4), words_b = (BN + B) * 8;
+        const size_t role_b = up16(nrole * 4), words_b = BN * 8, kp_b = up16(B * 4);
         const size_t hal = up16((size_t)h->relay_tiles * 32);
-        hipError_t ae = hipMalloc(&h->relay_mem, role_b + up16(words_b) + 2 * hal);
+        hipError_t ae = hipMalloc(&h->relay_mem, role_b + up16(words_b) + 2 * kp_b + 2 * hal);
         if (ae != hipSuccess) {
             set_err(h, "hipMalloc(relay) failed: %s", hipGetErrorString(ae));
             h->relay_mem = nullptr;
@@ -472,9 +475,10 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         char* m = (char*)h->relay_mem;
         h->relay_role = (int32_t*)m;
         h->relay_w = (uint64_t*)(m + role_b);
-        h->relay_k = h->relay_w + BN;
-        h->relay_halo[0] = (float*)(m + role_b + up16(words_b));
-        h->relay_halo[1] = (float*)(m + role_b + up16(words_b) + hal);
+        h->relay_kp[0] = (int32_t*)(m + role_b + up16(words_b));
+        h->relay_kp[1] = (int32_t*)(m + role_b + up16(words_b) + kp_b);
+        h->relay_halo[0] = (float*)(m + role_b + up16(words_b) + 2 * kp_b);
+        h->relay_halo[1] = (float*)(m + role_b + up16(words_b) + 2 * kp_b + hal);
         int32_t* role = (int32_t*)malloc(nrole * 4);
         if (!role) { set_err(h, "relay role table: out of host memory"); return fail(PMENV_ERR_ARG); }
         size_t at = 0;
@@ -497,6 +501,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->relay_epoch = 0;
         h->relay_par = 0;
         h->relay_obs = nullptr;
+        h->relay_kp_ok = false;
     }
     (void)flat1_invalidate(h, nullptr, kInvalSnap | kInvalHalo, true);   // no device sequencing yet
     char* base = (char*)h->state;
@@ -617,7 +622,8 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         // a step captured into a hipGraph replays with frozen arguments: from then on this
         // handle sequences its flat steps on the device (flat_seq_kernel + the kernel)
         if (!h->device_seq && capturing(stream)) h->device_seq = true;
-        h->relay_obs = nullptr;
+        h->relay_obs = nullptr;                // the relay step's halo and counter copy go stale
+        h->relay_kp_ok = false;
         note_capture(h, stream);
         launch_flat1(h, p, stream);
         return check_launch(h, "step_flat_kernel");

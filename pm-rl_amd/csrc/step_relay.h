@@ -37,7 +37,8 @@ namespace pmenv_dev {
 struct RelayParams {
     const int32_t* role;     // [tiles + scalar blocks]: >= 0 a tile index, < 0 -(scalar block + 1)
     uint64_t* w;             // [B * N] {epoch, w' bits}
-    uint64_t* k;             // [B]     {epoch, counter before the step}
+    const int32_t* kp_in;    // [B] the counter before this step (parity p: written by the last relay step or primed)
+    int32_t* kp_out;         // [B] the counter after it (parity 1 - p: the next relay step's kp_in)
     const float* halo_in;    // in place: [tiles - 1][2] float4, this step's input chunks past each tile
     float* halo_out;         // in place: the same for the next step (written by the tiles)
     uint32_t epoch;          // this step's tag (never 0: the words start zeroed)
@@ -52,7 +53,9 @@ __device__ __forceinline__ uint64_t relay_get(const uint64_t* w) {
 
 // The scalar role: the two-launch path's scalar step for envs [s * EPB, (s + 1) * EPB).
 // KA = 0: the register form, KL lanes per env (scalar_step_reg_kernel); KA > 0: the packed
-// form, KL lanes x KA strided assets (scalar_step_vec_kernel<KL, KA, true>).
+// form, KL lanes x KA strided assets (scalar_step_vec_kernel<KL, KA, true>). Only w' goes
+// through the relay words; the counter of the next step goes to kp_out (read after this
+// launch has ended).
 template <int BLOCK, int KL, int KA>
 __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayParams& r, int s) {
     constexpr int EPW = 64 / KL, EPB = (BLOCK / 64) * EPW;
@@ -65,7 +68,7 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
         const ScalarIn in = scalar_load<KL>(p, b, lane);
         const ScalarMid m = scalar_core<KL>(p, b, lane, in);
         if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, r.epoch, __float_as_uint(m.wp));
-        if (env_ok && j == 0) relay_put(r.k + b, r.epoch, (uint32_t)m.k);
+        if (env_ok && j == 0) r.kp_out[b] = m.k + 1;
         scalar_tail<KL>(p, b, lane, in, m);
     } else {
         const VecIn<KA> in = vec_load<KL, KA, true>(p, b, lane);
@@ -75,13 +78,56 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
             const int n = j + e * KL;
             if (env_ok && n < N) relay_put(r.w + (size_t)b * N + n, r.epoch, __float_as_uint(m.wp[e]));
         }
-        if (env_ok && j == 0) relay_put(r.k + b, r.epoch, (uint32_t)in.k);
+        if (env_ok && j == 0) r.kp_out[b] = in.k + 1;
         vec_tail<KL, KA, true>(p, b, lane, in, m);
     }
 }
 
-// The tile role: flat_wg_body_patch's stream of tile t, its rows' w' and counter from the
-// relay words. OUT: double-buffered (the chunks past the tile read straight from obs).
+// compose2 (env_step.h) in two halves, the same selects element by element: the common
+// form with whether the chunk holds a row's last day or its ring slot (then it needs the
+// row's bar and w'), and the patch of those elements
+__device__ __forceinline__ f4 relay_common(const StepParams& p, int kk, int32_t k, const float (&un)[4],
+                                           const float (&sh)[4], bool& need) {
+    constexpr int F = 5;
+    const int W = p.W, WF = W * F;
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
+    const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+        o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
+    }
+    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
+    need = kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u);
+    return f4{o[0], o[1], o[2], o[3]};
+}
+
+__device__ __forceinline__ f4 relay_patch(const StepParams& p, int kk, int32_t k, f4 c, f4 xb, float xwp) {
+    constexpr int F = 5;
+    const int W = p.W, WF = W * F;
+    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
+    const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
+    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
+    float o[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int pos = kk + e;
+        const int f = f0 + e >= F ? f0 + e - F : f0 + e;
+        const bool in_row = pos < WF;
+        const bool lastday = in_row && pos >= WF - F;
+        const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
+        o[e] = pick(lastday && f < F - 1, bsel, o[e]);
+        o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
+    }
+    return f4{o[0], o[1], o[2], o[3]};
+}
+
+// The tile role: flat_wg_body_patch's stream of tile t in two store phases. Its rows' bar
+// and counter (kp_in) are staged with the window, so every chunk that needs neither bar nor
+// w' is composed and stored before the tile looks at the relay words; then w' of its rows,
+// waited for where a scalar block has not relayed it yet, and the last-day / slot chunks.
+// OUT: double-buffered (the chunks past the tile read straight from obs).
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
                                            f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
@@ -110,30 +156,22 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     const bool mine = (uint32_t)tid <= g_hi - g_lo;
     const uint32_t g = g_lo + (mine ? (uint32_t)tid : 0u);
     const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
-    const float* barb = env_bar(p, (int)b);                         // null: a day outside the series
-    const float nanv = __int_as_float(0x7fc00000);
-    const f4 xb = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
-    uint64_t ww = relay_get(r.w + g), kw = relay_get(r.k + b);
-    bool ready = !mine || ((uint32_t)(ww >> 32) == r.epoch && (uint32_t)(kw >> 32) == r.epoch);
-    while (!__all(ready)) {                     // a scalar block placed before this tile is still running
-        __builtin_amdgcn_s_sleep(2);
-        if (!ready) {
-            ww = relay_get(r.w + g);
-            kw = relay_get(r.k + b);
-            ready = (uint32_t)(ww >> 32) == r.epoch && (uint32_t)(kw >> 32) == r.epoch;
-        }
-    }
     if (mine) {
-        sh_bar[tid] = xb;
-        sh_wp[tid] = __uint_as_float((uint32_t)ww);
-        sh_kc[tid] = (int32_t)(uint32_t)kw;
+        const float* barb = env_bar(p, (int)b);                     // null: a day outside the series
+        const float nanv = __int_as_float(0x7fc00000);
+        sh_bar[tid] = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
+        sh_kc[tid] = r.kp_in[b];
     }
 #pragma unroll
     for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
     if (tid < 2) sh4[CPW + tid] = hal;
     __syncthreads();
+    // phase 1: the chunks that need neither bar nor w'
     const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
     const bool first_out = !OUT && t > 0;                           // feeds the previous tile's halo
+    f4 com[V];
+    int kkv[V], iv[V];
+    uint32_t pend = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int j = 64 * V * wave + 64 * v + lane;
@@ -141,24 +179,51 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
         const uint32_t bq = fdiv(q, p.div_units);
         const uint32_t j0 = 4u * (q - bq * per4);
         const uint32_t row = fdiv(j0, p.div_wf);
-        const int kk = (int)(j0 - row * (uint32_t)WF);
-        const int i = (int)(bq * (uint32_t)N + row - g_lo);
+        kkv[v] = (int)(j0 - row * (uint32_t)WF);
+        iv[v] = (int)(bq * (uint32_t)N + row - g_lo);
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        const f4 o = compose2(p, kk, sh_kc[i], un, sh, [&](f4& x, float& xwp) {
-            x = sh_bar[i];
-            xwp = sh_wp[i];
-        });
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
+        bool need;
+        com[v] = relay_common(p, kkv[v], sh_kc[iv[v]], un, sh, need);
+        if (need) {
+            pend |= 1u << v;
+        } else {
+            buf_store4<kAux>(rd, (uint32_t)j * 16u, com[v]);         // past the end: dropped
+            if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = com[v];
+        }
+    }
+    // the rows' w': relayed by the scalar blocks placed before this tile
+    uint64_t ww = relay_get(r.w + g);
+    bool ready = !mine || (uint32_t)(ww >> 32) == r.epoch;
+    while (!__all(ready)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (!ready) {
+            ww = relay_get(r.w + g);
+            ready = (uint32_t)(ww >> 32) == r.epoch;
+        }
+    }
+    if (mine) sh_wp[tid] = __uint_as_float((uint32_t)ww);
+    __syncthreads();
+    // phase 2: the last-day / slot chunks
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        if (!(pend >> v & 1u)) continue;
+        const int j = 64 * V * wave + 64 * v + lane;
+        const int i = iv[v];
+        const f4 o = relay_patch(p, kkv[v], sh_kc[i], com[v], sh_bar[i], sh_wp[i]);
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);
         if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;
     }
 }
 
 // BLOCK x V tiles (the flat stream's 256 x 2 / 512 x 2), POL the window stream's cache
-// policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar)
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA>
-__global__ __launch_bounds__(BLOCK) void step_relay_kernel(StepParams p, RelayParams r, uint32_t qtot) {
+// policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar), OCC the waves
+// per SIMD the kernel is held to (the 8-assets-per-lane form would otherwise take 84 VGPRs
+// and cut the tiles to 5 waves per SIMD)
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void step_relay_kernel(
+    StepParams p, RelayParams r, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
     __shared__ f4 sh_bar[BLOCK];
     __shared__ float sh_wp[BLOCK];
@@ -168,8 +233,12 @@ __global__ __launch_bounds__(BLOCK) void step_relay_kernel(StepParams p, RelayPa
     else relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, (uint32_t)role, sh4, sh_bar, sh_wp, sh_kc);
 }
 
-// in place: relay halo[i] = chunks (i + 1) * CPW and + 1 of the window (primed by the host
-// when the halo of the last relay step does not belong to this window)
-static __global__ __launch_bounds__(256) void relay_prime_halo_kernel(StepParams p) { copy_halo(p); }
+// the relay step's copies when the previous relay step's do not hold: kp <- the state's
+// counter, and in place halo[i] <- chunks (i + 1) * CPW and + 1 of the window
+static __global__ __launch_bounds__(256) void relay_prime_kernel(StepParams p, int32_t* kp) {
+    copy_halo(p);
+    if (kp)
+        for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < p.B; b += gridDim.x * blockDim.x) kp[b] = p.k[b];
+}
 
 }  // namespace pmenv_dev
