@@ -45,6 +45,12 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+if _raw_stream is None:                        # older torch: the public (slower) accessor
+    def _raw_stream(index):
+        return torch.cuda.current_stream(index).cuda_stream
+
+
 def _version(t):
     """t's in-place write counter; None for inference-mode tensors, which keep none
     (their edits are then assumed on every step)."""
@@ -168,6 +174,8 @@ class TradingEnv:
             self._w_new = s[off[7]:off[7] + 4 * B * N].view(torch.float32).view(B, N)
         self.weights = RingView(self)
         self._obs_shape = (B, N, W, self.cfg.features)
+        self._obs_size = torch.Size(self._obs_shape)
+        self._dev_index = self.device.index
         self._args = _abi.PmenvStepArgs()          # reused: every field is set on every step
         self.track_info = (B == 1) if self._track_info_arg is None else bool(self._track_info_arg)
         # the last reset/step came unbatched / with CPU tensors; a TradingEnv() whose shape
@@ -204,7 +212,8 @@ class TradingEnv:
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the raw hipStream_t of the current stream (an int: ctypes passes it as void*)
+        return _raw_stream(self._dev_index)
 
     def _reset_info(self):
         """trading_env.py:13-18 / :34-39 (dict order is relied on by util/plot.py:61). With
@@ -283,6 +292,9 @@ class TradingEnv:
                 inf["rewards"].append(rews[i])
 
     def _obs_check(self, features, name="features"):
+        if features.shape == self._obs_size and features.dtype is torch.float32 and features.is_cuda and \
+                features.get_device() == self._dev_index and features.is_contiguous():
+            return False                                   # the common case: a batched device window
         cfg = self.cfg
         shape = self._obs_shape
         if features.dtype != torch.float32 or not features.is_contiguous() or \
@@ -301,8 +313,9 @@ class TradingEnv:
         B = self.cfg.num_envs
         if not torch.is_tensor(x):
             x = torch.as_tensor(x)
-        elif x.dtype == torch.float32 and x.device == self.device and x.is_contiguous() and x.numel() == B * per_env:
-            return x if x.dim() == 2 and x.shape[0] == B else x.view(B, per_env)   # the common case: as is
+        elif x.dtype is torch.float32 and x.is_cuda and x.get_device() == self._dev_index and x.is_contiguous() \
+                and x.numel() == B * per_env:
+            return x                                # the common case: as is (only its data pointer is used)
         if x.numel() != B * per_env:
             # weight_buffer.py:18-19 raises ValueError on a mis-shaped action
             raise ValueError(f"{name} must have {B} x {per_env} elements, got shape {tuple(x.shape)}")
@@ -386,9 +399,10 @@ class TradingEnv:
         once at capture — must be announced with window_written(features) /
         state_written(), or the next flat step composes tile seams from stale copies.
         """
-        self._fit(features)
+        if self._free:
+            self._fit(features)
         unb = self._obs_check(features)
-        if features.device.type == "cpu":           # the reference's CPU tensors: staged through the GPU
+        if not features.is_cuda:                    # the reference's CPU tensors: staged through the GPU
             if out is not None and out.device.type != "cpu":
                 raise ValueError("out must live where features does")
             dev_out = None if out is None else torch.empty(out.shape, dtype=out.dtype, device=self.device)
@@ -397,7 +411,7 @@ class TradingEnv:
             (features if out is None else out).copy_(res)
             self._host_io = True
             return r.cpu(), (features if out is None else out)
-        if out is not None and out.device.type == "cpu":
+        if out is not None and not out.is_cuda:
             raise ValueError("out must live where features does")
         self._host_io = False
         return self._step(action, features, prices, bar, out, series, day, weights_out, unb, host=False)
