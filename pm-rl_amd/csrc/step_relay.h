@@ -83,50 +83,11 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
     }
 }
 
-// compose2 (env_step.h) in two halves, the same selects element by element: the common
-// form with whether the chunk holds a row's last day or its ring slot (then it needs the
-// row's bar and w'), and the patch of those elements
-__device__ __forceinline__ f4 relay_common(const StepParams& p, int kk, int32_t k, const float (&un)[4],
-                                           const float (&sh)[4], bool& need) {
-    constexpr int F = 5;
-    const int W = p.W, WF = W * F;
-    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
-    const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
-    float o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int f = f0 + e >= F ? f0 + e - F : f0 + e;
-        o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
-    }
-    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
-    need = kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u);
-    return f4{o[0], o[1], o[2], o[3]};
-}
-
-__device__ __forceinline__ f4 relay_patch(const StepParams& p, int kk, int32_t k, f4 c, f4 xb, float xwp) {
-    constexpr int F = 5;
-    const int W = p.W, WF = W * F;
-    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
-    const int f0 = kk - (int)fdiv((uint32_t)kk, p.div_f) * F;
-    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
-    float o[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int pos = kk + e;
-        const int f = f0 + e >= F ? f0 + e - F : f0 + e;
-        const bool in_row = pos < WF;
-        const bool lastday = in_row && pos >= WF - F;
-        const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
-        o[e] = pick(lastday && f < F - 1, bsel, o[e]);
-        o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
-    }
-    return f4{o[0], o[1], o[2], o[3]};
-}
-
-// The tile role: flat_wg_body_patch's stream of tile t in two store phases. Its rows' bar
-// and counter (kp_in) are staged with the window, so every chunk that needs neither bar nor
-// w' is composed and stored before the tile looks at the relay words; then w' of its rows,
-// waited for where a scalar block has not relayed it yet, and the last-day / slot chunks.
+// The tile role: flat_wg_body_patch's stream of tile t, its rows' bar and counter (kp_in)
+// staged with the window and their w' from the relay words. (A form that stored every chunk
+// needing neither bar nor w' before reading the relay words, and the last-day / slot chunks
+// after, ran 1.1-1.4x slower: the deferred 16-B chunks leave partly written lines between the
+// two store waves — profiles/ab_r04/relay_split_r04s.err.)
 // OUT: double-buffered (the chunks past the tile read straight from obs).
 template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
@@ -156,44 +117,11 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     const bool mine = (uint32_t)tid <= g_hi - g_lo;
     const uint32_t g = g_lo + (mine ? (uint32_t)tid : 0u);
     const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
-    if (mine) {
-        const float* barb = env_bar(p, (int)b);                     // null: a day outside the series
-        const float nanv = __int_as_float(0x7fc00000);
-        sh_bar[tid] = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
-        sh_kc[tid] = r.kp_in[b];
-    }
-#pragma unroll
-    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
-    if (tid < 2) sh4[CPW + tid] = hal;
-    __syncthreads();
-    // phase 1: the chunks that need neither bar nor w'
-    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
-    const bool first_out = !OUT && t > 0;                           // feeds the previous tile's halo
-    f4 com[V];
-    int kkv[V], iv[V];
-    uint32_t pend = 0;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-        const int j = 64 * V * wave + 64 * v + lane;
-        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
-        const uint32_t bq = fdiv(q, p.div_units);
-        const uint32_t j0 = 4u * (q - bq * per4);
-        const uint32_t row = fdiv(j0, p.div_wf);
-        kkv[v] = (int)(j0 - row * (uint32_t)WF);
-        iv[v] = (int)(bq * (uint32_t)N + row - g_lo);
-        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
-        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
-        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        bool need;
-        com[v] = relay_common(p, kkv[v], sh_kc[iv[v]], un, sh, need);
-        if (need) {
-            pend |= 1u << v;
-        } else {
-            buf_store4<kAux>(rd, (uint32_t)j * 16u, com[v]);         // past the end: dropped
-            if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = com[v];
-        }
-    }
-    // the rows' w': relayed by the scalar blocks placed before this tile
+    const float* barb = env_bar(p, (int)b);                         // null: a day outside the series
+    const float nanv = __int_as_float(0x7fc00000);
+    const f4 xb = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
+    const int32_t kc = r.kp_in[b];
+    // w': relayed by the scalar blocks placed before this tile
     uint64_t ww = relay_get(r.w + g);
     bool ready = !mine || (uint32_t)(ww >> 32) == r.epoch;
     while (!__all(ready)) {
@@ -203,16 +131,34 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
             ready = (uint32_t)(ww >> 32) == r.epoch;
         }
     }
-    if (mine) sh_wp[tid] = __uint_as_float((uint32_t)ww);
+    if (mine) {
+        sh_bar[tid] = xb;
+        sh_wp[tid] = __uint_as_float((uint32_t)ww);
+        sh_kc[tid] = kc;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
     __syncthreads();
-    // phase 2: the last-day / slot chunks
+    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
+    const bool first_out = !OUT && t > 0;                           // feeds the previous tile's halo
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-        if (!(pend >> v & 1u)) continue;
         const int j = 64 * V * wave + 64 * v + lane;
-        const int i = iv[v];
-        const f4 o = relay_patch(p, kkv[v], sh_kc[i], com[v], sh_bar[i], sh_wp[i]);
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
+        const uint32_t bq = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - bq * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const int kk = (int)(j0 - row * (uint32_t)WF);
+        const int i = (int)(bq * (uint32_t)N + row - g_lo);
+        const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
+        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        const f4 o = compose2(p, kk, sh_kc[i], un, sh, [&](f4& x, float& xwp) {
+            x = sh_bar[i];
+            xwp = sh_wp[i];
+        });
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
         if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;
     }
 }
