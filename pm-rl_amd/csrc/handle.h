@@ -82,10 +82,8 @@ struct pmenv {
     int relay;            // PMENV_FUSE_* bits: which windows take it now
     int relay_kl, relay_ka;   // the scalar step's form: KL lanes per env, KA strided assets per lane (0: register)
     int relay_epb;        // envs per scalar block
-    int relay_lead;       // tiles a scalar block goes ahead of the first tile that needs it
     uint32_t relay_tiles, relay_scal;
-    void* relay_mem;      // role table | relay words | halo x 2
-    int32_t* relay_role;  // [relay_tiles + relay_scal]
+    void* relay_mem;      // relay words | counter copy x 2 | halo x 2
     uint64_t* relay_w;    // [B * N] {epoch, w'}
     int32_t* relay_kp[2]; // [B] per parity: the counter before the step (kp_in), after it (kp_out)
     bool relay_kp_ok;     // relay_kp[relay_par] equals the state's counter

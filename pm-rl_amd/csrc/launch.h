@@ -260,7 +260,7 @@ inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
         h->relay_epoch = 1;
     }
     RelayParams r;
-    r.role = h->relay_role;
+    r.scal = h->relay_scal;
     r.w = h->relay_w;
     r.kp_in = h->relay_kp[q];
     r.kp_out = h->relay_kp[1 - q];

@@ -368,7 +368,6 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->relay_kl = kv ? kv / 100 : (N <= 32 ? 32 : 64);
         h->relay_ka = kv ? kv % 100 : 0;
         h->relay_epb = (h->flat_ip_block / 64) * (64 / h->relay_kl);
-        h->relay_lead = 1024;
         h->relay_auto = 0;
     }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
@@ -456,46 +455,30 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
     }
     if (h->relay_ok) {
-        // the role table (scalar block s placed `lead` tiles ahead of the first tile that needs
-        // env s * EPB), the relay words (zero: no epoch yet) and the in-place halo's two parities
+        // the relay words (zero: no epoch yet), the counter copy's and the in-place halo's
+        // two parities
         const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
         const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
         h->relay_tiles = (h->flat_qtot + cpw - 1) / cpw;
         h->relay_scal = (uint32_t)((B + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
-        const size_t nrole = (size_t)h->relay_tiles + h->relay_scal;
         auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
-        const size_t role_b = up16(nrole * 4), words_b = BN * 8, kp_b = up16(B * 4);
+        const size_t words_b = BN * 8, kp_b = up16(B * 4);
         const size_t hal = up16((size_t)h->relay_tiles * 32);
-        hipError_t ae = hipMalloc(&h->relay_mem, role_b + up16(words_b) + 2 * kp_b + 2 * hal);
+        hipError_t ae = hipMalloc(&h->relay_mem, up16(words_b) + 2 * kp_b + 2 * hal);
         if (ae != hipSuccess) {
             set_err(h, "hipMalloc(relay) failed: %s", hipGetErrorString(ae));
             h->relay_mem = nullptr;
             return fail(PMENV_ERR_HIP);
         }
         char* m = (char*)h->relay_mem;
-        h->relay_role = (int32_t*)m;
-        h->relay_w = (uint64_t*)(m + role_b);
-        h->relay_kp[0] = (int32_t*)(m + role_b + up16(words_b));
-        h->relay_kp[1] = (int32_t*)(m + role_b + up16(words_b) + kp_b);
-        h->relay_halo[0] = (float*)(m + role_b + up16(words_b) + 2 * kp_b);
-        h->relay_halo[1] = (float*)(m + role_b + up16(words_b) + 2 * kp_b + hal);
-        int32_t* role = (int32_t*)malloc(nrole * 4);
-        if (!role) { set_err(h, "relay role table: out of host memory"); return fail(PMENV_ERR_ARG); }
-        size_t at = 0;
-        uint32_t s = 0;
-        const uint64_t per4 = h->per4, epb = (uint64_t)h->relay_epb;
-        for (uint32_t t = 0; t < h->relay_tiles; ++t) {
-            // the first tile holding a chunk of env s * EPB
-            while (s < h->relay_scal && (uint64_t)s * epb * per4 / cpw <= (uint64_t)t + (uint64_t)h->relay_lead)
-                role[at++] = -(int32_t)(s++) - 1;
-            role[at++] = (int32_t)t;
-        }
-        while (s < h->relay_scal) role[at++] = -(int32_t)(s++) - 1;
-        ae = hipMemcpy(h->relay_role, role, nrole * 4, hipMemcpyHostToDevice);
-        free(role);
-        if (ae == hipSuccess) ae = hipMemset(h->relay_w, 0, words_b);
+        h->relay_w = (uint64_t*)m;
+        h->relay_kp[0] = (int32_t*)(m + up16(words_b));
+        h->relay_kp[1] = (int32_t*)(m + up16(words_b) + kp_b);
+        h->relay_halo[0] = (float*)(m + up16(words_b) + 2 * kp_b);
+        h->relay_halo[1] = (float*)(m + up16(words_b) + 2 * kp_b + hal);
+        ae = hipMemset(h->relay_w, 0, words_b);
         if (ae != hipSuccess) {
-            set_err(h, "relay tables: %s", hipGetErrorString(ae));
+            set_err(h, "relay words: %s", hipGetErrorString(ae));
             return fail(PMENV_ERR_HIP);
         }
         h->relay_epoch = 0;

@@ -5,20 +5,26 @@
 // boundary: the stream cannot start before the last env's scalar step has ended. The flat
 // one-launch step (step_flat.h) removes the boundary but runs the scalar step inside every
 // tile an env straddles, which lengthens every tile's life. Here one launch carries both
-// roles, interleaved in dispatch order by a host-built role table:
+// roles: blocks [0, S) are the scalar blocks, blocks [S, S + T) the tiles (dispatch order):
 //   * a scalar block runs the two-launch path's own scalar step (the same code, so the same
-//     bits) for its envs and relays each lane's w' and the env's counter as 64-bit words
-//     {epoch, payload} — agent-scope relaxed atomic stores, coherent across the XCDs' L2s
-//     without an L2 write-back fence — then writes the state (scalar_tail);
+//     bits) for its envs and relays each lane's w' as a 64-bit word {epoch, w'} — an
+//     agent-scope relaxed atomic store, coherent across the XCDs' L2s without an L2
+//     write-back fence — then writes the state (scalar_tail) and the counter's next-step
+//     copy (kp_out, read by the next launch);
 //   * a tile streams its 16-B chunks of the flat window exactly as the in-place stream does
 //     (the two-level compose of flat_wg_body_patch), staging its rows' bar, w' and counter
-//     from the relay words; a word whose epoch is not this step's is not yet written, and
-//     the lane re-reads it (s_sleep between tries). Each word validates itself, so no flag
-//     and no ordering between words is needed (the pattern rocPRIM's look-back scan state
-//     uses on gfx942 / gfx950: atomic loads / stores that bypass the non-coherent L2).
-// A tile only ever waits for scalar blocks placed before it in the role table (dispatched
-// earlier, and those never wait), so every wait ends. The scalar blocks go `lead` tiles
-// ahead of the first tile that needs them.
+//     from the relay words and its rows' counter from the parity copy kp_in; a word whose
+//     epoch is not this step's is not yet written, and the lane re-reads it (s_sleep between
+//     tries). Each word validates itself, so no flag and no ordering between words is needed
+//     (the pattern rocPRIM's look-back scan state uses on gfx942 / gfx950: atomic loads /
+//     stores that bypass the non-coherent L2).
+// A tile only ever waits for scalar blocks, which come before every tile in dispatch order
+// and never wait, so every wait ends. Scalar blocks placed only `lead` tiles ahead of their
+// first consumer measured slower at every lead tried: 4,096 x 30 in place 41.2 us at 8,192
+// tiles against 40.7 with every scalar block first, 8,192 x 30 80.4 at 16,384 against 78.6,
+// 16-27 % slower at a 1,024-tile lead (profiles/ab_r04/relay_lead2_r04t.err,
+// relay_lead_r04l.err, relay_r04r.err): the first tiles wait for a scalar block either way,
+// and the ones that come later find their w' relayed.
 //
 // In place, the two chunks past a tile belong to the next tile, which may already have
 // stored them: they come from a halo the next tile wrote in the previous step (its first
@@ -35,7 +41,7 @@
 namespace pmenv_dev {
 
 struct RelayParams {
-    const int32_t* role;     // [tiles + scalar blocks]: >= 0 a tile index, < 0 -(scalar block + 1)
+    uint32_t scal;           // scalar blocks (the first `scal` blocks of the grid)
     uint64_t* w;             // [B * N] {epoch, w' bits}
     const int32_t* kp_in;    // [B] the counter before this step (parity p: written by the last relay step or primed)
     int32_t* kp_out;         // [B] the counter after it (parity 1 - p: the next relay step's kp_in)
@@ -174,9 +180,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) vo
     __shared__ f4 sh_bar[BLOCK];
     __shared__ float sh_wp[BLOCK];
     __shared__ int32_t sh_kc[BLOCK];
-    const int role = __builtin_amdgcn_readfirstlane(r.role[blockIdx.x]);
-    if (role < 0) relay_scalar<BLOCK, KL, KA>(p, r, -role - 1);
-    else relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, (uint32_t)role, sh4, sh_bar, sh_wp, sh_kc);
+    if (blockIdx.x < r.scal) relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
+    else relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
 }
 
 // the relay step's copies when the previous relay step's do not hold: kp <- the state's

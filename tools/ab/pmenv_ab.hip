@@ -334,7 +334,6 @@ void plan(pmenv* h) {
         if (bk == 128 || bk == 256 || bk == 512) t->flat_block = bk;
     }
     t->ablate = knob_int("PMENV_ABLATE", 0);
-    h->relay_lead = knob_int("PMENV_RELAY_LEAD", h->relay_lead);   // step_relay_kernel: scalar blocks' lead (tiles)
     t->one_nocap = knob_int("PMENV_ONE_NOCAP", 0) != 0;
     t->flat1_lds_pad = knob_int("PMENV_FLAT1_LDS_PAD", 0);
     t->flat_s80 = knob_int("PMENV_FLAT_S80", 0) != 0;
