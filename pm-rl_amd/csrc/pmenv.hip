@@ -359,8 +359,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // ---- the relayed one-launch step (step_relay_kernel): the flat stream's shapes (F = 5,
     // W >= 2, 16-B granular env windows) with the two-launch path's scalar step forms
     // (N <= 512, the packed forms' [B*N] descriptors under 2^32 bytes), the stream's tile
-    // geometry; at most BLOCK rows per tile (4 * 2 <= W * F). Forced only (RELAY) until
-    // measured against the other paths.
+    // geometry; at most BLOCK rows per tile (4 * 2 <= W * F).
     {
         const int N = c.num_assets;
         const int kv = h->k1_vec >= kK1Str ? h->k1_vec - kK1Str : h->k1_vec;
@@ -369,6 +368,26 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->relay_ka = kv ? kv % 100 : 0;
         h->relay_epb = (h->flat_ip_block / 64) * (64 / h->relay_kl);
         h->relay_auto = 0;
+    }
+    // AUTO gives the relay step the cache-resident windows where the kernel boundary of two
+    // launches, or the scalar step inside every tile, is what a step pays for (N <= 64,
+    // round 4, in-process interleaved, profiles/ab_r04/relay_band_r04b.err; us per step,
+    // AUTO's previous choice / relay): in place 24-256 MiB — N = 30 at 2,048 / 3,072 / 4,096 /
+    // 6,144 / 8,192 envs 24.9 / 23.7, 34.5 / 32.1, 44.3 / 40.6, 62.1 / 58.3, 81.9 / 80.0 (with
+    // commission 83.6 / 80.6), N = 8 at 4,096 / 8,192 / 16,384 16.2 / 14.5, 27.7 / 24.3, 46.4 /
+    // 42.7, N = 16 at 4,096 / 8,192 27.6 / 24.4, 46.4 / 42.4, N = 64 at 2,048 / 4,096 46.6 /
+    // 43.1, 85.9 / 84.3 — except 24-48 MiB where the one-workgroup-per-env step holds the env
+    // at >= 90 % (1,024 x 30: 13.5 / 14.9); double-buffered 48-128 MiB (2,048 / 4,096 x 30:
+    // 27.2 / 23.2, 49.1 / 41.6; 8,192: 83.2 / 90.6). From 256 MiB in place the flat step leads
+    // (12,288 / 16,384 / 65,536 x 30: 119.0 / 120.5, 156.8 / 159.9, 625.5 / 641.7), and at
+    // config 5 two launches (1,324.6 / 1,360.3).
+    if (h->relay_ok && c.num_assets <= 64) {
+        const double one_fill = h->one_ok ? (double)h->per4 / (256.0 * h->one_waves) : 0.0;
+        const bool one_holds = h->one_ok && one_fill >= 0.9 && win <= (48ll << 20);
+        if (win > (24ll << 20) && win <= (256ll << 20) && !one_holds) h->relay_auto |= PMENV_FUSE_INPLACE;
+        if (win > (48ll << 20) && win <= (128ll << 20)) h->relay_auto |= PMENV_FUSE_DB;
+        h->one_auto &= ~h->relay_auto;
+        h->flat1_auto &= ~h->relay_auto;
     }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {

@@ -270,13 +270,13 @@ def test_gpu_flat_inplace_shapes(N, W, B):
 
 def test_gpu_auto_path_rule():
     """AUTO: windows up to 24 MiB take the one-workgroup-per-env step (launch-latency
-    bound); in place from 24 to 100 MiB a one-launch step too — that one where its waves'
-    chunk slots hold the env with >= 90 % occupancy (N = 30), the flat step otherwise —
-    and from 100 to 256 MiB the two-launch stream (cache-resident windows); above, env
-    windows of >= 1,000 chunks take the flat one-launch step (step_flat_kernel) —
-    double-buffered from 48 MiB, in place from 256 MiB, with or without commission — and
-    the rest the two-launch stream; wide envs (64 < N <= 128) take step_flat_vec_kernel in
-    place above 1 GiB. Checked against the oracle at the band's shapes."""
+    bound); N <= 64 in place from 24 to 256 MiB the relayed one-launch step (step_relay_kernel)
+    — except up to 48 MiB where the one-workgroup-per-env step holds the env with >= 90 %
+    occupancy (N = 30) — and double-buffered from 48 to 128 MiB; above, env windows of
+    >= 1,000 chunks take the flat one-launch step (step_flat_kernel) — double-buffered from
+    128 MiB, in place from 256 MiB, with or without commission — and the rest the two-launch
+    stream; wide envs (64 < N <= 128) take step_flat_vec_kernel in place above 1 GiB.
+    Checked against the oracle at the band's shapes."""
     from pmenv import TradingEnv
 
     def parts(e):
@@ -287,21 +287,24 @@ def test_gpu_auto_path_rule():
     db, ip = parts(TradingEnv(num_envs=1500, num_assets=30, window=50, device=DEV))   # 45 MB
     assert db.startswith("step_env_kernel") and ip.startswith("step_env_kernel")
     db, ip = parts(TradingEnv(num_envs=1700, num_assets=30, window=50, device=DEV))   # 51 MB
-    assert db.startswith("step_flat_kernel") and ip.startswith("step_env_kernel")
+    assert db.startswith("step_relay_kernel") and ip.startswith("step_relay_kernel")
     db, ip = parts(TradingEnv(num_envs=3000, num_assets=30, window=50, device=DEV))   # 90 MB
-    assert db.startswith("step_flat_kernel") and ip.startswith("step_env_kernel")
+    assert db.startswith("step_relay_kernel") and ip.startswith("step_relay_kernel")
     db, ip = parts(TradingEnv(num_envs=4096, num_assets=30, window=50, device=DEV))   # 123 MB: config 2
-    assert db.startswith("step_flat_kernel") and "advance_flat_inplace_kernel" in ip
+    assert db.startswith("step_relay_kernel") and ip.startswith("step_relay_kernel")
+    db, ip = parts(TradingEnv(num_envs=8192, num_assets=30, window=50, device=DEV))   # 246 MB: config 4's share
+    assert db.startswith("step_flat_kernel") and ip.startswith("step_relay_kernel")
     db, ip = parts(TradingEnv(num_envs=4096, num_assets=16, window=50, device=DEV))   # 66 MB, 78 % fill
-    assert ip.startswith("step_flat_kernel")
+    assert ip.startswith("step_relay_kernel")
     db, ip = parts(TradingEnv(num_envs=4096, num_assets=8, window=50, device=DEV))    # 33 MB, 65 % fill
-    assert ip.startswith("step_flat_kernel") and db.startswith("step_env_kernel")
+    assert ip.startswith("step_relay_kernel") and db.startswith("step_env_kernel")
     huge = TradingEnv(num_envs=9000, num_assets=30, window=50, device=DEV)           # 270 MB
     assert huge.step_path.count("step_flat_kernel") == 2
     db, ip = parts(TradingEnv(num_envs=9000, num_assets=8, window=50, device=DEV))    # 72 MB, 500 chunks per env
-    assert "step_flat_kernel" not in db and "step_env_kernel" not in db and ip.startswith("step_flat_kernel")
+    assert db.startswith("step_relay_kernel") and ip.startswith("step_relay_kernel")
     thin = TradingEnv(num_envs=18000, num_assets=8, window=50, device=DEV)           # 144 MB
-    assert "step_flat_kernel" not in thin.step_path and "step_env_kernel" not in thin.step_path
+    db, ip = parts(thin)
+    assert ip.startswith("step_relay_kernel") and "step_flat_kernel" not in db and "step_env_kernel" not in db
     wide = TradingEnv(num_envs=2000, num_assets=65, window=50, device=DEV)           # N > 64
     assert "step_flat_kernel" not in wide.step_path
     comm = TradingEnv(num_envs=9000, num_assets=30, window=50, device=DEV, commission=0.0025)
