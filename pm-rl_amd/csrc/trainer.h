@@ -268,7 +268,9 @@ __device__ __forceinline__ RowQuad<EPL> load_row_quad(const float* a, const floa
     return q;
 }
 
-template <int EPL>
+// COH (tools A/B: the one-launch forward): the partial record is written with agent-scope
+// atomic stores, coherent across the XCDs' L2s for a fold in the same launch
+template <int EPL, bool COH = false>
 __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v_prev, const float* p, int B, int N,
                                                   int kind, int norm, double* work, double (*rec_w)[kPartStride],
                                                   int blk, int nblk) {
@@ -342,7 +344,10 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
     for (int i = 0; i < kPartStride; ++i) acc[i] = rec_w[0][i];
     for (int w = 1; w < 4; ++w) fold_record(kind, norm, acc, rec_w[w]);
     double* part = work + (size_t)6 * B + 8 + blk;        // field-major: coalesced final fold
-    for (int i = 0; i < kPartStride; ++i) part[(size_t)i * nblk] = acc[i];
+    for (int i = 0; i < kPartStride; ++i) {
+        if (COH) __hip_atomic_store(part + (size_t)i * nblk, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else part[(size_t)i * nblk] = acc[i];
+    }
 }
 
 template <int EPL>
@@ -429,6 +434,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_grad_quad_kernel(con
 // single workgroup over the `nparts` block partials: the normalisation decision, the reward
 // and the chosen candidate's mean / std. Thread t folds partials t, t + 256, ... in
 // order, then a fixed-shape LDS tree folds the 256 threads: deterministic.
+template <bool COH = false>
 __device__ __forceinline__ void final_fold(int B, int kind, int norm, double scale, double* work, float* reward_out,
                                            int nparts) {
     __shared__ double sh[4][kPartStride];
@@ -452,7 +458,10 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
             const size_t k = k0 + (size_t)j * kTrainBlock;
 #pragma unroll
             for (int i = 0; i < kPartStride; ++i)
-                q[j][i] = k < nblk && field_used(kind, norm, i) ? parts[(size_t)i * nblk + k] : 0.0;
+                q[j][i] = !(k < nblk && field_used(kind, norm, i)) ? 0.0
+                          : COH ? __hip_atomic_load(const_cast<double*>(parts) + (size_t)i * nblk + k, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : parts[(size_t)i * nblk + k];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j)

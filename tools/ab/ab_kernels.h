@@ -145,6 +145,35 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(cons
 }
 
 
+// The forward in one launch without a ticket (PMENV_BR_RELAY): every row block writes its
+// partial record with agent-scope atomic stores, then (after an order-only fence: a
+// workgroup-scope release and s_waitcnt vmcnt(0), no L2 write-back) a 64-bit flag with the
+// call's epoch; the LAST block, dispatched last, waits for every flag and folds the records
+// through agent-scope atomic loads — final_fold's code and order, so the same bits.
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_relay_kernel(const float* a, const float* v_prev,
+                                                                             const float* p, int B, int N, int kind,
+                                                                             int norm, double scale, double* work,
+                                                                             float* reward_out, uint64_t* flags,
+                                                                             uint64_t epoch) {
+    __shared__ double rec_w[4][kPartStride];
+    const int nblk = (int)gridDim.x;
+    rows_quad_partial<EPL, true>(a, v_prev, p, B, N, kind, norm, work, rec_w, (int)blockIdx.x, nblk);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));          // vmcnt(0): the record is written
+        __hip_atomic_store(flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (blockIdx.x != (unsigned)nblk - 1) return;
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x)
+        while (__hip_atomic_load(flags + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+            __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __syncthreads();
+    final_fold<true>(B, kind, norm, scale, work, reward_out, nblk);
+}
+
 // The in-place flat stream without the LDS image (PMENV_FLAT_DIRECT): each lane loads its
 // own chunk and its shifted source (floats 4j+5 .. 4j+8) straight from memory with a
 // dword-aligned 16-B load; the workgroup's last two chunks take theirs from the next chunk

@@ -753,6 +753,28 @@ bool metrics(const double* returns, const double* values, const float* weights, 
 bool batch_reward_forward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
                           int32_t reward_kind, int32_t norm, double scale, double* work, float* reward_out,
                           float* ret_out, hipStream_t stream, int* rc) {
+    if (knob("PMENV_BR_RELAY") && N <= kQuadMaxN) {   // one launch, flags instead of a ticket
+        static uint64_t* flags = nullptr;
+        static size_t nflags = 0;
+        static uint64_t epoch = 0x5eed000000000000ull ^ (uint64_t)(uintptr_t)&flags;
+        const int nblk = (B + kQuadRows - 1) / kQuadRows;
+        if ((size_t)nblk > nflags) {
+            if (flags) (void)hipFree(flags);
+            if (hipMalloc(&flags, (size_t)nblk * 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
+            (void)hipMemset(flags, 0, (size_t)nblk * 8);
+            nflags = (size_t)nblk;
+        }
+        ++epoch;
+        if (N <= 32)
+            batch_reward_fwd_relay_kernel<8><<<(unsigned)nblk, kTrainBlock, 0, stream>>>(
+                a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, flags, epoch);
+        else
+            batch_reward_fwd_relay_kernel<16><<<(unsigned)nblk, kTrainBlock, 0, stream>>>(
+                a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, flags, epoch);
+        if (ret_out) batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (!knob("PMENV_BR_ONE")) return false;
     if (hipMemsetAsync(work + 6 * (size_t)B + 6, 0, sizeof(uint32_t), stream) != hipSuccess) {
         *rc = PMENV_ERR_HIP;
