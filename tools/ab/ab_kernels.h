@@ -145,6 +145,22 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(cons
 }
 
 
+// scalar_step_vec_kernel held to OCC waves per SIMD (PMENV_K1_OCC; the 8-assets-per-lane
+// form takes 102 VGPRs, 4 waves per SIMD, unconstrained)
+template <int L, int A, bool STR, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void scalar_step_vec_occ_kernel(
+    StepParams p) {
+    const HaloRegs halo = halo_load(p);
+    constexpr int EPW = 64 / L;
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int b = w * EPW + lane / L;
+    const VecIn<A> in = vec_load<L, A, STR>(p, b, lane);
+    const VecMid<A> m = vec_core<L, A, STR>(p, b, lane, in);
+    vec_tail<L, A, STR>(p, b, lane, in, m);
+    halo_store(p, halo);
+}
+
 // The forward in one launch without a ticket (PMENV_BR_RELAY): every row block writes its
 // partial record with agent-scope atomic stores, then (after an order-only fence: a
 // workgroup-scope release and s_waitcnt vmcnt(0), no L2 write-back) a 64-bit flag with the

@@ -33,6 +33,7 @@ int knob_int(const char* name, int dflt) {
 
 // the knob state of one handle (pmenv::tools)
 struct Tools {
+    int k1_occ = 0;             // PMENV_K1_OCC: the 8-asset packed scalar step held to 6 / 8 waves per SIMD
     int ablate = 0;             // PMENV_ABLATE: timing-only variants (64 + SKIP: flat stream, 128 + ABL: step_env)
     bool one_nocap = false;     // PMENV_ONE_NOCAP: step_env_kernel without the 80-SGPR cap
     bool flat_s80 = false;      // PMENV_FLAT_S80: the in-place flat stream held to 80 SGPRs
@@ -334,6 +335,7 @@ void plan(pmenv* h) {
         if (bk == 128 || bk == 256 || bk == 512) t->flat_block = bk;
     }
     t->ablate = knob_int("PMENV_ABLATE", 0);
+    t->k1_occ = knob_int("PMENV_K1_OCC", 0);
     t->one_nocap = knob_int("PMENV_ONE_NOCAP", 0) != 0;
     t->flat1_lds_pad = knob_int("PMENV_FLAT1_LDS_PAD", 0);
     t->flat_s80 = knob_int("PMENV_FLAT_S80", 0) != 0;
@@ -435,6 +437,13 @@ bool launch_scalar(const pmenv* h, const StepParams& p, hipStream_t stream) {
     if (!t) return false;
     const bool ab_vec = !is_product_k1(h->k1_vec);
     const bool groups = t->k1_groups != 1 && h->cfg.num_assets <= 64 && h->k1_vec == 0;
+    if (t->k1_occ > 0 && h->k1_vec == kK1Str + 6408 && !t->ablate) {   // the wide form held to 6 / 8 waves
+        StepParams q = p;
+        const unsigned grid = (unsigned)((p.B + 3) / 4);
+        if (t->k1_occ >= 8) scalar_step_vec_occ_kernel<64, 8, true, 8><<<grid, 256, 0, stream>>>(q);
+        else scalar_step_vec_occ_kernel<64, 8, true, 6><<<grid, 256, 0, stream>>>(q);
+        return true;
+    }
     if (!t->ablate && !ab_vec && !groups) return false;
     StepParams q = p;
     // the ablations of the stream skip its halo copy too, except the side-data-only ones
