@@ -96,3 +96,56 @@ def test_gpu_sharded_ranks_equal_unsharded_run(impl_shards, impl_full):
         n_tot += m[0]
     assert n_tot == G * T
     np.testing.assert_allclose(res[0][10][1:] + res[1][10][1:], m_full[1:], rtol=1e-12)
+
+
+def _rccl_worker(port, root, q):
+    import sys
+    for p in (os.path.join(root, "pm-rl_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)       # RCCL
+    try:
+        from pmenv import parallel
+        from pmenv.rollout import moments
+        rew, _, _ = _run(0, G, dev)
+        z = parallel.normalize(rew)                               # HIP moments + RCCL all_reduce
+        n, mean, var = parallel.allreduce_moments(moments(rew).clone())
+        torch.manual_seed(0)
+        lin = torch.nn.Linear(N, 1).to(dev).double()
+        lin(rew.double().T[:, :N]).sum().backward()               # rewards [T = 60, B] -> B rows of N inputs
+        before = [p.grad.clone() for p in lin.parameters()]
+        total, cnt = parallel.allreduce_grads(list(lin.parameters()), torch.tensor(3.0, device=dev), 4.0)
+        after = [p.grad.clone() for p in lin.parameters()]
+        q.put((dist.get_backend(), z.cpu().numpy(), n, mean, var, total, cnt,
+               [b.cpu().numpy() for b in before], [a.cpu().numpy() for a in after], rew.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_rccl_single_rank_collectives():
+    """The RCCL branch ("nccl" backend) of the path's collectives, executed on the GPU with one
+    rank (the one-GPU box cannot hold two RCCL ranks on one device): the advantage moments'
+    all-reduce and normalisation, and the gradient bucket's all-reduce, equal the local
+    computation."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), root, q))
+    p.start()
+    backend, z, n, mean, var, total, cnt, before, after, rew = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    x = rew.astype(np.float64)
+    assert n == x.size
+    assert np.isclose(mean, x.mean(), rtol=1e-12, atol=1e-15)
+    assert np.isclose(var, x.var(), rtol=1e-9, atol=1e-18)
+    np.testing.assert_allclose(z, (rew - mean) / (var ** 0.5 + 1e-8), rtol=1e-5, atol=1e-6)
+    assert total == 3.0 and cnt == 4.0
+    for b, a in zip(before, after):
+        np.testing.assert_allclose(a, b / 4.0, rtol=1e-15)
