@@ -19,6 +19,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
+
 #include "../../include/pmenv.h"
 #include "data.h"
 #include "handle.h"
@@ -825,49 +828,50 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones, f
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 
-// Horizon split of the tiled GAE scan (gae_chunk_kernel): used when the B / 64 env
-// blocks leave CUs idle; chunks sized so blocks x chunks ~ 1024 workgroups, each
-// chunk a whole number of 128-day segments (NW = 8, U = 16) and at least 2 of them.
+// Horizon split of the tiled GAE scan: used when the B / 64 env blocks leave CUs idle (few
+// envs, long horizons). Round 4: one pass (gae_lookback_kernel, 64-day chunks, every chunk
+// composing the later chunks' published maps) in place of the round-3 maps + apply passes
+// (gae_chunk_kernel, now in the tools build).
 namespace {
-constexpr int kGaeSeg = 8 * 16;
-int gae_chunks(int32_t T, int32_t B, int* Lc) {
-    const int blocks = (B + 63) / 64;
+constexpr int kGaeLbSeg = 64;                 // NW = 8 waves x U = 8 days
+int gae_lb_chunks(int32_t T, int32_t B) {
     // from 8,192 envs (128 workgroups) the one-pass tile with nt stores wins: 2,048 x 8,192
-    // 59.0 vs 74.2 us split (profiles/rows_r03af/rows_r03af.json); the split keeps 512 envs
-    // x 4,096 days at 16.4 against the tile's 102
-    if (B >= 8192 || T < 4 * kGaeSeg) return 0;
+    // 59.0 vs 74.2 us for the round-3 split (profiles/rows_r03af/rows_r03af.json)
+    if (B >= 8192 || T < 512) return 0;
     if ((size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
-    int want = (1024 + blocks - 1) / blocks;                    // chunks for ~1024 workgroups
-    int lc = (T + want - 1) / want;
-    lc = (lc + kGaeSeg - 1) / kGaeSeg * kGaeSeg;
-    lc = lc < 2 * kGaeSeg ? 2 * kGaeSeg : lc;
-    const int n = (T + lc - 1) / lc;
-    if (n < 2) return 0;
-    *Lc = lc;
-    return n;
+    return (T + kGaeLbSeg - 1) / kGaeLbSeg;
+}
+// the look-back flags' epochs: a process-wide counter from a clock-mixed start, so a flag word
+// left in a reused workspace (an older epoch) or garbage (2^-64) never passes for this call's
+std::atomic<uint64_t> g_gae_epoch{0};
+uint64_t gae_next_epoch() {
+    uint64_t e = g_gae_epoch.load();
+    if (e == 0) {
+        const uint64_t seed = ((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() *
+                               0x9E3779B97F4A7C15ull) | 1ull;
+        g_gae_epoch.compare_exchange_strong(e, seed);
+    }
+    return g_gae_epoch.fetch_add(1) + 1;
 }
 }  // namespace
 
 size_t pmenv_gae_workspace(int32_t T, int32_t B) {
-    int lc = 0;
-    const int n = (T < 1 || B < 1) ? 0 : gae_chunks(T, B, &lc);
-    return n ? (size_t)2 * n * B * sizeof(double) : 0;
+    const int n = (T < 1 || B < 1) ? 0 : gae_lb_chunks(T, B);
+    return n ? ((size_t)2 * n * B + (size_t)n * ((B + 63) / 64)) * sizeof(double) : 0;
 }
 
 int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,
                  int32_t B, float gamma, float lam, double* work, size_t work_bytes, hipStream_t stream) {
     if (!rewards || !values || !adv || !ret || T < 1 || B < 1) return PMENV_ERR_ARG;
-    int lc = 0;
-    const int n = gae_chunks(T, B, &lc);
+    const int n = gae_lb_chunks(T, B);
     int rc = PMENV_OK;
     if (pmenv_tools::gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream, &rc)) return rc;
-    if (!n || !work || work_bytes < (size_t)2 * n * B * sizeof(double))
+    if (!n || !work || work_bytes < pmenv_gae_workspace(T, B) || ((uintptr_t)work & 7u))
         return pmenv_gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream);
-    const dim3 grid((unsigned)((B + 63) / 64), (unsigned)n);
-    gae_chunk_kernel<8, 16, true><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
-                                                            work);
-    gae_chunk_kernel<8, 16, false, 2><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
-                                                             work);
+    const int neb = (B + 63) / 64;
+    uint64_t* flags = reinterpret_cast<uint64_t*>(work + (size_t)2 * n * B);
+    gae_lookback_kernel<8, 8><<<(unsigned)(n * neb), 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma,
+                                                                     lam, n, work, flags, gae_next_epoch());
     return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
 }
 

@@ -333,6 +333,145 @@ __global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, cons
     }
 }
 
+// The horizon split in ONE pass for rollouts with too few envs to fill the chip: grid (env
+// blocks of 64) x (chunks of S = NW x U days), the LATER chunks dispatched first. A
+// workgroup loads its chunk once into registers (the tile kernel's loads), reduces it to the
+// per-env affine map A(chunk start) = D + C A(after the chunk), and publishes it: the maps
+// with agent-scope atomic stores, then — after an order-only fence (workgroup-scope release
+// and s_waitcnt vmcnt(0), no L2 write-back) — a 64-bit flag holding the call's epoch (the
+// pattern of rocPRIM's look-back scan state on gfx942 / gfx950). It then composes every
+// later chunk's map into its carry — the NW waves each take a contiguous part of the later
+// chunks, waiting for their flags and reading their maps through agent-scope atomic loads,
+// and the parts are composed in order through LDS — and walks its registers writing adv /
+// ret (nt stores: written once, read by the learner later). Inputs are read once (17 B
+// per element, against 26 for the maps + apply split) and a workgroup only waits for
+// chunks dispatched before it, which never wait for it, so every wait ends.
+template <int NW, int U>
+__global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, const float* v, const uint8_t* dones,
+                                                              float* adv, float* ret, int T, int B, float gamma,
+                                                              float lam, int nC, double* maps, uint64_t* flags,
+                                                              uint64_t epoch) {
+    __shared__ double shC[NW][64], shD[NW][64];     // the chunk's per-wave maps
+    __shared__ double sxC[NW][64], sxD[NW][64];     // the later chunks' maps, a part per wave
+    constexpr int S = NW * U;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nEB = (B + 63) / 64;
+    const int c = nC - 1 - (int)(blockIdx.x / (unsigned)nEB);
+    const int eb = (int)(blockIdx.x % (unsigned)nEB);
+    const int b = eb * 64 + lane;
+    const bool ok = b < B;
+    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
+    const uint32_t row = (uint32_t)B * 4u;
+    const auto rs_r = make_rsrc(r, (uint32_t)T * row);
+    const auto rs_v = make_rsrc(v, (uint32_t)(T + 1) * row);
+    const auto rs_d = make_rsrc(dones ? (const void*)dones : (const void*)r, dones ? (uint32_t)T * (uint32_t)B : 0u);
+    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
+    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
+    const uint32_t voff_st = ok ? voff : 0x80000000u;
+    const double g = (double)gamma, gl = (double)gamma * (double)lam;
+    const int seg_start = c * S, seg_end = min(T, seg_start + S);
+    const int t0 = seg_start + w * U;
+    float vv[U + 1], rr[U];
+    uint32_t alive = 0;
+#pragma unroll
+    for (int u = 0; u <= U; ++u) {                // v has T + 1 rows: row seg_end closes the chunk
+        const uint32_t t = (uint32_t)min(t0 + u, seg_end);
+        vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
+        rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
+        const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
+        alive |= (dn ? 0u : 1u) << u;
+    }
+    double dl[U];
+    double C = 1.0, D = 0.0;
+#pragma unroll
+    for (int u = U - 1; u >= 0; --u) {
+        const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+        dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
+        if (t0 + u < seg_end) {
+            D = dl[u] + gl * n * D;
+            C = gl * n * C;
+        }
+    }
+    shC[w][lane] = C;
+    shD[w][lane] = D;
+    __syncthreads();
+    double* mapC = maps;
+    double* mapD = maps + (size_t)nC * B;
+    if (w == 0) {                                 // publish the chunk's map
+        double Ca = 1.0, Da = 0.0;
+        for (int j = NW - 1; j >= 0; --j) {
+            Da = shD[j][lane] + shC[j][lane] * Da;
+            Ca = shC[j][lane] * Ca;
+        }
+        if (ok) {
+            __hip_atomic_store(mapC + (size_t)c * B + b, Ca, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(mapD + (size_t)c * B + b, Da, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));          // vmcnt(0): the maps are written
+        if (lane == 0) __hip_atomic_store(flags + (size_t)c * nEB + eb, epoch, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // this wave's part of the later chunks: [j0, j1)
+    const int nl = nC - 1 - c, m = (nl + NW - 1) / NW;
+    const int j0 = c + 1 + w * m, j1 = min(nC, j0 + m);
+    double Cw = 1.0, Dw = 0.0;
+    if (j0 < j1) {
+        for (int base = j0; base < j1; base += 64) {
+            const int j = base + lane;
+            bool ready = j >= j1 || __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            while (!__all(ready)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (!ready)
+                    ready = __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const size_t bb = (size_t)(ok ? b : B - 1);
+        for (int hi = j1 - 1; hi >= j0; hi -= 8) {    // eight maps in flight, composed in order
+            double cq[8], dq[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int j = max(hi - k, j0);
+                cq[k] = __hip_atomic_load(mapC + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dq[k] = __hip_atomic_load(mapD + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (hi - k >= j0) {
+                    Dw = dq[k] + cq[k] * Dw;
+                    Cw = cq[k] * Cw;
+                }
+            }
+        }
+    }
+    sxC[w][lane] = Cw;
+    sxD[w][lane] = Dw;
+    __syncthreads();
+    double a = 0.0;                               // the advantage just after the chunk
+    for (int j = NW - 1; j >= 0; --j) a = sxD[j][lane] + sxC[j][lane] * a;
+    for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
+#pragma unroll
+    for (int u = U - 1; u >= 0; --u) {
+        const int t = t0 + u;
+        if (t < seg_end) {
+            const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+            a = dl[u] + gl * n * a;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret, voff_st,
+                                                  (uint32_t)t * row, 2);
+        }
+    }
+}
+
 constexpr int kMomBlock = 256;
 constexpr int kMomBlocks = 1024;
 

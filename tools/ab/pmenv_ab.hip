@@ -587,6 +587,27 @@ bool gae(const float* rewards, const float* values, const uint8_t* dones, float*
         *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
         return true;
     }
+    if (k && !strcmp(k, "split")) {               // the round-3 horizon split: maps pass + apply pass
+        const int blocks = (B + 63) / 64;
+        int want = (1024 + blocks - 1) / blocks, lc = (T + want - 1) / want;
+        lc = (lc + 127) / 128 * 128;
+        lc = lc < 256 ? 256 : lc;
+        const int n = (T + lc - 1) / lc;
+        static double* ws = nullptr;
+        static size_t ws_n = 0;
+        const size_t need = (size_t)2 * n * B;
+        if (need > ws_n) {
+            if (ws) (void)hipFree(ws);
+            if (hipMalloc(&ws, need * 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
+            ws_n = need;
+        }
+        const dim3 grid((unsigned)blocks, (unsigned)n);
+        gae_chunk_kernel<8, 16, true><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc, ws);
+        gae_chunk_kernel<8, 16, false, 2><<<grid, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, lc,
+                                                                 ws);
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (!k && !knob("PMENV_GAE_U") && !knob("PMENV_GAE_E")) return false;
     const bool fits = (size_t)(T + 1) * (size_t)B * 4u < (1ull << 31);
     const bool scan = k ? !strcmp(k, "scan") : (B < 64 && T >= 256);
