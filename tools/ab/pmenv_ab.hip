@@ -587,6 +587,28 @@ bool gae(const float* rewards, const float* values, const uint8_t* dones, float*
         *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
         return true;
     }
+    if (k && (!strcmp(k, "lb16") || !strcmp(k, "lb4x16") || !strcmp(k, "lb16x4"))) {   // look-back geometries
+        const int nw = !strcmp(k, "lb4x16") ? 4 : !strcmp(k, "lb16x4") ? 16 : 8;
+        const int u = !strcmp(k, "lb16x4") ? 4 : 16;
+        const int seg = nw * u, n = (T + seg - 1) / seg, neb = (B + 63) / 64;
+        static double* ws = nullptr;
+        static size_t ws_n = 0;
+        const size_t need = (size_t)2 * n * B + (size_t)n * neb;
+        if (need > ws_n) {
+            if (ws) (void)hipFree(ws);
+            if (hipMalloc(&ws, need * 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
+            ws_n = need;
+        }
+        static uint64_t epoch = 0x7a11ull << 48;
+        ++epoch;
+        uint64_t* flags = reinterpret_cast<uint64_t*>(ws + (size_t)2 * n * B);
+        const unsigned g = (unsigned)(n * neb);
+        if (nw == 4) gae_lookback_kernel<4, 16><<<g, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        else if (nw == 16) gae_lookback_kernel<16, 4><<<g, 1024, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        else gae_lookback_kernel<8, 16><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (k && !strcmp(k, "split")) {               // the round-3 horizon split: maps pass + apply pass
         const int blocks = (B + 63) / 64;
         int want = (1024 + blocks - 1) / blocks, lc = (T + want - 1) / want;

@@ -23,12 +23,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--shapes", default="4096x512,16384x64,512x64,2048x4096,1000x200")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--calls", type=int, default=50)
+ap.add_argument("--variant", default="split", help="the tools build's PMENV_GAE: split | lb16 | lb4x16 | lb16x4")
 a = ap.parse_args()
-os.environ["PMENV_GAE"] = "split"
+os.environ["PMENV_GAE"] = a.variant
 dev = torch.device("cuda:0")
 libs = {}
 for name, path in (("lookback", os.path.join(ROOT, "pm-rl_amd/pmenv/libpmenv.so")),
-                   ("split", os.path.join(ROOT, "tools/libpmenv_ab.so"))):
+                   (a.variant, os.path.join(ROOT, "tools/libpmenv_ab.so"))):
     lib = ctypes.CDLL(path)
     for n, res, args in _abi.SIGNATURES:
         fn = getattr(lib, n, None)
