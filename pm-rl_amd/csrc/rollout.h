@@ -236,103 +236,6 @@ __global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const fl
     }
 }
 
-// The tiled scan with the horizon also split across workgroups, for rollouts with
-// too few envs to fill the chip (B / 64 workgroups): grid (B / 64, chunks), chunk c
-// covering days [c*Lc, (c+1)*Lc), Lc a multiple of the NW*U segment.
-//   MAPS  pass: each workgroup reduces its chunk to the per-env affine map
-//               A(chunk start) = D + C * A(after the chunk) -> maps[2][chunks][B] (f64)
-//   apply pass: each workgroup composes the maps of every later chunk into its
-//               carry-in, then runs the tiled scan over its chunk writing adv / ret.
-// The inputs are read twice (26 B per element instead of 17) in exchange for
-// chunks x the workgroups; selected by the host only where B / 64 leaves the CUs idle.
-// SP: cache-policy bits of the apply pass's adv / ret stores
-template <int NW, int U, bool MAPS, int SP = 0>
-__global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, const float* v, const uint8_t* dones,
-                                                           float* adv, float* ret, int T, int B, float gamma,
-                                                           float lam, int Lc, double* maps) {
-    __shared__ double shC[NW][64], shD[NW][64];
-    constexpr int S = NW * U;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.x * 64 + lane;
-    const int chunk = blockIdx.y, nchunks = gridDim.y;
-    const bool ok = b < B;
-    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
-    const uint32_t row = (uint32_t)B * 4u;
-    const auto rs_r = make_rsrc(r, (uint32_t)T * row);
-    const auto rs_v = make_rsrc(v, (uint32_t)(T + 1) * row);
-    const auto rs_d = make_rsrc(dones ? (const void*)dones : (const void*)r, dones ? (uint32_t)T * (uint32_t)B : 0u);
-    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
-    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
-    const uint32_t voff_st = ok ? voff : 0x80000000u;
-    const double g = (double)gamma, gl = (double)gamma * (double)lam;
-    const int c0 = chunk * Lc, c1 = min(T, c0 + Lc);
-    double* mapC = maps;
-    double* mapD = maps + (size_t)nchunks * B;
-    const int bb = ok ? b : B - 1;
-    double carry = 0.0, Cc = 1.0;                 // apply: advantage after the segment; maps: A = carry + Cc x
-    if (!MAPS)
-        for (int j = nchunks - 1; j > chunk; --j)
-            carry = mapD[(size_t)j * B + bb] + mapC[(size_t)j * B + bb] * carry;
-    for (int seg_end = c1; seg_end > c0; seg_end -= S) {
-        const int seg_start = max(seg_end - S, c0);
-        const int t0 = seg_start + w * U;
-        float vv[U + 1], rr[U];
-        uint32_t alive = 0;
-#pragma unroll
-        for (int u = 0; u <= U; ++u) {
-            const uint32_t t = (uint32_t)min(t0 + u, seg_end);
-            vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
-            rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
-            const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
-            alive |= (dn ? 0u : 1u) << u;
-        }
-        double dl[U];
-        double C = 1.0, D = 0.0;
-#pragma unroll
-        for (int u = U - 1; u >= 0; --u) {
-            const double n = (alive >> u) & 1u ? 1.0 : 0.0;
-            dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
-            if (t0 + u < seg_end) {
-                D = dl[u] + gl * n * D;
-                C = gl * n * C;
-            }
-        }
-        shC[w][lane] = C;
-        shD[w][lane] = D;
-        __syncthreads();
-        if (!MAPS) {
-            double a = carry;
-            for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
-#pragma unroll
-            for (int u = U - 1; u >= 0; --u) {
-                const int t = t0 + u;
-                if (t < seg_end) {
-                    const double n = (alive >> u) & 1u ? 1.0 : 0.0;
-                    a = dl[u] + gl * n * a;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st,
-                                                          (uint32_t)t * row, SP);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret,
-                                                          voff_st, (uint32_t)t * row, SP);
-                }
-            }
-        }
-        for (int j = NW - 1; j >= 0; --j) {
-            carry = shD[j][lane] + shC[j][lane] * carry;
-            if (MAPS) Cc = shC[j][lane] * Cc;
-        }
-        __syncthreads();
-    }
-    if (MAPS && w == 0 && ok) {
-        mapC[(size_t)chunk * B + b] = Cc;
-        mapD[(size_t)chunk * B + b] = carry;
-    }
-}
-
 // The horizon split in ONE pass for rollouts with too few envs to fill the chip: grid (env
 // blocks of 64) x (chunks of S = NW x U days), the LATER chunks dispatched first. A
 // workgroup loads its chunk once into registers (the tile kernel's loads), reduces it to the
