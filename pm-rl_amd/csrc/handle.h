@@ -81,7 +81,8 @@ struct pmenv {
     int relay_auto;       // PMENV_FUSE_* bits the automatic choice gives it
     int relay;            // PMENV_FUSE_* bits: which windows take it now
     int relay_kl, relay_ka;   // the scalar step's form: KL lanes per env, KA strided assets per lane (0: register)
-    int relay_epb;        // envs per scalar block
+    int relay_block, relay_v; // the tiles' geometry: relay_block threads x relay_v 16-B chunks
+    int relay_epb;        // envs per scalar block (relay_block / 64 waves x 64 / relay_kl envs)
     uint32_t relay_tiles, relay_scal;
     void* relay_mem;      // relay words | counter copy x 2 | halo x 2
     uint64_t* relay_w;    // [B * N] {epoch, w'}
@@ -228,6 +229,10 @@ inline int64_t window_bytes(const pmenv_cfg& c) {
 // ---------------------------------------------------------------- tools-build hooks
 // Defined weak (doing nothing) in pmenv.hip; tools/ab/pmenv_ab.hip defines them for
 // tools/libpmenv_ab.so. A launch hook returns true when it enqueued the launch itself.
+namespace pmenv_dev {
+struct RelayParams;
+}
+
 namespace pmenv_tools {
 void plan(pmenv* h);        // after the product's shape plan, before any allocation
 void release(pmenv* h);
@@ -235,6 +240,8 @@ bool launch_scalar(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t s
 bool launch_advance(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_one(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_fused(const pmenv* h, const pmenv_dev::StepParams& p, int fuse_bit, uint32_t phases, hipStream_t stream);
+bool launch_relay(const pmenv* h, const pmenv_dev::StepParams& p, const pmenv_dev::RelayParams& r, unsigned grid,
+                  hipStream_t stream);
 bool launch_flat1(const pmenv* h, const pmenv_dev::StepParams& p, unsigned grid, bool out, int pol,
                   hipStream_t stream);
 bool gae(const float* rewards, const float* values, const uint8_t* dones, float* adv, float* ret, int32_t T,

@@ -240,7 +240,7 @@ inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParam
 inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     const bool out = p.obs_out != p.obs;
     const int q = h->relay_par;
-    const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
+    const uint32_t cpw = (uint32_t)(h->relay_block * h->relay_v);
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
     const bool need_halo = !out && h->relay_obs != p.obs;
@@ -268,7 +268,8 @@ inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     r.halo_out = h->relay_halo[1 - q];
     r.epoch = h->relay_epoch;
     const unsigned grid = h->relay_tiles + h->relay_scal;
-    if (h->flat_ip_block == 256) {
+    if (pmenv_tools::launch_relay(h, p, r, grid, stream)) {
+    } else if (h->relay_block == 256) {
         if (out) launch_relay_g<256, 0, true>(h, p, r, grid, stream);
         else launch_relay_g<256, 0, false>(h, p, r, grid, stream);
     } else {

@@ -369,7 +369,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->relay_ok = h->flat_ok && c.window >= 2 && N <= 512 && (N <= 64 || h->k1_vec != 0);
         h->relay_kl = kv ? kv / 100 : (N <= 32 ? 32 : 64);
         h->relay_ka = kv ? kv % 100 : 0;
-        h->relay_epb = (h->flat_ip_block / 64) * (64 / h->relay_kl);
+        h->relay_block = h->flat_ip_block;
+        h->relay_v = 2;
         h->relay_auto = 0;
     }
     // AUTO gives the relay step the cache-resident windows where the kernel boundary of two
@@ -479,8 +480,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     if (h->relay_ok) {
         // the relay words (zero: no epoch yet), the counter copy's and the in-place halo's
         // two parities
-        const uint32_t cpw = (uint32_t)(h->flat_ip_block * 2);
+        const uint32_t cpw = (uint32_t)(h->relay_block * h->relay_v);
         const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
+        h->relay_epb = (h->relay_block / 64) * (64 / h->relay_kl);
         h->relay_tiles = (h->flat_qtot + cpw - 1) / cpw;
         h->relay_scal = (uint32_t)((B + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
         auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
@@ -1098,6 +1100,10 @@ __attribute__((weak, noinline)) bool launch_scalar(const pmenv*, const StepParam
 __attribute__((weak, noinline)) bool launch_advance(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_one(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_fused(const pmenv*, const StepParams&, int, uint32_t, hipStream_t) {
+    return false;
+}
+__attribute__((weak, noinline)) bool launch_relay(const pmenv*, const StepParams&, const RelayParams&, unsigned,
+                                                  hipStream_t) {
     return false;
 }
 __attribute__((weak, noinline)) bool launch_flat1(const pmenv*, const StepParams&, unsigned, bool, int,

@@ -336,6 +336,14 @@ void plan(pmenv* h) {
     }
     t->ablate = knob_int("PMENV_ABLATE", 0);
     t->k1_occ = knob_int("PMENV_K1_OCC", 0);
+    if (const char* k = knob("PMENV_RELAY_GEOM")) {   // "128x2" | "128x4" | "256x4" | "256x1": N <= 32 only
+        int bk = 0, v = 0;
+        if (sscanf(k, "%dx%d", &bk, &v) == 2 && h->cfg.num_assets <= 32 && h->k1_vec == 0 &&
+            ((bk == 128 && (v == 2 || v == 4)) || (bk == 256 && (v == 4 || v == 1)))) {
+            h->relay_block = bk;
+            h->relay_v = v;
+        }
+    }
     t->one_nocap = knob_int("PMENV_ONE_NOCAP", 0) != 0;
     t->flat1_lds_pad = knob_int("PMENV_FLAT1_LDS_PAD", 0);
     t->flat_s80 = knob_int("PMENV_FLAT_S80", 0) != 0;
@@ -524,6 +532,26 @@ bool launch_fused(const pmenv* h, const StepParams& p0, int fuse_bit, uint32_t p
     else { PMENV_FUSED_LAUNCH(4) }
 #undef PMENV_FUSED_LAUNCH
     return true;
+}
+
+// PMENV_RELAY_GEOM: the relay step's tiles in other geometries (the register scalar form, N <= 32)
+template <int BK, int V>
+static void relay_geom(const StepParams& p, const RelayParams& r, uint32_t q, unsigned grid, bool out,
+                       hipStream_t stream) {
+    if (out) step_relay_kernel<BK, V, 0, true, 32, 0><<<grid, BK, 0, stream>>>(p, r, q);
+    else step_relay_kernel<BK, V, 0, false, 32, 0><<<grid, BK, 0, stream>>>(p, r, q);
+}
+bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, hipStream_t stream) {
+    const int g = h->relay_block * 10 + h->relay_v;
+    const bool out = p.obs_out != p.obs;
+    const uint32_t q = h->flat_qtot;
+    switch (g) {
+    case 1282: relay_geom<128, 2>(p, r, q, grid, out, stream); return true;
+    case 1284: relay_geom<128, 4>(p, r, q, grid, out, stream); return true;
+    case 2564: relay_geom<256, 4>(p, r, q, grid, out, stream); return true;
+    case 2561: relay_geom<256, 1>(p, r, q, grid, out, stream); return true;
+    default: return false;
+    }
 }
 
 bool launch_flat1(const pmenv* h, const StepParams& p, unsigned grid, bool out, int pol, hipStream_t stream) {
