@@ -336,10 +336,12 @@ void plan(pmenv* h) {
     }
     t->ablate = knob_int("PMENV_ABLATE", 0);
     t->k1_occ = knob_int("PMENV_K1_OCC", 0);
-    if (const char* k = knob("PMENV_RELAY_GEOM")) {   // "128x2" | "128x4" | "256x4" | "256x1": N <= 32 only
+    if (const char* k = knob("PMENV_RELAY_GEOM")) {   // BLOCK x V of relay_geom's table: N <= 64 forms only
         int bk = 0, v = 0;
-        if (sscanf(k, "%dx%d", &bk, &v) == 2 && h->cfg.num_assets <= 32 && h->k1_vec == 0 &&
-            ((bk == 128 && (v == 2 || v == 4)) || (bk == 256 && (v == 4 || v == 1)))) {
+        const int g = sscanf(k, "%dx%d", &bk, &v) == 2 ? bk * 10 + v : 0;
+        const int form = h->relay_kl * 100 + h->relay_ka;
+        if ((g == 1282 || g == 1284 || g == 2564 || g == 2561 || g == 2568 || g == 5124) &&
+            (form == 801 || form == 1601 || form == 3200 || form == 6400)) {
             h->relay_block = bk;
             h->relay_v = v;
         }
@@ -534,22 +536,34 @@ bool launch_fused(const pmenv* h, const StepParams& p0, int fuse_bit, uint32_t p
     return true;
 }
 
-// PMENV_RELAY_GEOM: the relay step's tiles in other geometries (the register scalar form, N <= 32)
+// PMENV_RELAY_GEOM: the relay step's tiles in other geometries (the N <= 64 scalar forms)
+template <int BK, int V, bool OUT>
+static void relay_geom_o(const pmenv* h, const StepParams& p, const RelayParams& r, uint32_t q, unsigned grid,
+                         hipStream_t stream) {
+    switch (h->relay_kl * 100 + h->relay_ka) {
+    case 801: step_relay_kernel<BK, V, 0, OUT, 8, 1><<<grid, BK, 0, stream>>>(p, r, q); break;
+    case 1601: step_relay_kernel<BK, V, 0, OUT, 16, 1><<<grid, BK, 0, stream>>>(p, r, q); break;
+    case 3200: step_relay_kernel<BK, V, 0, OUT, 32, 0><<<grid, BK, 0, stream>>>(p, r, q); break;
+    default: step_relay_kernel<BK, V, 0, OUT, 64, 0><<<grid, BK, 0, stream>>>(p, r, q); break;
+    }
+}
 template <int BK, int V>
-static void relay_geom(const StepParams& p, const RelayParams& r, uint32_t q, unsigned grid, bool out,
+static void relay_geom(const pmenv* h, const StepParams& p, const RelayParams& r, uint32_t q, unsigned grid, bool out,
                        hipStream_t stream) {
-    if (out) step_relay_kernel<BK, V, 0, true, 32, 0><<<grid, BK, 0, stream>>>(p, r, q);
-    else step_relay_kernel<BK, V, 0, false, 32, 0><<<grid, BK, 0, stream>>>(p, r, q);
+    if (out) relay_geom_o<BK, V, true>(h, p, r, q, grid, stream);
+    else relay_geom_o<BK, V, false>(h, p, r, q, grid, stream);
 }
 bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, hipStream_t stream) {
     const int g = h->relay_block * 10 + h->relay_v;
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
     switch (g) {
-    case 1282: relay_geom<128, 2>(p, r, q, grid, out, stream); return true;
-    case 1284: relay_geom<128, 4>(p, r, q, grid, out, stream); return true;
-    case 2564: relay_geom<256, 4>(p, r, q, grid, out, stream); return true;
-    case 2561: relay_geom<256, 1>(p, r, q, grid, out, stream); return true;
+    case 1282: relay_geom<128, 2>(h, p, r, q, grid, out, stream); return true;
+    case 1284: relay_geom<128, 4>(h, p, r, q, grid, out, stream); return true;
+    case 2564: relay_geom<256, 4>(h, p, r, q, grid, out, stream); return true;
+    case 2561: relay_geom<256, 1>(h, p, r, q, grid, out, stream); return true;
+    case 2568: relay_geom<256, 8>(h, p, r, q, grid, out, stream); return true;
+    case 5124: relay_geom<512, 4>(h, p, r, q, grid, out, stream); return true;
     default: return false;
     }
 }
