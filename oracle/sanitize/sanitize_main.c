@@ -20,6 +20,19 @@
  *        nothing. Reads outside the env are checked never to feed a kept position.
  * 3. Emulates the flat one-launch step (step_flat.h) over consecutive steps: tiles in a
  *    random order, the halo and the state snapshot by parity, one owner per env (below).
+ * 4. Emulates the relayed step (step_relay.h) over consecutive steps: scalar blocks and
+ *    tiles interleaved at random, a tile runnable only once every relay word it stages
+ *    carries the step's epoch (the kernel's wait), through the epoch's wrap, caller edits,
+ *    a state write and a step of another path; the tile's staged rows are checked to fit
+ *    its BLOCK threads and every LDS / halo / counter index to stay in its buffer.
+ * 5. Emulates the one-pass look-back GAE (rollout.h gae_lookback_kernel) with the kernel's
+ *    indexing: workgroups publish and compose in a random order subject to the flag waits,
+ *    on a workspace of exactly pmenv_gae_workspace's size holding garbage or the previous
+ *    call's maps and flags; the result is checked against the restatement.
+ * 6. Audits, without data, the addresses of the in-place stream's halo copy
+ *    (env_step.h halo_load / halo_store / copy_halo) for every scalar-step grid, and of
+ *    the tools build's advance_flat_direct_kernel (the kernel of the round-3 record
+ *    profiles/ab_r03/direct_r03d.err), at the shapes of that record.
  * Exit status 0 = clean (UBSan built with -fno-sanitize-recover: any report aborts).
  */
 #include <math.h>
@@ -387,6 +400,377 @@ static void emulate_flat1(int B, int N, int W, int CPW, int T, int storage) {
     free(order); free(lds);
 }
 
+/* ------------------------------------------------------------ 4. the relayed step */
+/* step_relay.h: blocks [0, scal) are scalar blocks (EPB envs each), the rest tiles of CPW =
+ * BLOCK x V chunks. A scalar block writes each env's w' as {epoch, w'} words, the counter's
+ * next-step copy (kp parity 1 - q) and the canonical state. A tile stages one row per thread
+ * (g_lo .. g_hi), the rows' w' from the words (it waits until they carry this step's epoch)
+ * and their counter from kp parity q; in place, the two chunks past it from the halo of
+ * parity q, and it writes its first two output chunks into the halo of parity 1 - q. */
+typedef struct { uint64_t* w; int32_t* kp[2]; float* halo[2]; uint32_t epoch; int par, kp_ok; const float* obs; } relay_st;
+
+static void relay_prime(relay_st* r, const float* obs, int B, const int32_t* k, int64_t ntiles, int64_t CPW,
+                        int64_t qtot, int need_halo) {
+    if (need_halo)
+        for (int64_t i = 0; i + 1 < ntiles; ++i)
+            for (int h = 0; h < 2; ++h) {
+                const int64_t q = (i + 1) * CPW + h;
+                for (int e = 0; e < 4; ++e) r->halo[r->par][i * 8 + h * 4 + e] = q < qtot ? obs[q * 4 + e] : 0.0f;
+            }
+    if (!r->kp_ok)
+        for (int b = 0; b < B; ++b) r->kp[r->par][b] = k[b];
+}
+
+static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, int storage, int dbuf) {
+    const int F = 5, WF = W * F;
+    const int64_t per = (int64_t)N * WF, tot = per * B;
+    if (per % 4 || W < 2) return;
+    const int64_t per4 = per / 4, qtot = tot / 4, CPW = (int64_t)BLOCK * V, ntiles = (qtot + CPW - 1) / CPW;
+    const int EPB = (BLOCK / 64) * (64 / KL), scal = (B + EPB - 1) / EPB;
+    /* the host plan's closed form (pmenv.hip: at most BLOCK rows per tile) */
+    CHECK(4 * CPW / WF + 2 <= BLOCK, "relay: plan admits %lld rows per tile > %d", (long long)(4 * CPW / WF + 2), BLOCK);
+    float* buf[2] = {malloc(sizeof(float) * tot), malloc(sizeof(float) * tot)};
+    float* ref = malloc(sizeof(float) * tot);
+    float* nxt = malloc(sizeof(float) * tot);
+    float* bar = malloc(sizeof(float) * B * N * 4);
+    float* wp = malloc(sizeof(float) * B * N);
+    double* value = malloc(sizeof(double) * B);
+    int32_t* k = malloc(sizeof(int32_t) * B);
+    int32_t* k0 = malloc(sizeof(int32_t) * B);
+    double* v0 = malloc(sizeof(double) * B);
+    relay_st r;
+    r.w = calloc((size_t)B * N, sizeof(uint64_t));
+    r.kp[0] = malloc(sizeof(int32_t) * B); r.kp[1] = malloc(sizeof(int32_t) * B);
+    const int64_t nhal = ntiles > 1 ? (ntiles - 1) * 8 : 1;               /* [tiles - 1][2] float4 */
+    r.halo[0] = malloc(sizeof(float) * nhal); r.halo[1] = malloc(sizeof(float) * nhal);
+    r.epoch = 0xFFFFFFFDu; r.par = 0; r.kp_ok = 0; r.obs = NULL;
+    uint8_t* stored = calloc((size_t)qtot, 1);
+    uint8_t* halo_w[2] = {calloc((size_t)ntiles, 1), calloc((size_t)ntiles, 1)};   /* written this step, per parity */
+    uint8_t* scal_owner = calloc((size_t)B, 1);
+    uint8_t* done = calloc((size_t)(scal + ntiles), 1);
+    int* runnable = malloc(sizeof(int) * (size_t)(scal + ntiles));
+    float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
+    float* s_wp = malloc(sizeof(float) * BLOCK);
+    int32_t* s_kc = malloc(sizeof(int32_t) * BLOCK);
+    int cur = 0;
+    for (int64_t i = 0; i < tot; ++i) buf[0][i] = ref[i] = (float)nrand();
+    for (int b = 0; b < B; ++b) { value[b] = 25000.0 + b; k[b] = (int32_t)(urand() * 2 * W); }
+    for (int t = 0; t < T; ++t) {
+        float* in = buf[cur];
+        float* out = dbuf ? buf[1 - cur] : buf[cur];
+        if (t == T / 3 && !dbuf) {                      /* a caller edit of the window: window_written */
+            for (int64_t i = 0; i < tot; i += 7) { in[i] *= 0.5f; ref[i] = in[i]; }
+            r.obs = NULL;
+        }
+        if (t == T / 2) {                               /* a state write: pmenv_state_written */
+            for (int b = 0; b < B; b += 3) { value[b] = 25000.0; k[b] = 0; }
+            r.kp_ok = 0;
+        }
+        for (int i = 0; i < B * N * 4; ++i) bar[i] = (float)nrand();
+        for (int b = 0; b < B; ++b) {
+            k0[b] = k[b]; v0[b] = value[b];
+            for (int n = 0; n < N; ++n) wp[b * N + n] = flat1_wp(value[b], k[b], b, n);
+            const int shift_w = !(storage && k[b] >= W - 1), slot = (int)((1 + (int64_t)k[b]) % W);
+            advance_ref(ref + (size_t)b * per, nxt + (size_t)b * per, 1, N, W, bar + (size_t)b * N * 4,
+                        wp + (size_t)b * N, shift_w, slot);
+        }
+        if (t == 2 * T / 3) {                           /* a step of another path: both copies stale */
+            memcpy(out, nxt, sizeof(float) * tot);
+            for (int b = 0; b < B; ++b) { value[b] = value[b] * 1.0001 + 1.0; k[b] += 1; }
+            r.obs = NULL; r.kp_ok = 0;
+        } else {
+            /* launch_relay: prime, next epoch (the words restart at 0 on the wrap) */
+            relay_prime(&r, in, B, k, ntiles, CPW, qtot, !dbuf && r.obs != in);
+            if (++r.epoch == 0) { memset(r.w, 0, sizeof(uint64_t) * (size_t)B * N); r.epoch = 1; }
+            const int q = r.par;
+            memset(stored, 0, (size_t)qtot); memset(halo_w[0], 0, (size_t)ntiles); memset(halo_w[1], 0, (size_t)ntiles);
+            memset(scal_owner, 0, (size_t)B); memset(done, 0, (size_t)(scal + ntiles));
+            for (int left = scal + (int)ntiles; left > 0; --left) {
+                int nr = 0;
+                for (int i = 0; i < scal + ntiles; ++i) {
+                    if (done[i]) continue;
+                    if (i >= scal) {                    /* a tile waits for its rows' words */
+                        const int64_t c0 = (int64_t)(i - scal) * CPW, nb = qtot - c0 < CPW ? qtot - c0 : CPW;
+                        const int64_t b_lo = c0 / per4, g_lo = b_lo * N + 4 * (c0 - b_lo * per4) / WF;
+                        const int64_t ql = c0 + nb - 1, b_hi = ql / per4, g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
+                        int ready = 1;
+                        for (int64_t g = g_lo; g <= g_hi && ready; ++g) ready = (uint32_t)(r.w[g] >> 32) == r.epoch;
+                        if (!ready) continue;
+                    }
+                    runnable[nr++] = i;
+                }
+                CHECK(nr > 0, "relay: no block can run (B%d N%d W%d)", B, N, W);
+                if (!nr) break;
+                const int i = runnable[(int)(urand() * nr)];
+                done[i] = 1;
+                if (i < scal) {                         /* relay_scalar */
+                    for (int j = 0; j < EPB; ++j) {
+                        const int b = i * EPB + j;
+                        if (b >= B) continue;
+                        CHECK(!scal_owner[b]++, "relay: env %d stepped twice", b);
+                        for (int n = 0; n < N; ++n)
+                            r.w[(size_t)b * N + n] = ((uint64_t)r.epoch << 32) | 0u;   /* the tag; w' below */
+                        r.kp[1 - q][b] = k[b] + 1;                     /* parity 1 - q: no tile reads it */
+                        value[b] = value[b] * 1.0001 + 1.0;                            /* scalar_tail */
+                        k[b] += 1;
+                    }
+                    continue;
+                }
+                const int64_t tile = i - scal, c0 = tile * CPW;
+                const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
+                const int64_t nh = tile + 1 < ntiles ? (qtot - c0 - nblk < 2 ? qtot - c0 - nblk : 2) : 0;
+                for (int64_t j = 0; j < CPW + 2; ++j) {
+                    for (int e = 0; e < 4; ++e) lds[j * 4 + e] = 0.0f;
+                    if (j < nblk) {
+                        CHECK(dbuf || !stored[c0 + j], "relay: chunk %lld read after a store", (long long)(c0 + j));
+                        for (int e = 0; e < 4; ++e) lds[j * 4 + e] = in[(c0 + j) * 4 + e];
+                    } else if (j >= CPW && j - CPW < nh) {
+                        if (dbuf) {
+                            for (int e = 0; e < 4; ++e) lds[j * 4 + e] = in[(c0 + nblk + j - CPW) * 4 + e];
+                        } else {
+                            CHECK(!halo_w[q][tile], "relay: halo %lld read after this step wrote it", (long long)tile);
+                            CHECK(tile * 8 + (j - CPW) * 4 + 3 < nhal, "relay: halo index past its buffer");
+                            for (int e = 0; e < 4; ++e) lds[j * 4 + e] = r.halo[q][tile * 8 + (j - CPW) * 4 + e];
+                        }
+                    }
+                }
+                const int64_t b_lo = c0 / per4, g_lo = b_lo * N + 4 * (c0 - b_lo * per4) / WF;
+                const int64_t ql = c0 + nblk - 1, b_hi = ql / per4, g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
+                CHECK(g_hi - g_lo < BLOCK, "relay: tile %lld stages %lld rows > %d threads", (long long)tile,
+                      (long long)(g_hi - g_lo + 1), BLOCK);
+                for (int64_t g = g_lo; g <= g_hi && g - g_lo < BLOCK; ++g) {
+                    const int64_t b = g / N;
+                    CHECK(g < (int64_t)B * N, "relay: row %lld past the batch", (long long)g);
+                    s_kc[g - g_lo] = r.kp[q][b];
+                    s_wp[g - g_lo] = flat1_wp(v0[b], k0[b], b, (int)(g - b * N));   /* what the word carries */
+                }
+                for (int64_t j = 0; j < nblk; ++j) {
+                    const int64_t gq = c0 + j, bq = gq / per4, j0 = 4 * (gq - bq * per4), row = j0 / WF;
+                    const int kk = (int)(j0 - row * WF);
+                    const int64_t li = bq * N + row - g_lo;
+                    CHECK(li >= 0 && li <= g_hi - g_lo, "relay: chunk %lld row index %lld", (long long)gq, (long long)li);
+                    const int32_t kc = s_kc[li];
+                    CHECK(kc == k0[bq], "relay: env %lld counter copy %d != %d", (long long)bq, kc, k0[bq]);
+                    const int shift_w = !(storage && kc >= W - 1), slot = (int)((1 + (int64_t)kc) % W);
+                    for (int e = 0; e < 4; ++e) {
+                        const int pos = kk + e;
+                        const int64_t jg = gq * 4 + e, rg = jg / WF;
+                        const int f = (int)((jg - rg * WF) % F), td = (int)((jg - rg * WF) / F);
+                        const float un = lds[j * 4 + e], sh = lds[j * 4 + e + 5];
+                        float v;
+                        if (pos >= WF) v = sh;                                   /* the next row's positions 0..2 */
+                        else if (f == F - 1) v = shift_w ? (td == W - 1 ? s_wp[li] : sh) : (td == slot ? s_wp[li] : un);
+                        else v = td == W - 1 ? bar[rg * 4 + f] : sh;
+                        out[jg] = v;
+                        if (!dbuf && tile > 0 && j < 2) {
+                            CHECK((tile - 1) * 8 + j * 4 + e < nhal, "relay: halo_out index past its buffer");
+                            r.halo[1 - q][(tile - 1) * 8 + j * 4 + e] = v;
+                        }
+                    }
+                    stored[gq] = 1;
+                }
+                if (!dbuf && tile > 0) halo_w[1 - q][tile - 1] = 1;
+            }
+            for (int b = 0; b < B; ++b) CHECK(scal_owner[b] == 1, "relay: env %d stepped %d times", b, scal_owner[b]);
+            r.par = 1 - q; r.kp_ok = 1; r.obs = dbuf ? NULL : out;
+        }
+        float* sw = ref; ref = nxt; nxt = sw;
+        for (int64_t i = 0; i < tot; ++i)
+            if (memcmp(&out[i], &ref[i], 4)) {
+                CHECK(0, "relay: step %d float %lld differs (B%d N%d W%d %dx%d db%d)", t, (long long)i, B, N, W, BLOCK, V, dbuf);
+                break;
+            }
+        if (dbuf) cur = 1 - cur;
+    }
+    free(buf[0]); free(buf[1]); free(ref); free(nxt); free(bar); free(wp); free(value); free(k); free(k0); free(v0);
+    free(r.w); free(r.kp[0]); free(r.kp[1]); free(r.halo[0]); free(r.halo[1]); free(stored); free(halo_w[0]); free(halo_w[1]);
+    free(scal_owner); free(done); free(runnable); free(lds); free(s_wp); free(s_kc);
+}
+
+/* ------------------------------------------------------------ 5. the look-back GAE */
+/* pmenv.hip gae_lb_seg / gae_lb_chunks / pmenv_gae_workspace, restated */
+static int lb_seg(int T, int B) { return (int64_t)((T + 127) / 128) * ((B + 63) / 64) >= 128 ? 128 : 64; }
+static int lb_chunks(int T, int B, int seg) {
+    if (B >= 8192 || T < 512 || (size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
+    return (T + seg - 1) / seg;
+}
+
+/* one call of gae_lookback_kernel<NW, U> on a workspace `ws` of exactly the ABI's size */
+static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv, float* ret, int T, int B, double g,
+                    double gl, int NW, int U, int nC, double* ws, size_t ws_doubles, uint64_t epoch) {
+    const int S = NW * U, nEB = (B + 63) / 64, nblk = nC * nEB;
+    double* mapC = ws;
+    double* mapD = ws + (size_t)nC * B;
+    uint64_t* flags = (uint64_t*)(ws + (size_t)2 * nC * B);
+    CHECK((size_t)2 * nC * B + (size_t)nC * nEB <= ws_doubles, "gae_lb: workspace too small");
+    /* per block: its registers (dl, alive, vv) and LDS maps between the two phases */
+    double* st_dl = malloc(sizeof(double) * (size_t)nblk * 64 * S);
+    double* st_vv = malloc(sizeof(double) * (size_t)nblk * 64 * S);
+    uint8_t* st_al = malloc((size_t)nblk * 64 * S);
+    double* shC = malloc(sizeof(double) * (size_t)nblk * NW * 64);
+    double* shD = malloc(sizeof(double) * (size_t)nblk * NW * 64);
+    int* phase = calloc((size_t)nblk, sizeof(int));
+    int* runnable = malloc(sizeof(int) * (size_t)nblk);
+    for (int left = 2 * nblk; left > 0; --left) {
+        int nr = 0;
+        for (int bi = 0; bi < nblk; ++bi) {
+            if (phase[bi] == 2) continue;
+            if (phase[bi] == 1) {
+                const int c = nC - 1 - bi / nEB, eb = bi % nEB;
+                int ready = 1;
+                for (int j = c + 1; j < nC && ready; ++j) ready = flags[(size_t)j * nEB + eb] == epoch;
+                if (!ready) continue;
+            }
+            runnable[nr++] = bi;
+        }
+        CHECK(nr > 0, "gae_lb: no workgroup can run");
+        if (!nr) break;
+        const int bi = runnable[(int)(urand() * nr)];
+        const int c = nC - 1 - bi / nEB, eb = bi % nEB;
+        const int seg_start = c * S, seg_end = seg_start + S < T ? seg_start + S : T;
+        if (phase[bi] == 0) {                           /* load, reduce, publish */
+            for (int lane = 0; lane < 64; ++lane) {
+                const int b = eb * 64 + lane, ok = b < B, bb = ok ? b : B - 1;
+                double Ca = 1.0, Da = 0.0;
+                double wc[64], wd[64];
+                for (int w = 0; w < NW; ++w) {
+                    const int t0 = seg_start + w * U;
+                    double C = 1.0, D = 0.0;
+                    for (int u = U - 1; u >= 0; --u) {
+                        const int tv = t0 + u + 1 < seg_end ? t0 + u + 1 : seg_end;     /* vv[u + 1] */
+                        const int tu = t0 + u < seg_end ? t0 + u : seg_end;             /* vv[u] */
+                        const int tr = t0 + u < seg_end - 1 ? t0 + u : seg_end - 1;
+                        CHECK((size_t)tv * B + bb < (size_t)(T + 1) * B && (size_t)tr * B + bb < (size_t)T * B, "gae_lb: load index");
+                        const double n = d && d[(size_t)tr * B + bb] ? 0.0 : 1.0;
+                        const double dl = (double)r[(size_t)tr * B + bb] + g * n * (double)v[(size_t)tv * B + bb] -
+                                          (double)v[(size_t)tu * B + bb];
+                        const size_t si = ((size_t)bi * 64 + lane) * S + (size_t)w * U + u;
+                        st_dl[si] = dl; st_al[si] = (uint8_t)n; st_vv[si] = (double)v[(size_t)tu * B + bb];
+                        if (t0 + u < seg_end) { D = dl + gl * n * D; C = gl * n * C; }
+                    }
+                    wc[w] = C; wd[w] = D;
+                    shC[((size_t)bi * NW + w) * 64 + lane] = C;
+                    shD[((size_t)bi * NW + w) * 64 + lane] = D;
+                }
+                for (int w = NW - 1; w >= 0; --w) { Da = wd[w] + wc[w] * Da; Ca = wc[w] * Ca; }
+                if (ok) { mapC[(size_t)c * B + b] = Ca; mapD[(size_t)c * B + b] = Da; }
+            }
+            flags[(size_t)c * nEB + eb] = epoch;
+            phase[bi] = 1;
+            continue;
+        }
+        /* compose the later chunks' maps (a part per wave), then walk and store */
+        for (int lane = 0; lane < 64; ++lane) {
+            const int b = eb * 64 + lane, ok = b < B, bb = ok ? b : B - 1;
+            const int nl = nC - 1 - c, m = (nl + NW - 1) / NW;
+            double sxC[64], sxD[64];
+            for (int w = 0; w < NW; ++w) {
+                const int j0 = c + 1 + w * m, j1 = j0 + m < nC ? j0 + m : nC;
+                double Cw = 1.0, Dw = 0.0;
+                for (int j = j1 - 1; j >= j0; --j) {
+                    Dw = mapD[(size_t)j * B + bb] + mapC[(size_t)j * B + bb] * Dw;
+                    Cw = mapC[(size_t)j * B + bb] * Cw;
+                }
+                sxC[w] = Cw; sxD[w] = Dw;
+            }
+            for (int w = 0; w < NW; ++w) {
+                double a = 0.0;
+                for (int j = NW - 1; j >= 0; --j) a = sxD[j] + sxC[j] * a;
+                for (int j = NW - 1; j > w; --j)
+                    a = shD[((size_t)bi * NW + j) * 64 + lane] + shC[((size_t)bi * NW + j) * 64 + lane] * a;
+                const int t0 = seg_start + w * U;
+                for (int u = U - 1; u >= 0; --u) {
+                    const int t = t0 + u;
+                    if (t >= seg_end) continue;
+                    const size_t si = ((size_t)bi * 64 + lane) * S + (size_t)w * U + u;
+                    a = st_dl[si] + gl * (double)st_al[si] * a;
+                    if (ok) { adv[(size_t)t * B + b] = (float)a; ret[(size_t)t * B + b] = (float)(a + st_vv[si]); }
+                }
+            }
+        }
+        phase[bi] = 2;
+    }
+    free(st_dl); free(st_vv); free(st_al); free(shC); free(shD); free(phase); free(runnable);
+}
+
+static void emulate_gae_lb(int T, int B, int NW, int U) {
+    const int seg = NW * U, nC = (T + seg - 1) / seg, nEB = (B + 63) / 64;
+    const size_t ws_doubles = (size_t)2 * nC * B + (size_t)nC * nEB;
+    double* ws = malloc(sizeof(double) * ws_doubles);
+    for (size_t i = 0; i < ws_doubles; ++i) ((uint64_t*)ws)[i] = ((uint64_t)(urand() * 4294967296.0) << 32) ^ (uint64_t)(urand() * 4294967296.0);
+    float* r = malloc(sizeof(float) * (size_t)T * B);
+    float* v = malloc(sizeof(float) * (size_t)(T + 1) * B);
+    uint8_t* d = malloc((size_t)T * B);
+    float* adv = malloc(sizeof(float) * (size_t)T * B);
+    float* ret = malloc(sizeof(float) * (size_t)T * B);
+    float* oa = malloc(sizeof(float) * (size_t)T * B);
+    float* orr = malloc(sizeof(float) * (size_t)T * B);
+    uint64_t epoch = 0x51ED270B00000001ull;
+    for (int call = 0; call < 2; ++call, ++epoch) {    /* the second call finds the first's maps and flags */
+        for (size_t i = 0; i < (size_t)T * B; ++i) { r[i] = (float)nrand(); d[i] = urand() < 0.01; }
+        for (size_t i = 0; i < (size_t)(T + 1) * B; ++i) v[i] = (float)nrand();
+        const float gamma = 0.99f, lam = call ? 1.0f : 0.95f;
+        lb_call(r, v, call ? NULL : d, adv, ret, T, B, (double)gamma, (double)gamma * (double)lam, NW, U, nC, ws,
+                ws_doubles, epoch);
+        or_gae(r, v, call ? NULL : d, oa, orr, T, B, gamma, lam);
+        for (size_t i = 0; i < (size_t)T * B; ++i)
+            if (!(fabsf(adv[i] - oa[i]) <= 1e-5f * (1.0f + fabsf(oa[i]))) ||
+                !(fabsf(ret[i] - orr[i]) <= 1e-5f * (1.0f + fabsf(orr[i])))) {
+                CHECK(0, "gae_lb: T%d B%d %dx%d call %d element %zu: %g vs %g", T, B, NW, U, call, i, adv[i], oa[i]);
+                break;
+            }
+    }
+    free(ws); free(r); free(v); free(d); free(adv); free(ret); free(oa); free(orr);
+}
+
+/* ------------------------------------------------------------ 6. address audits (no data) */
+/* the scalar-step grids of launch.h launch_scalar_kernels (threads), per form */
+static int64_t scalar_threads(int B, int N, int form) {
+    if (form == 801) return ((int64_t)(B + 7) / 8 + 3) / 4 * 256;
+    if (form == 1601) return ((int64_t)(B + 3) / 4 + 3) / 4 * 256;
+    if (form == 1602) return ((int64_t)(B + 3) / 4 + 3) / 4 * 256;          /* tools: scalar_step_vec_kernel<16, 2> */
+    if (form == 6402 || form == 6404 || form == 6408) return ((int64_t)B + 3) / 4 * 256;
+    if (N <= 64) return ((int64_t)(B + (N <= 32 ? 1 : 0)) / (N <= 32 ? 2 : 1) + 3) / 4 * 256;
+    return (int64_t)B * 64;                                                  /* scalar_step_kernel: a wave per env */
+}
+
+static void audit_halo_and_direct(int B, int N, int W, int block, int vec, int form) {
+    const int64_t per4 = (int64_t)N * W * 5 / 4, qtot = (int64_t)B * per4, cpw = (int64_t)block * vec;
+    const int64_t wgs = (qtot + cpw - 1) / cpw, halo_wgs = wgs > 0 ? wgs - 1 : 0;
+    const int64_t halo_f4 = 2 * (halo_wgs + 1);                               /* hipMalloc((halo_wgs + 1) * 32) */
+    CHECK(qtot < (1ll << 31) - 1024, "audit: %d x %d past the flat stream's index", B, N);
+    uint8_t* written = calloc((size_t)halo_wgs + 1, 1);
+    const uint32_t nthr = (uint32_t)scalar_threads(B, N, form);
+    /* halo_load / halo_store (the register-held copy: two entries per thread, a loop beyond) */
+    for (uint32_t gid = 0; gid < nthr; ++gid) {
+        for (int t = 0; t < 2; ++t) {
+            const uint64_t i = (uint64_t)gid + (uint64_t)t * nthr;
+            if (i >= (uint64_t)halo_wgs) continue;
+            const uint64_t q = (i + 1) * (uint64_t)cpw;
+            CHECK(q <= 0xFFFFFFFFull, "audit: uint32 chunk index overflows");
+            CHECK(2 * i + 1 < (uint64_t)halo_f4, "audit: halo store past its buffer");
+            CHECK(q + 1 < (uint64_t)qtot, "audit: halo source past the window (%llu)", (unsigned long long)q);
+            CHECK(!written[i]++, "audit: halo %llu written twice", (unsigned long long)i);
+        }
+    }
+    for (uint64_t i = (uint64_t)2 * nthr; i < (uint64_t)halo_wgs; ++i) {    /* halo_store's loop */
+        CHECK(2 * i + 1 < (uint64_t)halo_f4 && (i + 1) * (uint64_t)cpw + 1 < (uint64_t)qtot, "audit: halo loop index");
+        CHECK(!written[i]++, "audit: halo %llu written twice", (unsigned long long)i);
+    }
+    for (int64_t i = 0; i < halo_wgs; ++i) CHECK(written[i] == 1, "audit: halo %lld not copied", (long long)i);
+    /* advance_flat_direct_kernel<block, vec>: descriptors and the halo pointer per tile */
+    for (int64_t t = 0; t < wgs; ++t) {
+        const int64_t c0 = t * cpw, nblk = qtot - c0 < cpw ? qtot - c0 : cpw;
+        CHECK(nblk > 0 && c0 + nblk <= qtot, "audit: direct tile %lld range", (long long)t);
+        const int64_t nh = t + 1 < wgs ? (qtot - c0 - nblk < 2 ? qtot - c0 - nblk : 2) : 0;
+        CHECK(nh == 0 || (t < halo_wgs && 2 * t + nh <= halo_f4), "audit: direct tile %lld halo", (long long)t);
+        for (int64_t j = 0; j < cpw; ++j)                          /* shifted source: j + 3 <= nblk */
+            if (j + 3 <= nblk) CHECK(j * 16 + 20 + 16 <= nblk * 16, "audit: direct shifted load past its range");
+        if (nblk >= 2) CHECK(nblk - 2 + 1 <= nblk, "audit: direct edge");
+    }
+    free(written);
+}
+
 int main(void) {
     /* every reward kind x norm x ring x ret mode, with and without commission */
     for (int kind = 0; kind < 4; ++kind)
@@ -415,6 +799,40 @@ int main(void) {
             for (int cpw = 0; cpw < 2; ++cpw)
                 emulate_flat1(fshapes[i][0], fshapes[i][1], fshapes[i][2], cpw ? 1024 : 96, 2 * fshapes[i][2] + 3,
                               storage);
+    /* the relayed step: the product's 256 x 2 and 512 x 2 tiles, small tiles that put many
+     * rows and envs in one tile, the register (32 / 64 lanes) and packed (8 / 16 lanes)
+     * scalar forms' blocks, W = 2 (every day a last day), both ring orders, in place and
+     * double-buffered */
+    const int rshapes[][4] = {{37, 30, 50, 32}, {301, 8, 12, 8}, {97, 16, 20, 16}, {9, 64, 47, 64}, {400, 30, 2, 32},
+                              {13, 5, 48, 8}, {3, 1, 600, 8}};
+    for (size_t i = 0; i < sizeof rshapes / sizeof rshapes[0]; ++i)
+        for (int storage = 0; storage < 2; ++storage)
+            for (int db = 0; db < 2; ++db) {
+                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 256, 2, rshapes[i][3], 12, storage, db);
+                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 512, 2, rshapes[i][3], 12, storage, db);
+                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 64, 2, rshapes[i][3], 12, storage, db);
+            }
+    /* the look-back GAE: the product's rule and both chunk lengths, ragged B and T, one chunk */
+    const int gshapes[][2] = {{700, 67}, {513, 3}, {1000, 130}, {600, 64}, {130, 5}};
+    for (size_t i = 0; i < sizeof gshapes / sizeof gshapes[0]; ++i) {
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8);
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16);
+    }
+    {   /* the rule's choice at the shapes the GPU tests run */
+        const int rs[][2] = {{512, 64}, {4096, 512}, {1000, 200}, {5000, 3}, {2048, 4096}, {700, 4099}, {16384, 64}};
+        for (size_t i = 0; i < sizeof rs / sizeof rs[0]; ++i)
+            CHECK(lb_chunks(rs[i][0], rs[i][1], lb_seg(rs[i][0], rs[i][1])) > 0 || rs[i][0] < 512,
+                  "gae_lb: rule declines %d x %d", rs[i][0], rs[i][1]);
+    }
+    /* addresses of the halo copy and the tools build's direct stream at the r03d record's
+     * shapes (16,384 x 30 included) and the BASELINE ones, every scalar grid */
+    const int ashapes[][3] = {{8192, 30, 50}, {4096, 30, 50}, {16384, 30, 50}, {65536, 30, 50}, {8192, 16, 50},
+                              {8192, 500, 50}, {4096, 8, 50}, {3, 1, 2}};
+    const int forms[] = {0, 801, 1601, 1602, 6402, 6408};
+    for (size_t i = 0; i < sizeof ashapes / sizeof ashapes[0]; ++i)
+        for (size_t f = 0; f < sizeof forms / sizeof forms[0]; ++f)
+            for (int g = 0; g < 2; ++g)
+                audit_halo_and_direct(ashapes[i][0], ashapes[i][1], ashapes[i][2], g ? 512 : 256, 2, forms[f]);
     if (fails) { fprintf(stderr, "%d check(s) failed\n", fails); return 1; }
     printf("sanitize ok\n");
     return 0;

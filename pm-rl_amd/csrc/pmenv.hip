@@ -366,11 +366,14 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     {
         const int N = c.num_assets;
         const int kv = h->k1_vec >= kK1Str ? h->k1_vec - kK1Str : h->k1_vec;
-        h->relay_ok = h->flat_ok && c.window >= 2 && N <= 512 && (N <= 64 || h->k1_vec != 0);
-        h->relay_kl = kv ? kv / 100 : (N <= 32 ? 32 : 64);
-        h->relay_ka = kv ? kv % 100 : 0;
         h->relay_block = h->flat_ip_block;
         h->relay_v = 2;
+        // a tile stages one row per thread: 4 CPW / (W F) + 2 rows must fit its BLOCK threads
+        // (for V = 2: W >= 2; the host schedule emulation under tests/ checks it per tile)
+        const bool rows_fit = 4 * h->relay_block * h->relay_v / (c.window * 5) + 2 <= h->relay_block;
+        h->relay_ok = h->flat_ok && c.window >= 2 && rows_fit && N <= 512 && (N <= 64 || h->k1_vec != 0);
+        h->relay_kl = kv ? kv / 100 : (N <= 32 ? 32 : 64);
+        h->relay_ka = kv ? kv % 100 : 0;
         h->relay_auto = 0;
     }
     // AUTO gives the relay step the cache-resident windows where the kernel boundary of two

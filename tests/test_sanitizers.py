@@ -1,10 +1,19 @@
 """Host sanitizers: the CPU restatement and the host emulation of the
-HIP path's two in-place window-advance schedules (the flat stream with its halo; one
-workgroup per env), built with AddressSanitizer + UndefinedBehaviorSanitizer
-(oracle/sanitize/build.sh) and run on random inputs in every mode. The emulation runs
-the workgroups in a random order with every store visible at once and checks that no
-workgroup reads a chunk another one has already stored (read-before-write) and that
-the in-place result equals an out-of-place advance. CPU only."""
+HIP path's in-place schedules, built with AddressSanitizer + UndefinedBehaviorSanitizer
+(oracle/sanitize/build.sh) and run on random inputs in every mode:
+  * the flat stream with its halo, one workgroup per env, and the flat one-launch step —
+    workgroups in a random order with every store visible at once; no workgroup reads a
+    chunk another one has already stored, and the in-place result equals an out-of-place
+    advance;
+  * the relayed step (step_relay.h) — scalar blocks and tiles interleaved at random, a tile
+    runnable only once its rows' relay words carry the step's epoch, through the epoch's
+    wrap, caller edits, a state write and a step of another path; every staged row fits the
+    tile's threads and every LDS / halo / counter index its buffer;
+  * the one-pass look-back GAE — workgroups publishing and composing in a random order under
+    the flag waits, on an exact-size workspace holding garbage or the previous call's flags;
+  * an address audit of the halo copy for every scalar-step grid and of the tools build's
+    advance_flat_direct_kernel at the shapes of profiles/ab_r03/direct_r03d.err.
+CPU only."""
 import os
 import shutil
 import subprocess

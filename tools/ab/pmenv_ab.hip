@@ -340,7 +340,8 @@ void plan(pmenv* h) {
         int bk = 0, v = 0;
         const int g = sscanf(k, "%dx%d", &bk, &v) == 2 ? bk * 10 + v : 0;
         const int form = h->relay_kl * 100 + h->relay_ka;
-        if ((g == 1282 || g == 1284 || g == 2564 || g == 2561 || g == 2568 || g == 5124) &&
+        const bool rows_fit = g && 4 * bk * v / (h->cfg.window * 5) + 2 <= bk;   // one staged row per thread
+        if ((g == 1282 || g == 1284 || g == 2564 || g == 2561 || g == 2568 || g == 5124) && rows_fit &&
             (form == 801 || form == 1601 || form == 3200 || form == 6400)) {
             h->relay_block = bk;
             h->relay_v = v;
