@@ -295,9 +295,12 @@ int pmenv_gae(const float* rewards, const float* values, const uint8_t* dones,
               float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam,
               hipStream_t stream);
 /* The same pass with caller-owned device scratch of pmenv_gae_workspace(T, B) bytes
- * (0 when the shape does not use it): rollouts with few envs (B < 16384) and long
- * horizons also split the horizon across workgroups (two launches, the chunks'
- * affine maps kept in `work`). work == NULL or work_bytes too small: as pmenv_gae. */
+ * (0 when the shape does not use it): rollouts with few envs (B < 8192) and long
+ * horizons (T >= 512) also split the horizon across workgroups in ONE launch — each
+ * chunk publishes its affine map and an epoch-tagged flag in `work`, then composes the
+ * later chunks' maps (replaces round 3's two launches). `work` must be 8-B aligned; it
+ * may be reused by later calls (each call tags its flags with a fresh epoch) but not
+ * shared by two calls in flight. work == NULL, too small or misaligned: as pmenv_gae. */
 size_t pmenv_gae_workspace(int32_t T, int32_t B);
 int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones,
                  float* adv, float* ret, int32_t T, int32_t B, float gamma, float lam,
