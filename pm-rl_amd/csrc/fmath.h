@@ -15,19 +15,35 @@
 
 namespace pmenv_dev {
 
+// a 64-bit constant built in an SGPR pair by an opaque scalar move, and the Horner step
+// fma(r, p, c) with c as the scalar operand of a VOP3 v_fma_f64: given a literal or an SGPR
+// addend the compiler emits v_fmac_f64 and copies the addend into a VGPR pair first, two
+// VALU moves per step. Neither asm has side effects (repeated constants are CSE'd across the
+// unrolled calls of a kernel); fma rounds once, so the bits are those of __builtin_fma.
+__device__ __forceinline__ double sconst(uint32_t hi, uint32_t lo) {
+    uint32_t h, l;
+    asm("s_mov_b32 %0, %1" : "=s"(h) : "i"(hi));
+    asm("s_mov_b32 %0, %1" : "=s"(l) : "i"(lo));
+    return __hiloint2double((int)h, (int)l);
+}
+__device__ __forceinline__ double fma_s(double a, double b, double c_sgpr) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c_sgpr));
+    return d;
+}
 __device__ __forceinline__ double exp_f64(double x) {
-    const double t = __builtin_rint(x * 0x1.71547652b82fep+0);
-    double r = __builtin_fma(-0x1.62e42fefa39efp-1, t, x);
-    r = __builtin_fma(-0x1.abc9e3b39803fp-56, t, r);
-    double p = __builtin_fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
-    p = __builtin_fma(r, p, 0x1.71dee623fde64p-19);
-    p = __builtin_fma(r, p, 0x1.a01997c89e6b0p-16);
-    p = __builtin_fma(r, p, 0x1.a01a014761f6ep-13);
-    p = __builtin_fma(r, p, 0x1.6c16c1852b7b0p-10);
-    p = __builtin_fma(r, p, 0x1.1111111122322p-7);
-    p = __builtin_fma(r, p, 0x1.55555555502a1p-5);
-    p = __builtin_fma(r, p, 0x1.5555555555511p-3);
-    p = __builtin_fma(r, p, 0x1.000000000000bp-1);
+    const double t = __builtin_rint(x * sconst(0x3ff71547u, 0x652b82feu));                 // log2 e
+    double r = __builtin_fma(sconst(0xbfe62e42u, 0xfefa39efu), t, x);                        // -ln2 hi
+    r = __builtin_fma(sconst(0xbc7abc9eu, 0x3b39803fu), t, r);                               // -ln2 lo
+    double p = __builtin_fma(sconst(0x3e5ade15u, 0x6a5dcb37u), r, sconst(0x3e928af3u, 0xfca7ab0cu));
+    p = fma_s(r, p, sconst(0x3ec71deeu, 0x623fde64u));
+    p = fma_s(r, p, sconst(0x3efa0199u, 0x7c89e6b0u));
+    p = fma_s(r, p, sconst(0x3f2a01a0u, 0x14761f6eu));
+    p = fma_s(r, p, sconst(0x3f56c16cu, 0x1852b7b0u));
+    p = fma_s(r, p, sconst(0x3f811111u, 0x11122322u));
+    p = fma_s(r, p, sconst(0x3fa55555u, 0x555502a1u));
+    p = fma_s(r, p, sconst(0x3fc55555u, 0x55555511u));
+    p = fma_s(r, p, sconst(0x3fe00000u, 0x0000000bu));
     p = __builtin_fma(r, p, 1.0);
     p = __builtin_fma(r, p, 1.0);
     // t is integral; clamped so the conversion is defined for every input (|t| > 2000 and

@@ -140,3 +140,20 @@ def test_gpu_batch_reward_backward_without_per_row_returns(B, N, norm):
     assert torch.equal(grads[0], grads[1])
     _, _, og = or_batch_reward(a_np, v.cpu().numpy(), p.reshape(B, N).cpu().numpy(), reward="sharpe_ratio", norm=norm)
     np.testing.assert_allclose(grads[0].reshape(B, N).cpu().numpy(), og, rtol=1e-5, atol=1e-6 * (np.abs(og).max() + 1e-30))
+
+
+def test_gpu_batch_reward_bits_match_the_library_of_record():
+    """Kernel rewrites of the batched reward must not move a bit: the reward, per-row
+    returns and gradient at every row form (quad EPL 8 / 16, wave form), reward kind and
+    norm mode, over simplex, raw and NaN-holding batches, against the fingerprints the
+    round-4 library of record wrote (tools/f2_bits.py -> tests/golden/f2_bits.json)."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import f2_bits
+    want = json.load(open(os.path.join(gu.GOLDEN_DIR, "f2_bits.json")))
+    got = f2_bits.fingerprints(str(DEV))
+    assert set(got) == set(want)
+    bad = sorted(k for k in want if got[k] != want[k])
+    assert not bad, f"{len(bad)} of {len(want)} fingerprints moved, e.g. {bad[:5]}"

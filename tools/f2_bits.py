@@ -8,6 +8,8 @@ not change a single bit; the numerics themselves are pinned against the oracle a
 reference's autograd elsewhere).
 
     python tools/f2_bits.py > tests/golden/f2_bits.json
+    python tools/f2_bits.py --lib tools/libpmenv_old.so > old.json     # another build
+    python tools/f2_bits.py --check old.json                            # exit 1 if a bit moved
 """
 import hashlib
 import json
@@ -59,4 +61,19 @@ def fingerprints(dev="cuda:0"):
 
 
 if __name__ == "__main__":
-    print(json.dumps(fingerprints(), indent=1, sort_keys=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", help="load this libpmenv build instead of the in-tree one")
+    ap.add_argument("--check", help="compare against these fingerprints instead of printing")
+    a = ap.parse_args()
+    if a.lib:
+        from pmenv import _abi
+        _abi.LIB_PATH = os.path.abspath(a.lib)
+    got = fingerprints()
+    if not a.check:
+        print(json.dumps(got, indent=1, sort_keys=True))
+        sys.exit(0)
+    want = json.load(open(a.check))
+    bad = sorted(k for k in want if got.get(k) != want[k])
+    print(f"f2_bits: {len(want) - len(bad)} of {len(want)} fingerprints equal" + (f"; moved: {bad[:8]}" if bad else ""))
+    sys.exit(1 if bad or set(got) != set(want) else 0)

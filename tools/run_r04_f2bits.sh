@@ -1,7 +1,7 @@
-# round 4: the batched reward's bit fingerprints from the library of record
+# round 4: the batched reward's bit fingerprints from the library of record (tools/libpmenv_r04l.so,
+# the r04l build) and the in-tree library checked against them; exp_f64 against the device library
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python3 tools/f2_bits.py > gpurun_out/f2_bits.json 2> gpurun_out/f2_bits.err || { tail -5 gpurun_out/f2_bits.err; exit 1; }
-wc -l gpurun_out/f2_bits.json
-timeout -k 10 120 ./tools/exp_check > gpurun_out/exp_check.log 2>&1; echo "exp_check rc=$?"; cat gpurun_out/exp_check.log
+timeout -k 10 300 python3 tools/f2_bits.py --lib tools/libpmenv_r04l.so > gpurun_out/f2_bits.json 2> gpurun_out/f2_bits.err || { tail -5 gpurun_out/f2_bits.err; exit 1; }
+timeout -k 10 300 python3 tools/f2_bits.py --check gpurun_out/f2_bits.json 2>> gpurun_out/f2_bits.err; echo "f2 check rc=$?"
