@@ -652,11 +652,12 @@ def test_gpu_gae_per_env_loop_beyond_tile_offsets():
 
 
 @pytest.mark.parametrize("T,B", [(512, 64), (4096, 512), (1000, 200), (5000, 3), (2048, 4096), (700, 4099),
-                                 (16384, 64)])
+                                 (16384, 64), (513, 1), (1024, 8191), (640, 65), (1280, 1600)])
 def test_gpu_gae_horizon_split_matches_oracle(T, B):
     """The default wrapper path (pmenv_gae_ex): few envs x long horizons split the
-    horizon across workgroups (maps pass + apply pass) — vs the oracle's recursion,
-    with episode ends inside and across the chunk boundaries."""
+    horizon across workgroups in one pass (gae_lookback_kernel: 64- and 128-day chunks,
+    one env, ragged env blocks and horizons, the largest B of the rule) — vs the oracle's
+    recursion, with episode ends inside and across the chunk boundaries."""
     from pmenv import _abi, rollout
     lib = _abi.load()
     assert lib.pmenv_gae_workspace(T, B) > 0
