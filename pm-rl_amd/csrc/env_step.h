@@ -18,7 +18,6 @@
 // kernel does not cover (F < 5, env blocks that are not 16-B granular, rows too long).
 #pragma once
 #include "common.h"
-#include "fmath.h"
 
 namespace pmenv_dev {
 
@@ -119,7 +118,7 @@ __device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scrat
         }
         double z = 0.0;
         for (int n = lane; n < N; n += 64) {
-            double e = exp_f64(s.wv[n] - shift);      // :59 exp(w) (no max-shift in AND mode)
+            double e = exp(s.wv[n] - shift);      // :59 exp(w) (no max-shift in AND mode)
             s.wv[n] = e;
             z += e;
         }
@@ -419,7 +418,7 @@ __device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int
     if (__any(norm)) {
         double shift = 0.0;
         if (p.norm_mode == PMENV_NORM_OR) shift = group_max<L>(act ? a : -INFINITY, lane);
-        const double e = act ? exp_f64(a - shift) : 0.0;             // :59 (no max-shift in AND mode)
+        const double e = act ? exp(a - shift) : 0.0;             // :59 (no max-shift in AND mode)
         const double z = group_sum<L>(e, lane);
         if (norm) w = e / z;                                      // :60
     }

@@ -163,7 +163,7 @@ __device__ __forceinline__ VecMid<A> vec_core(const StepParams& p, int b, int la
         double ex[A], z_loc = 0.0;
 #pragma unroll
         for (int e = 0; e < A; ++e) {
-            ex[e] = act[e] ? exp_f64(x[e] - shift) : 0.0;   // :59 (no max-shift in AND mode)
+            ex[e] = act[e] ? exp(x[e] - shift) : 0.0;   // :59 (no max-shift in AND mode)
             z_loc += ex[e];
         }
         const double z = gred<L, 0>(z_loc, lane);

@@ -12,7 +12,6 @@
 // part of this op.
 #pragma once
 #include "common.h"
-#include "fmath.h"
 
 namespace pmenv_dev {
 
@@ -175,7 +174,7 @@ __device__ __forceinline__ void rows_wave_partial(const float* a, const float* v
             double e[E];
 #pragma unroll
             for (int k = 0; k < E; ++k) {
-                e[k] = lane + 64 * k < N ? exp_f64((double)ra[j][k] - mx) : 0.0;   // exp_f64: the same bits (fmath.h)
+                e[k] = lane + 64 * k < N ? exp((double)ra[j][k] - mx) : 0.0;
                 z += e[k];
             }
             z = wave_sum(z);
@@ -183,10 +182,10 @@ __device__ __forceinline__ void rows_wave_partial(const float* a, const float* v
 #pragma unroll
             for (int k = 0; k < E; ++k) sm += v * ((e[k] * rz) * (double)rp[j][k]);   // torch.softmax(a, dim=1)
         } else {
-            for (int n = lane; n < N; n += 64) z += exp_f64((double)a[(size_t)b * N + n] - mx);
+            for (int n = lane; n < N; n += 64) z += exp((double)a[(size_t)b * N + n] - mx);
             z = wave_sum(z);
             for (int n = lane; n < N; n += 64) {
-                const double w = exp_f64((double)a[(size_t)b * N + n] - mx) / z;     // torch.softmax(a, dim=1)
+                const double w = exp((double)a[(size_t)b * N + n] - mx) / z;     // torch.softmax(a, dim=1)
                 sm += v * (w * (double)p[(size_t)b * N + n]);
             }
         }
@@ -304,7 +303,7 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
     double z = 0.0;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
-        e[i] = g * EPL + i < N ? exp_f64((double)q.a[i] - mx) : 0.0;   // exp_f64: the same bits (fmath.h)
+        e[i] = g * EPL + i < N ? exp((double)q.a[i] - mx) : 0.0;
         z += e[i];
     }
     z = quad_sum(z);
@@ -404,7 +403,7 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_grad_quad_kernel(con
         double e[EPL], z = 0.0;
 #pragma unroll
         for (int i = 0; i < EPL; ++i) {
-            e[i] = g * EPL + i < N ? exp_f64((double)q.a[i] - mx) : 0.0;   // exp_f64: the same bits (fmath.h)
+            e[i] = g * EPL + i < N ? exp((double)q.a[i] - mx) : 0.0;
             z += e[i];
         }
         z = quad_sum(z);
@@ -582,7 +581,7 @@ __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, 
             double e[E], z = 0.0;
 #pragma unroll
             for (int k = 0; k < E; ++k) {
-                e[k] = lane + 64 * k < N ? exp_f64((double)ra[k] - mx) : 0.0;   // exp_f64: the same bits (fmath.h)
+                e[k] = lane + 64 * k < N ? exp((double)ra[k] - mx) : 0.0;
                 z += e[k];
             }
             z = wave_sum(z);
@@ -608,16 +607,16 @@ __global__ __launch_bounds__(256) void batch_reward_grad_kernel(const float* a, 
     for (int n = lane; n < N; n += 64) mx = fmax(mx, (double)a[(size_t)b * N + n]);
     mx = wave_max(mx);
     double z = 0.0;
-    for (int n = lane; n < N; n += 64) z += exp_f64((double)a[(size_t)b * N + n] - mx);
+    for (int n = lane; n < N; n += 64) z += exp((double)a[(size_t)b * N + n] - mx);
     z = wave_sum(z);
     double wg = 0.0;                               // sum_m w_m g_m
     for (int n = lane; n < N; n += 64) {
-        const double w = exp_f64((double)a[(size_t)b * N + n] - mx) / z;
+        const double w = exp((double)a[(size_t)b * N + n] - mx) / z;
         wg += w * (dr * (v * (double)p[(size_t)b * N + n]) / v);
     }
     wg = wave_sum(wg);
     for (int n = lane; n < N; n += 64) {
-        const double w = exp_f64((double)a[(size_t)b * N + n] - mx) / z;
+        const double w = exp((double)a[(size_t)b * N + n] - mx) / z;
         const double gn = dr * (v * (double)p[(size_t)b * N + n]) / v;
         grad_a[(size_t)b * N + n] = (float)(w * (gn - wg));
     }

@@ -1,15 +1,19 @@
-// fmath.h — exp in f64 written out, bit for bit the device library's.
+// fmath.h — TOOLS ONLY: exp in f64 written out, bit for bit the device library's.
 //
 // The ROCm 7.2 device library's exp(double) for gfx950, as hipcc emits it (the sequence read
 // from the compiled kernels): t = rint(x log2 e); a two-constant Cody-Waite reduction
 // r = x - t ln2; a degree-11 polynomial in Horner form, then two fma steps with 1; ldexp by
 // t; +inf above x = 1024 and +0 below -1075 (NaN propagates). Written out with the same
-// constants and the same fma order it gives the same bits for every input
-// (tools/exp_check.hip checks 2^28 inputs on the GPU, the edges of both range checks, rint's
-// half-way points and every special value). What it changes is the code: called from an
-// unrolled loop it runs without a branch per element and its constants are materialised
-// once, where the library call re-materialised ten 64-bit constants into VGPR pairs per
-// call (SQ_INSTS_VALU: profiles/ab_r04/f2_pmc_r04n.txt).
+// constants and the same fma order it gives the same bits for every input: tools/exp_check.hip
+// found 0 mismatches in 2^28 inputs on the GPU (random doubles over the range checks, random
+// bit patterns, both edges, rint's half-way points, the special values), and the batched
+// reward's and the env step's fingerprints (tools/f2_bits.py, tools/step_bits.py) did not move
+// (profiles/ab_r04/exp_r04o/). What it changes is the code: the library call re-materialised
+// ten 64-bit constants into VGPR pairs per call (14 VALU moves); here they are scalar
+// operands. Measured in the batched reward and the env step's softmax (round 4): 112 fewer
+// VALU instructions per wave in batch_reward_rows_quad_kernel (1,117 -> 1,005) and
+// batch_reward_grad_quad_kernel (653 -> 541), and no faster — the rows kernel 8.93 -> 8.96 us,
+// config 5's 8-asset scalar step 38.5 -> 38.1 us — so the product keeps the library call.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -1,4 +1,4 @@
-// exp_check.hip — TOOLS: fmath.h's exp_f64 against the device library's exp(double), bit
+// exp_check.hip — TOOLS: tools/ab/fmath.h's exp_f64 against the device library's exp(double), bit
 // for bit, on the GPU: random doubles over the whole range checks, random bit patterns
 // (every exponent: NaN, inf, subnormals), dense sweeps around the range checks' edges and
 // rint's half-way points (x log2 e near k + 1/2), and the special values.
@@ -11,7 +11,7 @@
 #include <cstdio>
 #include <cstring>
 
-#include "../pm-rl_amd/csrc/fmath.h"
+#include "ab/fmath.h"
 
 __device__ __forceinline__ uint64_t mix(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;

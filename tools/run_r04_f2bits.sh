@@ -1,4 +1,5 @@
-# round 4: the batched reward's bit fingerprints from the library of record (tools/libpmenv_r04l.so,
+# round 4: the batched reward's bit fingerprints from the library of record (tools/libpmenv_r04l.so, a copy
+# of the r04l build kept for the r04o run and removed after it: the product rebuilt to the same binary;
 # the r04l build) and the in-tree library checked against them; exp_f64 against the device library
 set -u
 export TMPDIR=/tmp
