@@ -372,4 +372,20 @@ __global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, cons
     }
 }
 
+// step_relay_kernel whose scalar role raises its waves' issue priority (PMENV_RELAY_PRIO), so
+// the chains the first tiles wait for are not slowed by the tiles' waves on the same CUs
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int PRIO>
+__global__ __launch_bounds__(BLOCK) void step_relay_prio_kernel(StepParams p, RelayParams r, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    __shared__ f4 sh_bar[BLOCK];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    if (blockIdx.x < r.scal) {
+        __builtin_amdgcn_s_setprio(PRIO);
+        relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
+    } else {
+        relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
+    }
+}
+
 }  // namespace pmenv_dev
