@@ -693,6 +693,91 @@ static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv
     free(st_dl); free(st_vv); free(st_al); free(shC); free(shD); free(phase); free(runnable);
 }
 
+/* gae_lookback2_kernel (tools build, PMENV_GAE=lb2): pairs of adjacent chunks (B = 2p, A = 2p + 1)
+ * per workgroup, later pairs dispatched first, at most `resident` workgroups on the device at
+ * once (a finished one frees its slot for the next in dispatch order). Phases: 0 load A and B,
+ * publish A; 1 look back A (waits for chunks > A) and store it; 2 publish B; 3 look back B
+ * (waits for chunks > B) and store it. Every wait must be on a published chunk or on a
+ * workgroup already resident: a schedule in which no resident workgroup can move is a
+ * deadlock, which the kernel must never have. Checks the result against the restatement. */
+static void emulate_gae_lb2(int T, int B, int NW, int U, int resident) {
+    const int S = NW * U, nC = (T + S - 1) / S, nEB = (B + 63) / 64, nP = (nC + 1) / 2, nblk = nP * nEB;
+    float* r = malloc(sizeof(float) * (size_t)T * B);
+    float* v = malloc(sizeof(float) * (size_t)(T + 1) * B);
+    uint8_t* d = malloc((size_t)T * B);
+    float* adv = malloc(sizeof(float) * (size_t)T * B);
+    float* ret = malloc(sizeof(float) * (size_t)T * B);
+    float* oa = malloc(sizeof(float) * (size_t)T * B);
+    float* orr = malloc(sizeof(float) * (size_t)T * B);
+    for (size_t i = 0; i < (size_t)T * B; ++i) { r[i] = (float)nrand(); d[i] = urand() < 0.01; }
+    for (size_t i = 0; i < (size_t)(T + 1) * B; ++i) v[i] = (float)nrand();
+    const double g = 0.99, gl = 0.99 * (double)0.95f;
+    /* per chunk: the published map (C, D per env) and whether it is published */
+    double* mC = malloc(sizeof(double) * (size_t)nC * B);
+    double* mD = malloc(sizeof(double) * (size_t)nC * B);
+    uint8_t* pub = calloc((size_t)nC * nEB, 1);
+    int* phase = calloc((size_t)nblk, sizeof(int));
+    int* runnable = malloc(sizeof(int) * (size_t)nblk);
+    int next = 0, live = 0;                          /* dispatch cursor, resident count */
+    uint8_t* res = calloc((size_t)nblk, 1);
+    /* the chunk's reduction and walk, as the kernel's lanes do them, straight on the arrays */
+    #define LB_MAP(c, eb) do { \
+        for (int lane = 0; lane < 64; ++lane) { const int b_ = (eb) * 64 + lane; if (b_ >= B) continue; \
+            const int s0 = (c) * S, s1 = s0 + S < T ? s0 + S : T; double Ca = 1.0, Da = 0.0; \
+            for (int w = NW - 1; w >= 0; --w) { double C = 1.0, D = 0.0; \
+                for (int u = U - 1; u >= 0; --u) { const int t = s0 + w * U + u; if (t >= s1) continue; \
+                    const double n = d[(size_t)t * B + b_] ? 0.0 : 1.0; \
+                    const double dl = (double)r[(size_t)t * B + b_] + g * n * (double)v[(size_t)(t + 1) * B + b_] - (double)v[(size_t)t * B + b_]; \
+                    D = dl + gl * n * D; C = gl * n * C; } \
+                Da = D + C * Da; Ca = C * Ca; } \
+            mC[(size_t)(c) * B + b_] = Ca; mD[(size_t)(c) * B + b_] = Da; } \
+        pub[(size_t)(c) * nEB + (eb)] = 1; } while (0)
+    #define LB_WALK(c, eb) do { \
+        for (int lane = 0; lane < 64; ++lane) { const int b_ = (eb) * 64 + lane; if (b_ >= B) continue; \
+            double a = 0.0; for (int j = nC - 1; j > (c); --j) a = mD[(size_t)j * B + b_] + mC[(size_t)j * B + b_] * a; \
+            const int s0 = (c) * S, s1 = s0 + S < T ? s0 + S : T; \
+            for (int t = s1 - 1; t >= s0; --t) { const double n = d[(size_t)t * B + b_] ? 0.0 : 1.0; \
+                const double dl = (double)r[(size_t)t * B + b_] + g * n * (double)v[(size_t)(t + 1) * B + b_] - (double)v[(size_t)t * B + b_]; \
+                a = dl + gl * n * a; adv[(size_t)t * B + b_] = (float)a; ret[(size_t)t * B + b_] = (float)(a + (double)v[(size_t)t * B + b_]); } } } while (0)
+    for (;;) {
+        while (live < resident && next < nblk) { res[next++] = 1; ++live; }
+        int nr = 0, left = 0;
+        for (int bi = 0; bi < nblk; ++bi) {
+            if (phase[bi] == 4) continue;
+            ++left;
+            if (!res[bi]) continue;
+            const int pr = nP - 1 - bi / nEB, eb = bi % nEB, cA = 2 * pr + 1, cB = 2 * pr;
+            int ok = 1;
+            if (phase[bi] == 1 || phase[bi] == 3) {
+                const int c = phase[bi] == 1 ? cA : cB;
+                for (int j = c + 1; j < nC && ok; ++j) ok = pub[(size_t)j * nEB + eb];
+            }
+            if (ok) runnable[nr++] = bi;
+        }
+        if (!left) break;
+        CHECK(nr > 0, "gae_lb2: deadlock (T%d B%d %dx%d, %d resident)", T, B, NW, U, resident);
+        if (!nr) break;
+        const int bi = runnable[(int)(urand() * nr)];
+        const int pr = nP - 1 - bi / nEB, eb = bi % nEB, cA = 2 * pr + 1, cB = 2 * pr;
+        switch (phase[bi]) {
+        case 0: if (cA < nC) LB_MAP(cA, eb); phase[bi] = cA < nC ? 1 : 2; break;
+        case 1: LB_WALK(cA, eb); phase[bi] = 2; break;
+        case 2: LB_MAP(cB, eb); phase[bi] = 3; break;
+        default: LB_WALK(cB, eb); phase[bi] = 4; res[bi] = 0; --live; break;
+        }
+    }
+    #undef LB_MAP
+    #undef LB_WALK
+    or_gae(r, v, d, oa, orr, T, B, 0.99f, 0.95f);
+    for (size_t i = 0; i < (size_t)T * B; ++i)
+        if (!(fabsf(adv[i] - oa[i]) <= 1e-5f * (1.0f + fabsf(oa[i])))) {
+            CHECK(0, "gae_lb2: T%d B%d element %zu: %g vs %g", T, B, i, adv[i], oa[i]);
+            break;
+        }
+    free(r); free(v); free(d); free(adv); free(ret); free(oa); free(orr); free(mC); free(mD); free(pub); free(phase);
+    free(runnable); free(res);
+}
+
 static void emulate_gae_lb(int T, int B, int NW, int U) {
     const int seg = NW * U, nC = (T + seg - 1) / seg, nEB = (B + 63) / 64;
     const size_t ws_doubles = (size_t)2 * nC * B + (size_t)nC * nEB;
@@ -817,6 +902,12 @@ int main(void) {
     for (size_t i = 0; i < sizeof gshapes / sizeof gshapes[0]; ++i) {
         emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8);
         emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16);
+    }
+    /* the paired kernel (tools build) under every residency, down to one workgroup */
+    for (int res = 1; res <= 9; res += 4) {
+        emulate_gae_lb2(700, 67, 8, 8, res);
+        emulate_gae_lb2(1000, 130, 8, 16, res);
+        emulate_gae_lb2(130, 5, 8, 8, res);
     }
     {   /* the rule's choice at the shapes the GPU tests run */
         const int rs[][2] = {{512, 64}, {4096, 512}, {1000, 200}, {5000, 3}, {2048, 4096}, {700, 4099}, {16384, 64}};
