@@ -389,7 +389,7 @@ __global__ __launch_bounds__(BLOCK) void step_relay_prio_kernel(StepParams p, Re
 }
 
 // gae_lookback_kernel with TWO adjacent chunks per workgroup (PMENV_GAE=lb2): pair p holds
-// chunk A = 2p + 1 and B = 2p; B's loads are issued before A's look-back, so they are in
+// chunk A = 2p + 1 and B = 2p; B's loads are issued after A's look-back, so they are in
 // flight while A's adv / ret are stored — the read and write phases of the chip overlap
 // instead of all workgroups loading, then all storing. The same look-back and walk as the
 // product kernel (the same bits). Waits: A needs chunks > 2p + 1, B needs A and chunks
@@ -466,18 +466,12 @@ __device__ __forceinline__ void lb_reduce_publish(const LbChunk<NW, U>& k, doubl
     }
 }
 
-// the later chunks' maps composed into the advantage just after chunk c, then the walk
+// the later chunks' maps composed into the advantage just after this wave's segment of chunk c
 template <int NW, int U>
-__device__ __forceinline__ void lb_lookback_walk(const LbChunk<NW, U>& k, const double (&dl)[U], float* adv, float* ret,
-                                                 int T, int B, int c, int w, int lane, int b, bool ok, uint32_t voff,
-                                                 int nEB, int eb, double gl, double (*shC)[64], double (*shD)[64],
-                                                 double (*sxC)[64], double (*sxD)[64], const double* maps, int nC,
-                                                 const uint64_t* flags, uint64_t epoch) {
-    constexpr int S = NW * U;
-    const uint32_t row = (uint32_t)B * 4u;
-    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
-    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
-    const uint32_t voff_st = ok ? voff : 0x80000000u;
+__device__ __forceinline__ double lb_lookback(int B, int c, int w, int lane, int b, bool ok, int nEB, int eb,
+                                              double (*shC)[64], double (*shD)[64], double (*sxC)[64],
+                                              double (*sxD)[64], const double* maps, int nC, const uint64_t* flags,
+                                              uint64_t epoch) {
     const double* mapC = maps;
     const double* mapD = maps + (size_t)nC * B;
     const int nl = nC - 1 - c, m = (nl + NW - 1) / NW;
@@ -521,6 +515,17 @@ __device__ __forceinline__ void lb_lookback_walk(const LbChunk<NW, U>& k, const 
     double a = 0.0;
     for (int j = NW - 1; j >= 0; --j) a = sxD[j][lane] + sxC[j][lane] * a;
     for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
+    return a;
+}
+
+template <int NW, int U>
+__device__ __forceinline__ void lb_walk(const LbChunk<NW, U>& k, const double (&dl)[U], double a, float* adv, float* ret,
+                                        int T, int B, int c, int w, bool ok, uint32_t voff, double gl) {
+    constexpr int S = NW * U;
+    const uint32_t row = (uint32_t)B * 4u;
+    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
+    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
+    const uint32_t voff_st = ok ? voff : 0x80000000u;
     const int seg_start = c * S, seg_end = min(T, seg_start + S);
     const int t0 = seg_start + w * U;
 #pragma unroll
@@ -559,17 +564,19 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback2_kernel(const float* r, 
     if (cA < nC) {
         LbChunk<NW, U> kA;
         lb_load<NW, U>(r, v, dones, T, B, cA, w, voff, kA);
-        lb_load<NW, U>(r, v, dones, T, B, cB, w, voff, kB);      // in flight through A's look-back and stores
         lb_reduce_publish<NW, U>(kA, dl, T, B, cA, w, lane, b, ok, nEB, eb, g, gl, shC, shD, maps, nC, flags, epoch);
-        lb_lookback_walk<NW, U>(kA, dl, adv, ret, T, B, cA, w, lane, b, ok, voff, nEB, eb, gl, shC, shD, sxC, sxD, maps,
-                                nC, flags, epoch);
+        const double a = lb_lookback<NW, U>(B, cA, w, lane, b, ok, nEB, eb, shC, shD, sxC, sxD, maps, nC, flags, epoch);
+        // B's loads go out after the last wait of A (a wait on anything issued later would wait
+        // for them too: vmcnt counts in order), so they are in flight while A's stores drain
+        lb_load<NW, U>(r, v, dones, T, B, cB, w, voff, kB);
+        lb_walk<NW, U>(kA, dl, a, adv, ret, T, B, cA, w, ok, voff, gl);
         __syncthreads();                            // shC / shD / sxC / sxD are reused by B
     } else {
         lb_load<NW, U>(r, v, dones, T, B, cB, w, voff, kB);
     }
     lb_reduce_publish<NW, U>(kB, dl, T, B, cB, w, lane, b, ok, nEB, eb, g, gl, shC, shD, maps, nC, flags, epoch);
-    lb_lookback_walk<NW, U>(kB, dl, adv, ret, T, B, cB, w, lane, b, ok, voff, nEB, eb, gl, shC, shD, sxC, sxD, maps, nC,
-                            flags, epoch);
+    const double a = lb_lookback<NW, U>(B, cB, w, lane, b, ok, nEB, eb, shC, shD, sxC, sxD, maps, nC, flags, epoch);
+    lb_walk<NW, U>(kB, dl, a, adv, ret, T, B, cB, w, ok, voff, gl);
 }
 
 }  // namespace pmenv_dev
