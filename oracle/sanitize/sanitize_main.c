@@ -590,10 +590,8 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
 /* ------------------------------------------------------------ 5. the look-back GAE */
 /* pmenv.hip gae_lb_seg / gae_lb_chunks / pmenv_gae_workspace, restated */
 static int lb_seg(int T, int B) { return (int64_t)((T + 127) / 128) * ((B + 63) / 64) >= 128 ? 128 : 64; }
-static int lb_paired(int T, int B) { return lb_seg(T, B) == 128; }   /* then 2 x 64-day chunks per workgroup */
 static int lb_chunks(int T, int B, int seg) {
     if (B >= 8192 || T < 512 || (size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
-    if (lb_paired(T, B)) seg = 64;
     return (T + seg - 1) / seg;
 }
 
@@ -695,7 +693,7 @@ static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv
     free(st_dl); free(st_vv); free(st_al); free(shC); free(shD); free(phase); free(runnable);
 }
 
-/* gae_lookback2_kernel (the product's form where 128-day chunks would pay): pairs of adjacent chunks (B = 2p, A = 2p + 1)
+/* gae_lookback2_kernel (tools build, PMENV_GAE=lb2 / lb2x16): pairs of adjacent chunks (B = 2p, A = 2p + 1)
  * per workgroup, later pairs dispatched first, at most `resident` workgroups on the device at
  * once (a finished one frees its slot for the next in dispatch order). Phases: 0 load A and B,
  * publish A; 1 look back A (waits for chunks > A) and store it; 2 publish B; 3 look back B
@@ -905,7 +903,7 @@ int main(void) {
         emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8);
         emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16);
     }
-    /* the paired kernel under every residency, down to one workgroup */
+    /* the paired kernel (tools build) under every residency, down to one workgroup */
     for (int res = 1; res <= 9; res += 4) {
         emulate_gae_lb2(700, 67, 8, 8, res);
         emulate_gae_lb2(1000, 130, 8, 16, res);

@@ -841,21 +841,17 @@ namespace {
 // chunk length S = NW x U days: 8 waves x 16 days where that still makes 128 workgroups, else
 // 8 x 8 (fewer composes per chunk against fewer workgroups). T x B = 4,096 x 512: 9.85 us for
 // 128-day chunks against 12.7 for 64-day; 16,384 x 64: 10.3 vs 11.2; 2,048 x 4,096: 31.5 vs
-// 32.4; 1,000 x 200 (32 workgroups): 8.7 vs 7.7 (profiles/ab_r04/gae_geom_r04h.err).
-// Where 128-day chunks pay, two adjacent 64-day chunks per workgroup instead
-// (gae_lookback2_kernel: the same workgroups, the second chunk's loads in flight while the
-// first chunk's adv / ret drain)
+// 32.4; 1,000 x 200 (32 workgroups): 8.7 vs 7.7 (profiles/ab_r04/gae_geom_r04h.err)
 int gae_lb_seg(int32_t T, int32_t B) {
     const int64_t wg16 = (int64_t)((T + 127) / 128) * ((B + 63) / 64);
     return wg16 >= 128 ? 128 : 64;
 }
-bool gae_lb_paired(int32_t T, int32_t B) { return gae_lb_seg(T, B) == 128; }
 int gae_lb_chunks(int32_t T, int32_t B) {
     // from 8,192 envs (128 workgroups) the one-pass tile with nt stores wins: 2,048 x 8,192
     // 59.0 vs 74.2 us for the round-3 split (profiles/rows_r03af/rows_r03af.json)
     if (B >= 8192 || T < 512) return 0;
     if ((size_t)(T + 1) * (size_t)B * 4u >= (1ull << 31)) return 0;
-    const int seg = gae_lb_paired(T, B) ? 64 : gae_lb_seg(T, B);
+    const int seg = gae_lb_seg(T, B);
     return (T + seg - 1) / seg;
 }
 // the look-back flags' epochs: a process-wide counter from a clock-mixed start, so a flag word
@@ -887,9 +883,9 @@ int pmenv_gae_ex(const float* rewards, const float* values, const uint8_t* dones
         return pmenv_gae(rewards, values, dones, adv, ret, T, B, gamma, lam, stream);
     const int neb = (B + 63) / 64;
     uint64_t* flags = reinterpret_cast<uint64_t*>(work + (size_t)2 * n * B);
-    if (gae_lb_paired(T, B))
-        gae_lookback2_kernel<8, 8><<<(unsigned)(((n + 1) / 2) * neb), 512, 0, stream>>>(
-            rewards, values, dones, adv, ret, T, B, gamma, lam, n, work, flags, gae_next_epoch());
+    if (gae_lb_seg(T, B) == 128)
+        gae_lookback_kernel<8, 16><<<(unsigned)(n * neb), 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B,
+                                                                          gamma, lam, n, work, flags, gae_next_epoch());
     else
         gae_lookback_kernel<8, 8><<<(unsigned)(n * neb), 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B,
                                                                          gamma, lam, n, work, flags, gae_next_epoch());

@@ -249,53 +249,52 @@ __global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const fl
 // ret (nt stores: written once, read by the learner later). Inputs are read once (17 B
 // per element, against 26 for the maps + apply split) and a workgroup only waits for
 // chunks dispatched before it, which never wait for it, so every wait ends.
-// The pieces (a chunk's registers, its load, reduction and publication, the look-back and the
-// walk) are shared with gae_lookback2_kernel below.
 template <int NW, int U>
-struct LbChunk {
-    float vv[U + 1], rr[U];
-    uint32_t alive;
-};
-
-template <int NW, int U>
-__device__ __forceinline__ void lb_load(const float* r, const float* v, const uint8_t* dones, int T, int B, int c,
-                                        int w, uint32_t voff, LbChunk<NW, U>& k) {
+__global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, const float* v, const uint8_t* dones,
+                                                              float* adv, float* ret, int T, int B, float gamma,
+                                                              float lam, int nC, double* maps, uint64_t* flags,
+                                                              uint64_t epoch) {
+    __shared__ double shC[NW][64], shD[NW][64];     // the chunk's per-wave maps
+    __shared__ double sxC[NW][64], sxD[NW][64];     // the later chunks' maps, a part per wave
     constexpr int S = NW * U;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nEB = (B + 63) / 64;
+    const int c = nC - 1 - (int)(blockIdx.x / (unsigned)nEB);
+    const int eb = (int)(blockIdx.x % (unsigned)nEB);
+    const int b = eb * 64 + lane;
+    const bool ok = b < B;
+    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
     const uint32_t row = (uint32_t)B * 4u;
     const auto rs_r = make_rsrc(r, (uint32_t)T * row);
     const auto rs_v = make_rsrc(v, (uint32_t)(T + 1) * row);
     const auto rs_d = make_rsrc(dones ? (const void*)dones : (const void*)r, dones ? (uint32_t)T * (uint32_t)B : 0u);
+    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
+    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
+    const uint32_t voff_st = ok ? voff : 0x80000000u;
+    const double g = (double)gamma, gl = (double)gamma * (double)lam;
     const int seg_start = c * S, seg_end = min(T, seg_start + S);
     const int t0 = seg_start + w * U;
+    float vv[U + 1], rr[U];
+    uint32_t alive = 0;
 #pragma unroll
-    for (int u = 0; u <= U; ++u) {
+    for (int u = 0; u <= U; ++u) {                // v has T + 1 rows: row seg_end closes the chunk
         const uint32_t t = (uint32_t)min(t0 + u, seg_end);
-        k.vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
+        vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
     }
-    k.alive = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
-        k.rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
+        rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
         const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
-        k.alive |= (dn ? 0u : 1u) << u;
+        alive |= (dn ? 0u : 1u) << u;
     }
-}
-
-// reduce the chunk (dl kept), publish its map and flag; returns nothing, fills dl and LDS
-template <int NW, int U>
-__device__ __forceinline__ void lb_reduce_publish(const LbChunk<NW, U>& k, double (&dl)[U], int T, int B, int c, int w,
-                                                  int lane, int b, bool ok, int nEB, int eb, double g, double gl,
-                                                  double (*shC)[64], double (*shD)[64], double* maps, int nC,
-                                                  uint64_t* flags, uint64_t epoch) {
-    constexpr int S = NW * U;
-    const int seg_start = c * S, seg_end = min(T, seg_start + S);
-    const int t0 = seg_start + w * U;
+    double dl[U];
     double C = 1.0, D = 0.0;
 #pragma unroll
     for (int u = U - 1; u >= 0; --u) {
-        const double n = (k.alive >> u) & 1u ? 1.0 : 0.0;
-        dl[u] = (double)k.rr[u] + g * n * (double)k.vv[u + 1] - (double)k.vv[u];
+        const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+        dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
         if (t0 + u < seg_end) {
             D = dl[u] + gl * n * D;
             C = gl * n * C;
@@ -306,7 +305,7 @@ __device__ __forceinline__ void lb_reduce_publish(const LbChunk<NW, U>& k, doubl
     __syncthreads();
     double* mapC = maps;
     double* mapD = maps + (size_t)nC * B;
-    if (w == 0) {
+    if (w == 0) {                                 // publish the chunk's map
         double Ca = 1.0, Da = 0.0;
         for (int j = NW - 1; j >= 0; --j) {
             Da = shD[j][lane] + shC[j][lane] * Da;
@@ -317,50 +316,42 @@ __device__ __forceinline__ void lb_reduce_publish(const LbChunk<NW, U>& k, doubl
             __hip_atomic_store(mapD + (size_t)c * B + b, Da, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));
-        if (lane == 0) __hip_atomic_store(flags + (size_t)c * nEB + eb, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));          // vmcnt(0): the maps are written
+        if (lane == 0) __hip_atomic_store(flags + (size_t)c * nEB + eb, epoch, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-// the later chunks' maps composed into the advantage just after this wave's segment of chunk c
-template <int NW, int U>
-__device__ __forceinline__ double lb_lookback(int B, int c, int w, int lane, int b, bool ok, int nEB, int eb,
-                                              double (*shC)[64], double (*shD)[64], double (*sxC)[64],
-                                              double (*sxD)[64], const double* maps, int nC, const uint64_t* flags,
-                                              uint64_t epoch) {
-    const double* mapC = maps;
-    const double* mapD = maps + (size_t)nC * B;
+    // this wave's part of the later chunks: [j0, j1)
     const int nl = nC - 1 - c, m = (nl + NW - 1) / NW;
     const int j0 = c + 1 + w * m, j1 = min(nC, j0 + m);
     double Cw = 1.0, Dw = 0.0;
     if (j0 < j1) {
         for (int base = j0; base < j1; base += 64) {
             const int j = base + lane;
-            bool ready = j >= j1 || __hip_atomic_load(const_cast<uint64_t*>(flags) + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
+            bool ready = j >= j1 || __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT) == epoch;
             while (!__all(ready)) {
                 __builtin_amdgcn_s_sleep(1);
                 if (!ready)
-                    ready = __hip_atomic_load(const_cast<uint64_t*>(flags) + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
+                    ready = __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT) == epoch;
             }
         }
         __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const size_t bb = (size_t)(ok ? b : B - 1);
-        for (int hi = j1 - 1; hi >= j0; hi -= 8) {
+        for (int hi = j1 - 1; hi >= j0; hi -= 8) {    // eight maps in flight, composed in order
             double cq[8], dq[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int j = max(hi - q, j0);
-                cq[q] = __hip_atomic_load(const_cast<double*>(mapC) + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                dq[q] = __hip_atomic_load(const_cast<double*>(mapD) + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 0; k < 8; ++k) {
+                const int j = max(hi - k, j0);
+                cq[k] = __hip_atomic_load(mapC + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dq[k] = __hip_atomic_load(mapD + (size_t)j * B + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (hi - q >= j0) {
-                    Dw = dq[q] + cq[q] * Dw;
-                    Cw = cq[q] * Cw;
+            for (int k = 0; k < 8; ++k) {
+                if (hi - k >= j0) {
+                    Dw = dq[k] + cq[k] * Dw;
+                    Cw = cq[k] * Cw;
                 }
             }
         }
@@ -368,102 +359,20 @@ __device__ __forceinline__ double lb_lookback(int B, int c, int w, int lane, int
     sxC[w][lane] = Cw;
     sxD[w][lane] = Dw;
     __syncthreads();
-    double a = 0.0;
+    double a = 0.0;                               // the advantage just after the chunk
     for (int j = NW - 1; j >= 0; --j) a = sxD[j][lane] + sxC[j][lane] * a;
     for (int j = NW - 1; j > w; --j) a = shD[j][lane] + shC[j][lane] * a;
-    return a;
-}
-
-template <int NW, int U>
-__device__ __forceinline__ void lb_walk(const LbChunk<NW, U>& k, const double (&dl)[U], double a, float* adv, float* ret,
-                                        int T, int B, int c, int w, bool ok, uint32_t voff, double gl) {
-    constexpr int S = NW * U;
-    const uint32_t row = (uint32_t)B * 4u;
-    const auto rs_adv = make_rsrc(adv, (uint32_t)T * row);
-    const auto rs_ret = make_rsrc(ret, (uint32_t)T * row);
-    const uint32_t voff_st = ok ? voff : 0x80000000u;
-    const int seg_start = c * S, seg_end = min(T, seg_start + S);
-    const int t0 = seg_start + w * U;
 #pragma unroll
     for (int u = U - 1; u >= 0; --u) {
         const int t = t0 + u;
         if (t < seg_end) {
-            const double n = (k.alive >> u) & 1u ? 1.0 : 0.0;
+            const double n = (alive >> u) & 1u ? 1.0 : 0.0;
             a = dl[u] + gl * n * a;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)a), rs_adv, voff_st, (uint32_t)t * row, 2);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)k.vv[u])), rs_ret, voff_st,
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(a + (double)vv[u])), rs_ret, voff_st,
                                                   (uint32_t)t * row, 2);
         }
     }
-}
-
-template <int NW, int U>
-__global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, const float* v, const uint8_t* dones,
-                                                              float* adv, float* ret, int T, int B, float gamma,
-                                                              float lam, int nC, double* maps, uint64_t* flags,
-                                                              uint64_t epoch) {
-    __shared__ double shC[NW][64], shD[NW][64];     // the chunk's per-wave maps
-    __shared__ double sxC[NW][64], sxD[NW][64];     // the later chunks' maps, a part per wave
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nEB = (B + 63) / 64;
-    const int c = nC - 1 - (int)(blockIdx.x / (unsigned)nEB);
-    const int eb = (int)(blockIdx.x % (unsigned)nEB);
-    const int b = eb * 64 + lane;
-    const bool ok = b < B;
-    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
-    const double g = (double)gamma, gl = (double)gamma * (double)lam;
-    LbChunk<NW, U> k;
-    double dl[U];
-    lb_load<NW, U>(r, v, dones, T, B, c, w, voff, k);
-    lb_reduce_publish<NW, U>(k, dl, T, B, c, w, lane, b, ok, nEB, eb, g, gl, shC, shD, maps, nC, flags, epoch);
-    const double a = lb_lookback<NW, U>(B, c, w, lane, b, ok, nEB, eb, shC, shD, sxC, sxD, maps, nC, flags, epoch);
-    lb_walk<NW, U>(k, dl, a, adv, ret, T, B, c, w, ok, voff, gl);
-}
-
-// gae_lookback_kernel with TWO adjacent chunks per workgroup (PMENV_GAE=lb2): pair p holds
-// chunk A = 2p + 1 and B = 2p; B's loads are issued after A's look-back, so they are in
-// flight while A's adv / ret are stored — the read and write phases of the chip overlap
-// instead of all workgroups loading, then all storing. The same look-back and walk as the
-// product kernel (the same bits). Waits: A needs chunks > 2p + 1, B needs A and chunks
-// > 2p + 1 — all published by this workgroup or by pairs dispatched before it (later pairs
-// first), so every wait ends whatever the residency.
-template <int NW, int U>
-__global__ __launch_bounds__(64 * NW) void gae_lookback2_kernel(const float* r, const float* v, const uint8_t* dones,
-                                                               float* adv, float* ret, int T, int B, float gamma,
-                                                               float lam, int nC, double* maps, uint64_t* flags,
-                                                               uint64_t epoch) {
-    __shared__ double shC[NW][64], shD[NW][64];
-    __shared__ double sxC[NW][64], sxD[NW][64];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nEB = (B + 63) / 64;
-    const int nP = (nC + 1) / 2;                   // pairs: B chunk 2p, A chunk 2p + 1 (if < nC)
-    const int pr = nP - 1 - (int)(blockIdx.x / (unsigned)nEB);
-    const int eb = (int)(blockIdx.x % (unsigned)nEB);
-    const int b = eb * 64 + lane;
-    const bool ok = b < B;
-    const uint32_t voff = (uint32_t)(ok ? b : B - 1) * 4u;
-    const double g = (double)gamma, gl = (double)gamma * (double)lam;
-    const int cA = 2 * pr + 1, cB = 2 * pr;
-    LbChunk<NW, U> kB;
-    double dl[U];
-    if (cA < nC) {
-        LbChunk<NW, U> kA;
-        lb_load<NW, U>(r, v, dones, T, B, cA, w, voff, kA);
-        lb_reduce_publish<NW, U>(kA, dl, T, B, cA, w, lane, b, ok, nEB, eb, g, gl, shC, shD, maps, nC, flags, epoch);
-        const double a = lb_lookback<NW, U>(B, cA, w, lane, b, ok, nEB, eb, shC, shD, sxC, sxD, maps, nC, flags, epoch);
-        // B's loads go out after the last wait of A (a wait on anything issued later would wait
-        // for them too: vmcnt counts in order), so they are in flight while A's stores drain
-        lb_load<NW, U>(r, v, dones, T, B, cB, w, voff, kB);
-        lb_walk<NW, U>(kA, dl, a, adv, ret, T, B, cA, w, ok, voff, gl);
-        __syncthreads();                            // shC / shD / sxC / sxD are reused by B
-    } else {
-        lb_load<NW, U>(r, v, dones, T, B, cB, w, voff, kB);
-    }
-    lb_reduce_publish<NW, U>(kB, dl, T, B, cB, w, lane, b, ok, nEB, eb, g, gl, shC, shD, maps, nC, flags, epoch);
-    const double a = lb_lookback<NW, U>(B, cB, w, lane, b, ok, nEB, eb, shC, shD, sxC, sxD, maps, nC, flags, epoch);
-    lb_walk<NW, U>(kB, dl, a, adv, ret, T, B, cB, w, ok, voff, gl);
 }
 
 constexpr int kMomBlock = 256;
