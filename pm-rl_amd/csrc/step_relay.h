@@ -94,8 +94,9 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
 // needing neither bar nor w' before reading the relay words, and the last-day / slot chunks
 // after, ran 1.1-1.4x slower: the deferred 16-B chunks leave partly written lines between the
 // two store waves — profiles/ab_r04/relay_split_r04s.err.)
-// OUT: double-buffered (the chunks past the tile read straight from obs).
-template <int BLOCK, int V, int POL, bool OUT>
+// OUT: double-buffered (the chunks past the tile read straight from obs). WAIT = false (tools
+// ablation only: the stream's cost inside this kernel, wrong results): no wait for the words.
+template <int BLOCK, int V, int POL, bool OUT, bool WAIT = true>
 __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
                                            f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
     constexpr int kAux = POL == 1 ? 2 : 0;
@@ -129,7 +130,7 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     const int32_t kc = r.kp_in[b];
     // w': relayed by the scalar blocks placed before this tile
     uint64_t ww = relay_get(r.w + g);
-    bool ready = !mine || (uint32_t)(ww >> 32) == r.epoch;
+    bool ready = !WAIT || !mine || (uint32_t)(ww >> 32) == r.epoch;
     while (!__all(ready)) {
         __builtin_amdgcn_s_sleep(2);
         if (!ready) {

@@ -580,4 +580,17 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback2_kernel(const float* r, 
     lb_walk<NW, U>(kB, dl, a, adv, ret, T, B, cB, w, ok, voff, gl);
 }
 
+// timing-only ablation of the relayed step (PMENV_RELAY_PRIO=2): the scalar blocks exit at
+// once and the tiles do not wait for the relay words — the stream's own cost inside the
+// relay kernel (wrong results: a measurement of the wait, never a path)
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA>
+__global__ __launch_bounds__(BLOCK) void step_relay_nowait_kernel(StepParams p, RelayParams r, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    __shared__ f4 sh_bar[BLOCK];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    if (blockIdx.x < r.scal) return;
+    relay_tile<BLOCK, V, POL, OUT, false>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
+}
+
 }  // namespace pmenv_dev

@@ -561,6 +561,11 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
     const Tools* t = tools(h);
+    if (t && t->relay_prio == 2 && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {   // the no-wait ablation
+        if (out) step_relay_nowait_kernel<256, 2, 0, true, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
+        else step_relay_nowait_kernel<256, 2, 0, false, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
+        return true;
+    }
     if (t && t->relay_prio && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {   // PMENV_RELAY_PRIO
         if (out) step_relay_prio_kernel<256, 2, 0, true, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
         else step_relay_prio_kernel<256, 2, 0, false, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
