@@ -96,7 +96,7 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
 // two store waves — profiles/ab_r04/relay_split_r04s.err.)
 // OUT: double-buffered (the chunks past the tile read straight from obs). WAIT = false (tools
 // ablation only: the stream's cost inside this kernel, wrong results): no wait for the words.
-template <int BLOCK, int V, int POL, bool OUT, bool WAIT = true>
+template <int BLOCK, int V, int POL, bool OUT, bool WAIT = true, int ABL = 0>
 __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
                                            f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
     constexpr int kAux = POL == 1 ? 2 : 0;
@@ -126,10 +126,15 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
     const float* barb = env_bar(p, (int)b);                         // null: a day outside the series
     const float nanv = __int_as_float(0x7fc00000);
-    const f4 xb = barb ? *reinterpret_cast<const f4*>(barb + (size_t)n * 4) : f4{nanv, nanv, nanv, nanv};
-    const int32_t kc = r.kp_in[b];
-    // w': relayed by the scalar blocks placed before this tile
-    uint64_t ww = relay_get(r.w + g);
+    f4 xb = f4{nanv, nanv, nanv, nanv};
+    int32_t kc = 0;
+    uint64_t ww = 0;
+    if (!(ABL & 1) || mine) {                                       // ABL & 1 (tools): only the staging threads load
+        if (barb) xb = *reinterpret_cast<const f4*>(barb + (size_t)n * 4);
+        kc = r.kp_in[b];
+        // w': relayed by the scalar blocks placed before this tile
+        ww = relay_get(r.w + g);
+    }
     bool ready = !WAIT || !mine || (uint32_t)(ww >> 32) == r.epoch;
     while (!__all(ready)) {
         __builtin_amdgcn_s_sleep(2);
@@ -166,7 +171,7 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
             xwp = sh_wp[i];
         });
         buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
-        if (first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;
+        if (!(ABL & 2) && first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;   // ABL & 2: timing only
     }
 }
 

@@ -593,4 +593,16 @@ __global__ __launch_bounds__(BLOCK) void step_relay_nowait_kernel(StepParams p, 
     relay_tile<BLOCK, V, POL, OUT, false>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
 }
 
+// relay_tile ablations (PMENV_RELAY_PRIO = 4 + ABL): ABL 1 only the staging threads issue the
+// side loads (the same results), 2 no halo_out stores (timing only), 3 both
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int ABL>
+__global__ __launch_bounds__(BLOCK) void step_relay_abl_kernel(StepParams p, RelayParams r, uint32_t qtot) {
+    __shared__ f4 sh4[BLOCK * V + 2];
+    __shared__ f4 sh_bar[BLOCK];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    if (blockIdx.x < r.scal) relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
+    else relay_tile<BLOCK, V, POL, OUT, true, ABL>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
+}
+
 }  // namespace pmenv_dev

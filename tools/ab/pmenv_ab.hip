@@ -561,6 +561,20 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
     const Tools* t = tools(h);
+    if (t && t->relay_prio >= 5 && t->relay_prio <= 7 && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {
+        const int abl = t->relay_prio - 4;
+        if (abl == 1) {
+            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 1><<<grid, 256, 0, stream>>>(p, r, q);
+            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 1><<<grid, 256, 0, stream>>>(p, r, q);
+        } else if (abl == 2) {
+            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 2><<<grid, 256, 0, stream>>>(p, r, q);
+            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 2><<<grid, 256, 0, stream>>>(p, r, q);
+        } else {
+            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
+            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
+        }
+        return true;
+    }
     if (t && t->relay_prio == 2 && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {   // the no-wait ablation
         if (out) step_relay_nowait_kernel<256, 2, 0, true, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
         else step_relay_nowait_kernel<256, 2, 0, false, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
