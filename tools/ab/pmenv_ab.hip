@@ -678,10 +678,10 @@ bool gae(const float* rewards, const float* values, const uint8_t* dones, float*
         return true;
     }
     if (k && (!strcmp(k, "lb16") || !strcmp(k, "lb4x16") || !strcmp(k, "lb16x4") || !strcmp(k, "lb8o1") ||
-              !strcmp(k, "lb4o1") || !strcmp(k, "lb16o1"))) {   // look-back geometries; o1: one workgroup per CU
+              !strcmp(k, "lb4o1") || !strcmp(k, "lb16o1") || !strcmp(k, "lb16x8"))) {   // look-back geometries; o1: one workgroup per CU
         const bool o1 = strstr(k, "o1") != nullptr;
-        const int nw = !strcmp(k, "lb4x16") ? 4 : !strcmp(k, "lb16x4") ? 16 : 8;
-        const int u = !strcmp(k, "lb16x4") || !strcmp(k, "lb4o1") ? 4 : !strcmp(k, "lb8o1") ? 8 : 16;
+        const int nw = !strcmp(k, "lb4x16") ? 4 : (!strcmp(k, "lb16x4") || !strcmp(k, "lb16x8")) ? 16 : 8;
+        const int u = !strcmp(k, "lb16x4") || !strcmp(k, "lb4o1") ? 4 : (!strcmp(k, "lb8o1") || !strcmp(k, "lb16x8")) ? 8 : 16;
         const int seg = nw * u, n = (T + seg - 1) / seg, neb = (B + 63) / 64;
         static double* ws = nullptr;
         static size_t ws_n = 0;
@@ -705,6 +705,7 @@ bool gae(const float* rewards, const float* values, const uint8_t* dones, float*
         else if (o1 && u == 8) gae_lookback_kernel<8, 8><<<g, 512, pad, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
         else if (o1) gae_lookback_kernel<8, 16><<<g, 512, pad, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
         else if (nw == 4) gae_lookback_kernel<4, 16><<<g, 256, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        else if (nw == 16 && u == 8) gae_lookback_kernel<16, 8><<<g, 1024, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
         else if (nw == 16) gae_lookback_kernel<16, 4><<<g, 1024, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
         else gae_lookback_kernel<8, 16><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
         *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
