@@ -130,6 +130,42 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(cons
         final_fold(B, kind, norm, scale, work, reward_out, nblk);
 }
 
+// the ticketed one-launch forward without a fence or a per-call memset (PMENV_BR_TICKET): the
+// record goes out with agent-scope atomic stores, thread 0 waits for them (vmcnt(0), no L2
+// write-back) and draws a ticket from a 64-bit word {epoch, count} — the first block of a call
+// finds an older epoch and restarts the count (a CAS loop) — and the block that draws the last
+// ticket folds the records through agent-scope atomic loads (final_fold<true>: the same bits)
+__device__ __forceinline__ bool drew_last_ticket_epoch(uint64_t* t, uint32_t epoch, uint32_t nblk) {
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));          // vmcnt(0): the record is written
+        uint64_t old = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nw;
+        do {
+            nw = (uint32_t)(old >> 32) == epoch ? old + 1 : (((uint64_t)epoch << 32) | 1u);
+        } while (!__hip_atomic_compare_exchange_strong(t, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+        last = (uint32_t)nw == nblk ? 1u : 0u;
+    }
+    __syncthreads();
+    return last != 0;
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_ticket_kernel(const float* a, const float* v_prev,
+                                                                              const float* p, int B, int N, int kind,
+                                                                              int norm, double scale, double* work,
+                                                                              float* reward_out, uint64_t* ticket,
+                                                                              uint32_t epoch) {
+    __shared__ double rec_w[4][kPartStride];
+    const int nblk = (int)gridDim.x;
+    rows_quad_partial<EPL, true>(a, v_prev, p, B, N, kind, norm, work, rec_w, (int)blockIdx.x, nblk);
+    if (!drew_last_ticket_epoch(ticket, epoch, (uint32_t)nblk)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    final_fold<true>(B, kind, norm, scale, work, reward_out, nblk);
+}
+
 template <int EPL, int FENCE>
 __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_rows_kernel(const float* a, const float* v_prev,
                                                                             const float* p, int B, int N, int kind,

@@ -907,6 +907,25 @@ bool metrics(const double* returns, const double* values, const float* weights, 
 bool batch_reward_forward(const float* a, const float* v_prev, const float* p, int32_t B, int32_t N,
                           int32_t reward_kind, int32_t norm, double scale, double* work, float* reward_out,
                           float* ret_out, hipStream_t stream, int* rc) {
+    if (knob("PMENV_BR_TICKET") && N <= kQuadMaxN) {   // one launch, an epoch-tagged ticket, no fence
+        static uint64_t* ticket = nullptr;
+        static uint32_t epoch = 0x7e11u;
+        if (!ticket) {
+            if (hipMalloc(&ticket, 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
+            (void)hipMemset(ticket, 0, 8);
+        }
+        if (++epoch == 0) epoch = 1;
+        const int nblk = (B + kQuadRows - 1) / kQuadRows;
+        if (N <= 32)
+            batch_reward_fwd_ticket_kernel<8><<<(unsigned)nblk, kTrainBlock, 0, stream>>>(
+                a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, ticket, epoch);
+        else
+            batch_reward_fwd_ticket_kernel<16><<<(unsigned)nblk, kTrainBlock, 0, stream>>>(
+                a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, ticket, epoch);
+        if (ret_out) batch_reward_select_kernel<<<(B + 255) / 256, 256, 0, stream>>>(B, norm, work, ret_out);
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (knob("PMENV_BR_RELAY") && N <= kQuadMaxN) {   // one launch, flags instead of a ticket
         static uint64_t* flags = nullptr;
         static size_t nflags = 0;
