@@ -132,21 +132,19 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_quad_kernel(cons
 
 // the ticketed one-launch forward without a fence or a per-call memset (PMENV_BR_TICKET): the
 // record goes out with agent-scope atomic stores, thread 0 waits for them (vmcnt(0), no L2
-// write-back) and draws a ticket from a 64-bit word {epoch, count} — the first block of a call
-// finds an older epoch and restarts the count (a CAS loop) — and the block that draws the last
-// ticket folds the records through agent-scope atomic loads (final_fold<true>: the same bits)
+// write-back) and draws a ticket with one fetch-add on a 64-bit word {epoch, count}; the block
+// that draws count nblk - 1 folds the records through agent-scope atomic loads
+// (final_fold<true>: the same bits) and re-arms the word as {epoch + 1, 0} for the next call
+// (the host steps the epoch by one per call; the word starts as {first epoch, 0}). (A CAS loop
+// that restarted the count on a stale epoch serialised 1,024 blocks: 2.7 ms at 65,536 rows.)
 __device__ __forceinline__ bool drew_last_ticket_epoch(uint64_t* t, uint32_t epoch, uint32_t nblk) {
     __shared__ uint32_t last;
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_s_waitcnt(0 | (0x7 << 4) | (0xf << 8));          // vmcnt(0): the record is written
-        uint64_t old = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nw;
-        do {
-            nw = (uint32_t)(old >> 32) == epoch ? old + 1 : (((uint64_t)epoch << 32) | 1u);
-        } while (!__hip_atomic_compare_exchange_strong(t, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT));
-        last = (uint32_t)nw == nblk ? 1u : 0u;
+        const uint64_t old = __hip_atomic_fetch_add(t, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (uint32_t)(old >> 32) == epoch && (uint32_t)old == nblk - 1u ? 1u : 0u;
     }
     __syncthreads();
     return last != 0;
@@ -164,6 +162,8 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_fwd_ticket_kernel(co
     if (!drew_last_ticket_epoch(ticket, epoch, (uint32_t)nblk)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     final_fold<true>(B, kind, norm, scale, work, reward_out, nblk);
+    if (threadIdx.x == 0)
+        __hip_atomic_store(ticket, (uint64_t)(epoch + 1u) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int EPL, int FENCE>

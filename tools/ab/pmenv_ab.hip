@@ -910,11 +910,12 @@ bool batch_reward_forward(const float* a, const float* v_prev, const float* p, i
     if (knob("PMENV_BR_TICKET") && N <= kQuadMaxN) {   // one launch, an epoch-tagged ticket, no fence
         static uint64_t* ticket = nullptr;
         static uint32_t epoch = 0x7e11u;
-        if (!ticket) {
+        if (!ticket) {                            // armed once as {first epoch, 0}; each call re-arms it
             if (hipMalloc(&ticket, 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
-            (void)hipMemset(ticket, 0, 8);
+            const uint64_t armed = (uint64_t)(epoch + 1u) << 32;
+            (void)hipMemcpy(ticket, &armed, 8, hipMemcpyHostToDevice);
         }
-        if (++epoch == 0) epoch = 1;
+        ++epoch;
         const int nblk = (B + kQuadRows - 1) / kQuadRows;
         if (N <= 32)
             batch_reward_fwd_ticket_kernel<8><<<(unsigned)nblk, kTrainBlock, 0, stream>>>(
