@@ -35,7 +35,8 @@ extern "C" {
 /* 2: pmenv_window_written / pmenv_state_written and PMENV_STEP_PATH_RELAY added;
  *    pmenv_cfg_default's ret_mode is PMENV_RET_GROSS (trading_env.py:88 for every reward
  *    kind; was AUTO in 1) */
-#define PMENV_ABI_VERSION 2
+/* 3: pmenv_step_host / pmenv_reset_host (host buffers, the reference driver's call shape) */
+#define PMENV_ABI_VERSION 3
 
 /* Opaque HIP stream (identical to HIP's own typedef); NULL = default stream. */
 typedef struct ihipStream_t* hipStream_t;
@@ -190,6 +191,22 @@ typedef struct pmenv_step_args {
 int pmenv_step_ex(pmenv* h, const pmenv_step_args* args, hipStream_t stream);
 int pmenv_step(pmenv* h, const float* action, const float* prices, const float* bar,
                float* obs, float* reward, hipStream_t stream);
+
+/* TradingEnv.step / reset with HOST buffers — the call shape of the reference's own driver,
+ * which hands the env the data loader's CPU tensors (train/on_policy.py:59-67, :81-89;
+ * trading_env.py:21-41, :44-105). Surface contract only: action [B, N], prices [B, N] and
+ * the caller's window obs [B, N, W, F] are host memory (pageable is fine); channel F-1 of
+ * obs is rewritten in place, exactly as trading_env.py:32 / :103 do. Outputs, each
+ * optional (NULL): reward [B] f32, value [B] f64 (TradingEnv.value after the call), ret [B]
+ * f64 (info["returns"]), weights [B, N] f32 (info["actions"]).
+ * The step kernel reads the action, the prices and the window's last closes (N floats per
+ * env) straight from pinned, device-mapped staging, and writes the [N, W] weight channel
+ * and the outputs back into it; the market channels never cross PCIe. SYNCHRONOUS: one
+ * stream sync per call, after which the outputs are in place (so not graph-capturable).
+ * The staging is allocated on the first call. */
+int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* obs, float* reward, double* value,
+                    double* ret, float* weights, hipStream_t stream);
+int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream);
 
 /* Which kernels the advance path launches for this handle's shape (diagnostics):
  * "<obs_out path> (obs_out) | <in-place path> (in place)", each either

@@ -1381,7 +1381,22 @@ __global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) 
 // ---------------------------------------------------------------- surface kernel
 // The reference contract: obs is the caller's next-day window; only channel F-1
 // is rewritten with ActionBuffer.get_all() (trading_env.py:103).
-static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
+//
+// Host-I/O form (pmenv_step_host, the reference driver's CPU tensors, train/on_policy.py:
+// 59-67): `io` is non-null and every per-step input and output lives in pinned,
+// device-mapped host staging — action / prices (p.action, p.prices) and the window's last
+// closes (io.close_in) are read straight over PCIe, and the channel goes out as a dense
+// [B, N, W] block (io.chan) beside the reward, return, post-drift weights and value
+// (io.value_out), which the host scatters into the caller's window after one stream sync.
+// The window itself never crosses the bus: only channel F-1 is the env's to write.
+struct HostIO {
+    const float* close_in;   // [B, N] obs[b, n, W-1, close] gathered by the host
+    float* chan;             // [B, N, W] channel F-1 out
+    double* value_out;       // [B] the value after the step (TradingEnv.value)
+};
+
+template <bool HOST>
+__device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1392,15 +1407,18 @@ static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams 
         const double v_prev = p.value[b];
         gather_inputs(p, b, s, k);
         scalar_compute(p, b, s, k, v_prev);
+        // the lane that wrote the value (scalar_compute's lane 0) hands it out
+        if (HOST && tid == 0) io.value_out[b] = p.value[b];
     }
     __syncthreads();
-    if (!p.obs) return;
+    if (HOST ? !io.chan : !p.obs) return;
     const int slot = s.ints[1];
     const int32_t k1 = s.ints[2];                 // updates since reset, after this step
     const int idx = (int)((1 + (int64_t)k1) % W);
     const bool full = (int64_t)k1 >= W - 1;
     const float* ringb = p.ring + (size_t)b * W * N;
-    float* obs = p.obs + (size_t)b * N * W * F;
+    float* obs = HOST ? io.chan + (size_t)b * N * W : p.obs + (size_t)b * N * W * F;
+    const int fs = HOST ? 1 : F, fo = HOST ? 0 : F - 1;
     for (int i = tid; i < N * W; i += kBlock) {
         const int n = (int)fdiv((uint32_t)i, p.div_w);
         const int t = i - n * W;
@@ -1408,15 +1426,26 @@ static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams 
         if (!full) rs = t < W - idx ? -1 : t - (W - idx);
         else rs = p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
         float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
-        obs[((size_t)n * W + t) * F + (F - 1)] = v;
+        obs[((size_t)n * W + t) * fs + fo] = v;
     }
     // keep the advance-mode close in step with the caller's window
     for (int n = tid; n < N; n += kBlock)
-        p.last_close[(size_t)b * N + n] = obs[((size_t)n * W + (W - 1)) * F + p.close_ch];
+        p.last_close[(size_t)b * N + n] = HOST ? io.close_in[(size_t)b * N + n]
+                                               : obs[((size_t)n * W + (W - 1)) * F + p.close_ch];
+}
+
+static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
+    surface_body<false>(p, HostIO{});
+}
+static __global__ __launch_bounds__(kBlock) void step_surface_host_kernel(StepParams p, HostIO io) {
+    surface_body<true>(p, io);
 }
 
 // ---------------------------------------------------------------- reset kernel
-static __global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask) {
+// io non-null: the host-I/O form (pmenv_reset_host) — the channel goes to io.chan [B, N, W]
+// and the last closes come from io.close_in, as in step_surface_host_kernel.
+static __global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, float* obs, const uint8_t* mask,
+                                                              HostIO io = HostIO{}) {
     const int b = blockIdx.x;
     if (mask && !mask[b]) return;
     const int tid = threadIdx.x;
@@ -1426,10 +1455,17 @@ static __global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, floa
         p.k[b] = 0;                               // weight_buffer.py:49 idx = 1
         p.sa[b] = 0.0;
         p.sb[b] = 0.0;
+        if (io.value_out) io.value_out[b] = p.init_cash;
     }
     float* ringb = p.ring + (size_t)b * W * N;     // weight_buffer.py:47-48 e0 in slot 0
     for (int i = tid; i < W * N; i += kBlock) ringb[i] = i == 0 ? 1.0f : 0.0f;
     for (int n = tid; n < N; n += kBlock) p.w_new[(size_t)b * N + n] = n == 0 ? 1.0f : 0.0f;   // get_last()
+    if (io.chan) {
+        float* ch = io.chan + (size_t)b * N * W;   // the same channel, dense, for the host to scatter
+        for (int i = tid; i < N * W; i += kBlock) ch[i] = i == W - 1 ? 1.0f : 0.0f;
+        for (int n = tid; n < N; n += kBlock) p.last_close[(size_t)b * N + n] = io.close_in[(size_t)b * N + n];
+        return;
+    }
     if (!obs) return;
     float* ob = obs + (size_t)b * N * W * F;       // trading_env.py:31-32 get_all() at idx = 1
     for (int i = tid; i < N * W; i += kBlock) {

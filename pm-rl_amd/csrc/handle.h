@@ -94,8 +94,14 @@ struct pmenv {
     uint32_t relay_epoch; // the last step's tag
     bool relay_captured;  // a step / reset / state write of this handle was captured into a hipGraph:
                           // replays write behind the host's back, so relay steps run as two launches
+    // host-I/O staging (pmenv_step_host / pmenv_reset_host): one pinned, device-mapped block,
+    // allocated on the first host-I/O call — action | prices | last closes | channel [B,N,W] |
+    // weights | reward (f32), then return | value (f64); `hio_dev` is its device address
+    char* hio;
+    char* hio_dev;
+    size_t hio_off[8];
     int path;             // pmenv_step_path_kind
-    void* tools;          // tools build: its knob state (null in the product library)
+    void* tools;        // tools build: its knob state (null in the product library)
     char err[512];
 };
 

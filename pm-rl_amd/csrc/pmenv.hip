@@ -556,6 +556,7 @@ int pmenv_destroy(pmenv* h) {
     if (h->halo) (void)hipFree(h->halo);
     if (h->snap) (void)hipFree(h->snap);
     if (h->relay_mem) (void)hipFree(h->relay_mem);
+    if (h->hio) (void)hipHostFree(h->hio);
     free(h);
     return PMENV_OK;
 }
@@ -689,6 +690,127 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
     memset(&a, 0, sizeof(a));
     a.action = action; a.prices = prices; a.bar = bar; a.obs = obs; a.reward = reward;
     return pmenv_step_ex(h, &a, stream);
+}
+
+}  // extern "C"
+
+namespace {
+// The host-I/O staging block (allocated on first use, freed by destroy): f32 action |
+// prices | closes [B*N] each, channel [B*N*W], weights [B*N], reward [B]; f64 return |
+// value [B]. Pinned and device-mapped, so the kernels read and write it over PCIe directly.
+int hio_ensure(pmenv* h) {
+    if (h->hio) return PMENV_OK;
+    const size_t B = (size_t)h->cfg.num_envs, BN = B * (size_t)h->cfg.num_assets;
+    auto up64 = [](size_t x) { return (x + 63) / 64 * 64; };
+    size_t o = 0;
+    const size_t sizes[8] = {BN * 4, BN * 4, BN * 4, BN * (size_t)h->cfg.window * 4, BN * 4, B * 4, B * 8, B * 8};
+    for (int i = 0; i < 8; ++i) {
+        h->hio_off[i] = o;
+        o = up64(o + sizes[i]);
+    }
+    void* p = nullptr;
+    // coherent (fine-grained): the GPU never caches it, so each step reads what the host
+    // just wrote and the host reads the kernel's stores after the stream sync
+    hipError_t e = hipHostMalloc(&p, o, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) {
+        set_err(h, "hipHostMalloc(%zu) for host-I/O staging failed: %s", o, hipGetErrorString(e));
+        return PMENV_ERR_HIP;
+    }
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(p);
+        set_err(h, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+        return PMENV_ERR_HIP;
+    }
+    h->hio = (char*)p;
+    h->hio_dev = (char*)d;
+    return PMENV_OK;
+}
+enum { kHioAct, kHioPri, kHioClose, kHioChan, kHioW, kHioRew, kHioRet, kHioVal };
+template <class T>
+T* hio_host(const pmenv* h, int f) { return reinterpret_cast<T*>(h->hio + h->hio_off[f]); }
+template <class T>
+T* hio_dev(const pmenv* h, int f) { return reinterpret_cast<T*>(h->hio_dev + h->hio_off[f]); }
+
+// the window's last closes obs[b, n, W-1, close] -> staging (the only window bytes the step reads)
+void hio_gather_closes(pmenv* h, const float* obs) {
+    const pmenv_cfg& c = h->cfg;
+    const size_t BN = (size_t)c.num_envs * c.num_assets, row = (size_t)c.window * c.features;
+    const float* src = obs + (size_t)(c.window - 1) * c.features + c.close_channel;
+    float* dst = hio_host<float>(h, kHioClose);
+    for (size_t i = 0; i < BN; ++i) dst[i] = src[i * row];
+}
+// the [B, N, W] channel the kernel wrote -> obs[..., F-1] of the caller's window
+void hio_scatter_channel(const pmenv* h, float* obs) {
+    const pmenv_cfg& c = h->cfg;
+    const size_t BNW = (size_t)c.num_envs * c.num_assets * c.window;
+    const int F = c.features;
+    const float* src = hio_host<float>(h, kHioChan);
+    float* dst = obs + (F - 1);
+    for (size_t i = 0; i < BNW; ++i) dst[i * F] = src[i];
+}
+int hio_sync(pmenv* h, hipStream_t stream, const char* what) {
+    if (const int rc = check_launch(h, what)) return rc;
+    const hipError_t e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) {
+        set_err(h, "%s: %s", what, hipGetErrorString(e));
+        return PMENV_ERR_HIP;
+    }
+    return PMENV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* obs, float* reward, double* value,
+                    double* ret, float* weights, hipStream_t stream) {
+    if (!h) return PMENV_ERR_ARG;
+    if (!action || !prices) { set_err(h, "host step: action and prices are required"); return PMENV_ERR_ARG; }
+    DeviceGuard g(h->device);
+    if (const int rc = hio_ensure(h)) return rc;
+    const pmenv_cfg& c = h->cfg;
+    const size_t B = (size_t)c.num_envs, BN = B * (size_t)c.num_assets;
+    memcpy(hio_host<float>(h, kHioAct), action, BN * 4);
+    memcpy(hio_host<float>(h, kHioPri), prices, BN * 4);
+    if (obs) hio_gather_closes(h, obs);
+    if (const int rc = flat1_invalidate(h, stream)) return rc;   // the snapshot / halos go stale
+    StepParams p = base_params(h);
+    p.action = hio_dev<float>(h, kHioAct);
+    p.prices = hio_dev<float>(h, kHioPri);
+    p.reward = hio_dev<float>(h, kHioRew);
+    p.ret = hio_dev<double>(h, kHioRet);
+    p.weights = hio_dev<float>(h, kHioW);
+    HostIO io;
+    io.close_in = hio_dev<float>(h, kHioClose);
+    io.chan = obs ? hio_dev<float>(h, kHioChan) : nullptr;
+    io.value_out = hio_dev<double>(h, kHioVal);
+    step_surface_host_kernel<<<c.num_envs, kBlock, h->lds_surface, stream>>>(p, io);
+    if (const int rc = hio_sync(h, stream, "step_surface_host_kernel")) return rc;
+    if (obs) hio_scatter_channel(h, obs);
+    if (reward) memcpy(reward, hio_host<float>(h, kHioRew), B * 4);
+    if (ret) memcpy(ret, hio_host<double>(h, kHioRet), B * 8);
+    if (value) memcpy(value, hio_host<double>(h, kHioVal), B * 8);
+    if (weights) memcpy(weights, hio_host<float>(h, kHioW), BN * 4);
+    return PMENV_OK;
+}
+
+int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream) {
+    if (!h) return PMENV_ERR_ARG;
+    DeviceGuard g(h->device);
+    if (const int rc = hio_ensure(h)) return rc;
+    if (obs) hio_gather_closes(h, obs);
+    if (const int rc = flat1_invalidate(h, stream)) return rc;
+    StepParams p = base_params(h);
+    HostIO io;
+    io.close_in = hio_dev<float>(h, kHioClose);
+    io.chan = obs ? hio_dev<float>(h, kHioChan) : nullptr;
+    io.value_out = hio_dev<double>(h, kHioVal);
+    reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, nullptr, nullptr, io);
+    if (const int rc = hio_sync(h, stream, "reset_kernel (host I/O)")) return rc;
+    if (obs) hio_scatter_channel(h, obs);
+    if (value) memcpy(value, hio_host<double>(h, kHioVal), (size_t)h->cfg.num_envs * 8);
+    return PMENV_OK;
 }
 
 double* pmenv_value(pmenv* h) { return h ? h->value : nullptr; }

@@ -13,7 +13,8 @@ import torch  # noqa: F401
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PMENV_LIB", os.path.join(HERE, "libpmenv.so"))
 
-PMENV_ABI_VERSION = 2   # 2: pmenv_window_written / pmenv_state_written; cfg default ret_mode GROSS
+PMENV_ABI_VERSION = 3   # 2: pmenv_window_written / pmenv_state_written; cfg default ret_mode GROSS
+                        # 3: pmenv_step_host / pmenv_reset_host
 
 # enums (include/pmenv.h)
 REWARD_KINDS = {"log_returns": 0, "returns": 1, "sharpe_ratio": 2, "diff_sharpe": 3}
@@ -66,6 +67,8 @@ SIGNATURES = [
     ("pmenv_reset", ctypes.c_int, [_P, _P, _P, _P]),
     ("pmenv_step_ex", ctypes.c_int, [_P, ctypes.POINTER(PmenvStepArgs), _P]),
     ("pmenv_step", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    ("pmenv_step_host", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    ("pmenv_reset_host", ctypes.c_int, [_P, _P, _P, _P]),
     ("pmenv_value", _P, [_P]),
     ("pmenv_ring", _P, [_P]),
     ("pmenv_counter", _P, [_P]),

@@ -26,13 +26,18 @@ Every compute call goes through libpmenv.so (include/pmenv.h); there is no CPU
 path. `features` must be a float32, contiguous tensor: it is written in place and
 returned, exactly as trading_env.py:32,103 mutate the caller's tensor. A caller that
 keeps the reference's CPU tensors (train/on_policy.py:59-67 hands the env host
-tensors) may pass them unchanged: they are staged to the env's GPU and back (a PCIe
-round trip per call — the slow path; keep tensors on the GPU for throughput), and
-the reward, `.value` and `.info` come back on the host with the reference's types.
+tensors) may pass them unchanged: reset / step (surface contract) then run through
+pmenv_reset_host / pmenv_step_host — only the action, the prices and the window's last
+closes go to the GPU, only the [N, W] weight channel and the outputs come back, through
+pinned device-mapped staging with one stream sync per call — and the reward, `.value`
+and `.info` are host objects with the reference's types. (The fused advance with host
+tensors stages the whole window to the GPU and back; keep tensors on the GPU for
+throughput.)
 """
 import ctypes
 import weakref
 
+import numpy as np
 import torch
 
 from . import _abi
@@ -188,6 +193,10 @@ class TradingEnv:
         self._state_ver = _version(self._state)
         self._win = None
         self._win_ver = -1
+        # host I/O: the per-call record chunks and the host value of the last host-I/O call
+        # (valid while the state blob is as that call left it)
+        self._rec_blk, self._rec_n, self._rec_i = None, 0, 0
+        self._hval, self._hval_ver = None, None
         self.set_step_impl(self.step_impl)
         self._reset_info()
 
@@ -326,7 +335,13 @@ class TradingEnv:
     def value(self):
         """Portfolio value (trading_env.py:9,89) — f64 [B] view of the device state
         (a host copy when the caller drives the env with CPU tensors)."""
-        v = self._value.cpu() if self._host_io else self._value
+        if self._host_io:
+            hv = self._hval
+            if hv is not None and self._hval_ver == _version(self._state) and self._hval_ver is not None:
+                return hv                          # the host copy the last host-I/O call left
+            v = self._value.cpu()
+        else:
+            v = self._value
         return v[0] if self._unbatched else v
 
     def set_step_impl(self, impl):
@@ -347,11 +362,19 @@ class TradingEnv:
         """trading_env.py:21-41 for all envs (or the envs where mask is True)."""
         unb = False
         dev_features = features
+        self._hval = None
         if features is not None:
             self._fit(features)
             unb = self._obs_check(features)
             self._unbatched = unb
             self._host_io = features.device.type == "cpu"
+            if self._host_io and mask is None and self._HOST_DIRECT:   # the driver's reset (on_policy.py:61)
+                if self._info is not None:
+                    _ = self.info                  # the old history, final (flushed, seed action frozen)
+                self._reset_host(features, unb)
+                self._state_ver = _version(self._state)
+                self._reset_info()
+                return features
             if self._host_io:
                 dev_features = features.to(self.device)
         if mask is None and self._info is not None:
@@ -402,6 +425,9 @@ class TradingEnv:
         if self._free:
             self._fit(features)
         unb = self._obs_check(features)
+        if not features.is_cuda and bar is None and series is None and out is None and weights_out is None \
+                and prices is not None and self._HOST_DIRECT:
+            return self._step_host(action, features, prices, unb)
         if not features.is_cuda:                    # the reference's CPU tensors: staged through the GPU
             if out is not None and out.device.type != "cpu":
                 raise ValueError("out must live where features does")
@@ -416,7 +442,85 @@ class TradingEnv:
         self._host_io = False
         return self._step(action, features, prices, bar, out, series, day, weights_out, unb, host=False)
 
+    # ------------------------------------------------------------------ host I/O
+    # The reference driver's call shape (train/on_policy.py:59-67): CPU action, window and
+    # prices. One pmenv_step_host call per step: the kernel reads the action, the prices and
+    # the window's last closes from pinned device-mapped staging and writes the [B, N, W]
+    # weight channel back into it; the library scatters the channel into `features` (the
+    # market channels never cross PCIe) and fills the per-step records below, so `.value`,
+    # the reward and `info` need no further device round trip.
+    _REC_STEPS = 256
+    _HOST_DIRECT = True      # False: stage the whole window through the GPU (round 4's path; A/B only)
+
+    def _host_vec(self, x, name):
+        """action / prices as a host float32 contiguous tensor of B*N elements."""
+        n = self.cfg.num_envs * self.cfg.num_assets
+        if not torch.is_tensor(x):
+            x = torch.as_tensor(x)
+        if x.dtype is torch.float32 and not x.is_cuda and x.numel() == n and x.is_contiguous():
+            return x
+        if x.numel() != n:
+            # weight_buffer.py:18-19 raises ValueError on a mis-shaped action
+            raise ValueError(f"{name} must have {self.cfg.num_envs} x {self.cfg.num_assets} elements, "
+                             f"got shape {tuple(x.shape)}")
+        return x.detach().to(device=_CPU, dtype=torch.float32).contiguous()
+
+    def _rec(self):
+        """Host arrays for one call's outputs: views into chunks of _REC_STEPS calls, so a call
+        costs no allocation and the records handed to the caller (the reward, `.value`,
+        info entries) stay valid after later calls."""
+        i = self._rec_i
+        if self._rec_blk is None or i == self._rec_n:
+            B, N = self.cfg.num_envs, self.cfg.num_assets
+            K = max(1, min(self._REC_STEPS, (1 << 22) // (B * (N + 6) * 4)))
+            blk = (np.empty((K, B), np.float32), np.empty((K, B), np.float64), np.empty((K, B), np.float64),
+                   np.empty((K, B, N), np.float32))
+            self._rec_blk, self._rec_n, i = blk, K, 0
+            self._rec_ptr = tuple(a.ctypes.data for a in blk)
+            self._rec_sz = (4 * B, 8 * B, 8 * B, 4 * B * N)
+        self._rec_i = i + 1
+        return i
+
+    def _step_host(self, action, features, prices, unb):
+        a = self._host_vec(action, "action")
+        p = self._host_vec(prices, "prices")
+        track = self.track_info and self._info is not None
+        i = self._rec()
+        rp, sz = self._rec_ptr, self._rec_sz
+        rc = self._lib.pmenv_step_host(self._h, a.data_ptr(), p.data_ptr(), features.data_ptr(), rp[0] + i * sz[0],
+                                       rp[2] + i * sz[2], rp[1] + i * sz[1] if track else None,
+                                       rp[3] + i * sz[3] if track else None, self._stream())
+        if rc:
+            _abi.check(rc, self._h, "pmenv_step_host")
+        rew, ret, val, w = (x[i] for x in self._rec_blk)
+        if unb:
+            rew, ret, val, w = rew[0, ...], ret[0, ...], val[0, ...], w[0]
+        r = torch.from_numpy(rew)                  # r and info["rewards"][-1] share memory, as :99-100
+        v = torch.from_numpy(val)
+        self._hval, self._hval_ver = v, _version(self._state)
+        self._host_io = True
+        self._unbatched = unb
+        if track:
+            if self._pending:
+                self._flush_info()
+            inf = self._info
+            inf["values"].append(v)                # :80 the value tensor (also .value, :89)
+            inf["actions"].append(w)               # :85 w'.cpu().numpy()
+            inf["returns"].append(ret)             # :90
+            inf["rewards"].append(rew)             # :100
+            self._slot0_dirty = True
+        return r, features
+
+    def _reset_host(self, features, unb):
+        i = self._rec()
+        rp, sz = self._rec_ptr, self._rec_sz
+        _abi.check(self._lib.pmenv_reset_host(self._h, features.data_ptr(), rp[2] + i * sz[2], self._stream()),
+                   self._h, "pmenv_reset_host")
+        val = self._rec_blk[2][i]
+        self._hval, self._hval_ver = torch.from_numpy(val[0, ...] if unb else val), _version(self._state)
+
     def _step(self, action, features, prices, bar, out, series, day, weights_out, unb, host):
+        self._hval = None
         cfg = self.cfg
         B, N = cfg.num_envs, cfg.num_assets
         a = self._vec(action, N, "action")
@@ -541,6 +645,7 @@ class TradingEnv:
             raise ValueError("state blob mismatch (a uint8 blob of this env shape's size expected)")
         # through pmenv_set_state: the handle re-primes what it derives from the state
         src = st.to(device=self.device, dtype=torch.uint8).contiguous()
+        self._hval = None
         _abi.check(self._lib.pmenv_set_state(self._h, _ptr(src), self._stream()), self._h, "pmenv_set_state")
 
     @property

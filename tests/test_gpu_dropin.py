@@ -143,6 +143,47 @@ def test_gpu_feature_count_bound_by_first_reset(name):
     compare(g, out)
 
 
+@pytest.mark.parametrize("B,N,W,F", [(1, 32, 32, 5), (1, 5, 50, 5), (3, 7, 10, 3), (2, 30, 50, 8)])
+def test_gpu_host_io_direct_equals_staged_bitwise(B, N, W, F):
+    """pmenv_step_host (action, prices and the last closes in through mapped staging, the
+    [N, W] channel out) gives bitwise what round 4's whole-window staging gave: rewards,
+    values, returns, post-drift weights and every float of the caller's window, through
+    a reset mid-run and past the ring's wrap."""
+    from pmenv import TradingEnv
+    rng = np.random.default_rng(B * 1000 + N)
+    T = 2 * W + 5
+    shape = (N, W, F) if B == 1 else (B, N, W, F)
+    wins = rng.uniform(0.5, 1.5, (T + 1,) + shape).astype(np.float32)
+    acts = rng.standard_normal((T + 1, B, N)).astype(np.float32)
+    acts[::3] = np.abs(acts[::3])                              # raw positive: the AND rule keeps them
+    prices = rng.uniform(0.95, 1.05, (T + 1, B, N)).astype(np.float32)
+    res = []
+    for direct in (True, False):
+        env = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device="cuda:0", track_info=True)
+        env._HOST_DIRECT = direct
+        rec = {"r": [], "v": [], "win": []}
+        for t in range(T + 1):
+            x = torch.tensor(wins[t])
+            if t in (0, W + 2):
+                env.reset(x)
+            else:
+                r, y = env.step(torch.tensor(acts[t]).reshape(shape[:-2] + (1,)) if B == 1 else torch.tensor(acts[t]),
+                                x, torch.tensor(prices[t]))
+                assert y is x and r.device.type == "cpu"
+                rec["r"].append(r.numpy().copy())
+            rec["v"].append(np.array(env.value, dtype=np.float64).copy())
+            rec["win"].append(x.numpy().copy())
+        inf = env.info
+        rec["info"] = [np.array([np.asarray(e, dtype=np.float64) for e in inf[k][1:]]) for k in inf]
+        res.append(rec)
+    d, s = res
+    for key in ("r", "v", "win"):
+        for a, b in zip(d[key], s[key]):
+            assert np.array_equal(np.atleast_1d(a).view(np.uint8), np.atleast_1d(b).view(np.uint8)), key
+    for a, b in zip(d["info"], s["info"]):
+        assert np.array_equal(a, b)
+
+
 def test_gpu_given_dims_are_checked_against_the_first_tensor():
     """A dimension the constructor fixes is not rebound: a window of another shape raises
     ValueError (as the reference's fixed-size ring fails on it)."""

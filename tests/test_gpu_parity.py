@@ -26,15 +26,17 @@ def _t(x, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
 
 
-def replay_gpu(g, mode, host=False, impl="auto"):
+def replay_gpu(g, mode, host=False, impl="auto", direct=True):
     """host=True: the reference's own call shape with CPU tensors (train/on_policy.py:59-67
-    hands the env host tensors); the env stages them through the GPU. impl: the advance
-    step's implementation (TradingEnv.set_step_impl)."""
+    hands the env host tensors): surface steps through pmenv_step_host (direct=False: the
+    whole window staged through the GPU, round 4's path), advance steps staged. impl: the
+    advance step's implementation (TradingEnv.set_step_impl)."""
     from pmenv import TradingEnv
     m = g["meta"]
     N, W, F, T = m["N"], m["W"], m["F"], m["T"]
     env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, track_info=True, step_impl=impl,
                      close_channel=gu.close_channel(g))
+    env._HOST_DIRECT = direct
     _t = (lambda x, dtype=torch.float32: torch.as_tensor(np.ascontiguousarray(x), dtype=dtype)) if host else \
         globals()["_t"]
     out = {"rewards": np.full(T + 1, np.nan), "values": np.zeros(T + 1), "rets": np.full(T + 1, np.nan),
@@ -74,7 +76,7 @@ def test_gpu_matches_reference_goldens(name, mode):
 
 
 @pytest.mark.parametrize("name", gu.cases())
-@pytest.mark.parametrize("impl", ["flat", "one_launch", "two_launch"])
+@pytest.mark.parametrize("impl", ["flat", "one_launch", "two_launch", "relay"])
 def test_gpu_every_step_path_matches_reference_goldens(name, impl):
     """The reference's recorded outputs replayed through each advance-step implementation
     forced (AUTO takes one_launch at one env). A path refuses exactly the shapes its
@@ -87,28 +89,44 @@ def test_gpu_every_step_path_matches_reference_goldens(name, impl):
     granular = F == 5 and (N * W * F) % 4 == 0
     misfit = {"two_launch": not granular,
               "one_launch": not (granular and W >= 2 and N <= 64 and N * W * F * 4 <= 64 * 1024),
-              "flat": not (granular and W >= 2 and N <= 64 and N * W * F // 4 >= 148)}[impl]
+              "flat": not (granular and W >= 2 and N <= 64 and N * W * F // 4 >= 148),
+              "relay": not (granular and W >= 2 and N <= 512)}[impl]
     try:
-        TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
+        env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device=DEV, step_impl=impl)
     except ValueError:
         assert misfit, f"{impl} refused N={N} W={W} F={F}"
         return
     assert not misfit, f"{impl} accepted N={N} W={W} F={F}"
+    kern = {"flat": "step_flat_kernel", "one_launch": "step_env_kernel", "relay": "step_relay_kernel",
+            "two_launch": "+"}[impl]
+    assert kern in env.step_path.split(" | ")[1], env.step_path      # the in-place path is the one forced
     g = gu.load(name)
     out = replay_gpu(g, "advance", impl=impl)
     assert out["market_ok"]
     compare(g, out)
 
 
-@pytest.mark.parametrize("name", ["simplex_n30_w50_t256_f64", "mixed_n30_w50_t64_f32", "wrap_n5_w8_t40_f64", "reset_n5_w8_t40_f64"])
-def test_gpu_reference_goldens_with_host_tensors(name):
+HOST_LEGS = {"surface_direct": ("surface", "auto", True), "surface_staged": ("surface", "auto", False),
+             "advance_relay": ("advance", "relay", True), "advance_auto": ("advance", "auto", True)}
+
+
+@pytest.mark.parametrize("name", ["simplex_n30_w50_t256_f64", "mixed_n30_w50_t64_f32", "wrap_n5_w8_t40_f64",
+                                  "reset_n5_w8_t40_f64", "simplex_n5_w50_t64_f32", "feat8_n32_w32_t80_f64"])
+@pytest.mark.parametrize("leg", list(HOST_LEGS))
+def test_gpu_reference_goldens_with_host_tensors(name, leg):
     """The reference's callers drive the env with CPU tensors, unchanged: features,
     actions and prices on the host in, reward and value back on the host, the
-    features mutated in place and returned (trading_env.py:102-105)."""
+    features mutated in place and returned (trading_env.py:102-105). Surface steps run
+    through pmenv_step_host (direct) and through round 4's whole-window staging; advance
+    steps with host tensors through the relayed step and AUTO's."""
     if name not in gu.cases():
         pytest.skip("golden case absent")
+    mode, impl, direct = HOST_LEGS[leg]
     g = gu.load(name)
-    out = replay_gpu(g, "surface", host=True)
+    m = g["meta"]
+    if impl == "relay" and not (m["F"] == 5 and (m["N"] * m["W"] * 5) % 4 == 0 and m["W"] >= 2):
+        pytest.skip("relay refuses this shape (checked in test_gpu_every_step_path_matches_reference_goldens)")
+    out = replay_gpu(g, mode, host=True, impl=impl, direct=direct)
     compare(g, out)
 
 

@@ -1,0 +1,123 @@
+"""Per-step wall time of the reference driver's own env sequence through pmenv's TradingEnv.
+
+train/on_policy.py:56-67 (_rollout) and :76-90 (_evaluate) drive ONE env with the data
+loader's CPU tensors:
+
+    for step, (datetime, prices, data) in enumerate(dl):
+        if step == 0: s = env.reset(data)
+        else:
+            a = agent.act(s)                       # [N, 1]
+            r, s_ = env.step(a, data, prices)
+            buffer.add(s, a, env.value, r)         # rollout_buffer.py:55 np.array(env.value)
+            s = s_
+        logger.log_rollout(step, datetime, r, env.value)
+
+then Metrics reads env.info (util/eval.py:14-37). This times exactly the env's share of that
+loop — reset, T x step(a, data, prices) with host tensors, float(env.value) and
+np.array(env.value) per step, one info read at the end — with the loader's windows and the
+agent's actions prebuilt (their cost is the driver's, not the env's). Shapes: config/base.py
+(1 x 32 x 32 x 5, WINDOW_SIZE = NUM_ASSETS = 32) and BASELINE config 1 (1 x 5 x 50 x 5).
+
+Legs: "direct" = pmenv_step_host (the product path); "staged" = round 4's path (the whole
+window to the GPU and back per call, TradingEnv._HOST_DIRECT = False); "oracle_b1" = the C
+restatement (oracle/liboracle.so) at B = 1 on one thread through its ctypes wrapper, the
+same call shape; the reference's own step() is ~120 us per call (measured in
+the build container, 1 thread). Prints one JSON object."""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pm-rl_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from pmenv import TradingEnv, EnvConfig  # noqa: E402
+
+T = int(os.environ.get("HOSTIO_T", "2000"))
+REPS = int(os.environ.get("HOSTIO_REPS", "5"))
+
+
+def inputs(N, W, F, seed=0):
+    g = np.random.default_rng(seed)
+    close = np.cumprod(1 + 0.01 * g.standard_normal((N, T + W + 1)), axis=1).astype(np.float32)
+    series = np.repeat(close[:, :, None], F, axis=2)
+    series[:, :, F - 1] = g.random((N, T + W + 1))
+    datas = [torch.tensor(series[:, t:t + W, :]) for t in range(T + 1)]
+    prices = [torch.tensor(close[:, t + W - 1] / close[:, t + W - 2]) for t in range(T + 1)]
+    logits = g.standard_normal((T + 1, N)).astype(np.float32)
+    acts = [torch.softmax(torch.tensor(logits[t]), 0).reshape(N, 1) for t in range(T + 1)]
+    return datas, prices, acts
+
+
+def drive(env, datas, prices, acts):
+    """The env's share of on_policy.py:59-67, per step (us)."""
+    t0 = time.perf_counter()
+    s = None
+    for step in range(T + 1):
+        if step == 0:
+            s = env.reset(datas[0])
+        else:
+            r, s_ = env.step(acts[step], datas[step], prices[step])
+            np.array(env.value)                 # buffer.add(s, a, env.value, r)
+            s = s_
+        float(env.value)                        # logger.log_rollout(..., r, env.value)
+    info = env.info
+    assert len(info["values"]) == T + 1
+    return (time.perf_counter() - t0) / T * 1e6, s
+
+
+def main():
+    torch.cuda.set_device(0)
+    out = {"T": T, "reps": REPS, "reference_step_us": 120.0,
+           "reference_step_note": "SURVEY.md §0.5: trading_env.py:44-105 on CPU tensors, 1 thread, build container"}
+    for (N, W, F) in ((32, 32, 5), (5, 50, 5)):
+        datas, prices, acts = inputs(N, W, F)
+        res = {}
+        for leg in ("direct", "staged"):
+            times = []
+            for rep in range(REPS + 1):
+                env = TradingEnv()
+                env._HOST_DIRECT = leg == "direct"
+                us, s = drive(env, [d.clone() for d in datas] if rep == 0 else datas, prices, acts)
+                if rep:
+                    times.append(us)
+                env.close()
+            res[leg] = {"us_per_step_median": statistics.median(times), "us_per_step_min": min(times)}
+        # the C restatement at B = 1, one thread, the same call shape (ctypes wrapper included)
+        try:
+            from oracle.oracle import OracleEnv
+            o = OracleEnv(EnvConfig(num_envs=1, num_assets=N, window=W, features=F, close_channel=min(3, F - 2)))
+            dn = [d.numpy().reshape(1, N, W, F) for d in datas]
+            an = [a.numpy().reshape(1, N) for a in acts]
+            pn = [p.numpy().reshape(1, N) for p in prices]
+            times = []
+            for rep in range(REPS):
+                t0 = time.perf_counter()
+                o.reset(dn[0])
+                for step in range(1, T + 1):
+                    o.step(an[step], obs=dn[step], prices=pn[step], threads=1)
+                    float(o.value[0])
+                times.append((time.perf_counter() - t0) / T * 1e6)
+            res["oracle_b1"] = {"us_per_step_median": statistics.median(times), "threads": 1}
+        except ImportError as e:
+            res["oracle_b1"] = {"error": str(e)}
+        # one direct step, timed alone (reset, 50 steps warm, then per call)
+        env = TradingEnv()
+        env.reset(datas[0])
+        lat = []
+        for step in range(1, min(T, 500) + 1):
+            t0 = time.perf_counter()
+            env.step(acts[step], datas[step], prices[step])
+            lat.append((time.perf_counter() - t0) * 1e6)
+        res["direct_step_call_us"] = {"median": statistics.median(lat[50:]), "p90": float(np.percentile(lat[50:], 90))}
+        out[f"{N}x{W}x{F}"] = res
+        print(f"{N}x{W}x{F}", json.dumps(res), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
