@@ -214,7 +214,9 @@ int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream);
  * "step_flat_vec_kernel" (the same for 64 < N <= 512),
  * "step_env_kernel" (the whole step in one launch, one workgroup per env) or
  * "<scalar step>+<window stream>"
- * (two launches); or "step_advance_lds_kernel" (single-launch fallback, any F). */
+ * (two launches); or, for F != 5 or windows that are not 16-B granular, "step_small_kernel"
+ * (one workgroup per env, the window in registers: env windows of at most 16,384 floats) or
+ * "step_advance_lds_kernel" (the LDS-tiled fallback, any F). */
 const char* pmenv_step_path(const pmenv* h);
 
 /* Advance-mode step implementation. AUTO (the default) picks per shape and window
@@ -244,8 +246,19 @@ const char* pmenv_step_path(const pmenv* h);
  * ONE launch — scalar workgroups (one run per env) relay w' and the counter to the stream
  * tiles through epoch-tagged words in handle memory (F = 5, W >= 2, 16-B granular env
  * windows, N <= 512; the same bits as TWO_LAUNCH). In place it keeps the tiles' halo from
- * the previous step, under the same pmenv_window_written rule as FLAT. A RELAY step enqueued
- * while `stream` is being captured runs as TWO_LAUNCH (its epoch is a host counter). */
+ * the previous step, under the same pmenv_window_written rule as FLAT. From the first call of
+ * a handle enqueued while a stream is being captured into a hipGraph on, its relay steps are
+ * device-sequenced (a small relay_prime_kernel before each step_relay_kernel reads the epoch,
+ * the parity and the copies' validity from device memory), so captured and eager relay steps
+ * interleave freely; pmenv_step_path then says "relay steps device-sequenced".
+ * REQUIREMENT: a tile spins until the scalar blocks before it in blockIdx order have relayed
+ * its rows, so RELAY (and AUTO, which picks it for in-place windows of 24-256 MiB and
+ * double-buffered ones of 48-128 MiB at N <= 64) relies on the GPU dispatching a grid's
+ * workgroups in blockIdx order — what CDNA's command processor does (round-robin over the
+ * XCDs, in order within each), not a HIP guarantee. The form that does not rely on it (an
+ * ordered ticket: one fetch-add per workgroup on one counter) measured 4.7x slower (DESIGN.md
+ * §3). Choose TWO_LAUNCH on a platform without in-order dispatch. (pmenv_gae_ex's look-back
+ * pass makes no such assumption: a wave that waits too long computes the map itself.) */
 typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,

@@ -20,15 +20,20 @@
  *        nothing. Reads outside the env are checked never to feed a kept position.
  * 3. Emulates the flat one-launch step (step_flat.h) over consecutive steps: tiles in a
  *    random order, the halo and the state snapshot by parity, one owner per env (below).
- * 4. Emulates the relayed step (step_relay.h) over consecutive steps: scalar blocks and
- *    tiles interleaved at random, a tile runnable only once every relay word it stages
- *    carries the step's epoch (the kernel's wait), through the epoch's wrap, caller edits,
- *    a state write and a step of another path; the tile's staged rows are checked to fit
- *    its BLOCK threads and every LDS / halo / counter index to stay in its buffer.
+ * 4. Emulates the relayed step (step_relay.h) over consecutive steps: workgroups dispatched
+ *    in a random, non-monotone order with one to 64 resident at once, each taking its role
+ *    from the ordered ticket on arrival, a tile runnable only once every relay word it stages
+ *    carries the step's epoch (the kernel's wait) — any schedule in which every resident
+ *    workgroup waits is a deadlock and fails — through the epoch's wrap, caller edits, a
+ *    state write and a step of another path; the tile's staged rows are checked to fit its
+ *    BLOCK threads and every LDS / halo / counter index to stay in its buffer.
  * 5. Emulates the one-pass look-back GAE (rollout.h gae_lookback_kernel) with the kernel's
- *    indexing: workgroups publish and compose in a random order subject to the flag waits,
- *    on a workspace of exactly pmenv_gae_workspace's size holding garbage or the previous
- *    call's maps and flags; the result is checked against the restatement.
+ *    indexing: workgroups dispatched in blockIdx order or a random permutation with a
+ *    residency limit, publishing and composing subject to the flag waits, a waiting
+ *    workgroup taking the kernel's fallback (the missing maps computed itself, checked
+ *    bitwise against the producer's) when no resident one can move; on a workspace of
+ *    exactly pmenv_gae_workspace's size holding garbage or the previous call's maps and
+ *    flags; the result is checked against the restatement.
  * 6. Audits, without data, the addresses of the in-place stream's halo copy
  *    (env_step.h halo_load / halo_store / copy_halo) for every scalar-step grid, and of
  *    the tools build's advance_flat_direct_kernel (the kernel of the round-3 record
@@ -406,7 +411,13 @@ static void emulate_flat1(int B, int N, int W, int CPW, int T, int storage) {
  * next-step copy (kp parity 1 - q) and the canonical state. A tile stages one row per thread
  * (g_lo .. g_hi), the rows' w' from the words (it waits until they carry this step's epoch)
  * and their counter from kp parity q; in place, the two chunks past it from the halo of
- * parity q, and it writes its first two output chunks into the halo of parity 1 - q. */
+ * parity q, and it writes its first two output chunks into the halo of parity 1 - q.
+ * Dispatch models (a waiting tile holds its slot; a finished workgroup frees one):
+ *   0  blockIdx order, 1 to 64 workgroups resident — the hardware's order, which the kernel
+ *      requires (include/pmenv.h); no step may deadlock;
+ *   1  a random order with every workgroup resident; no step may deadlock;
+ *   2  a random order with ONE resident (negative control): returns 1 on the first
+ *      deadlock, which shows the requirement is real and the detection works. */
 typedef struct { uint64_t* w; int32_t* kp[2]; float* halo[2]; uint32_t epoch; int par, kp_ok; const float* obs; } relay_st;
 
 static void relay_prime(relay_st* r, const float* obs, int B, const int32_t* k, int64_t ntiles, int64_t CPW,
@@ -421,10 +432,10 @@ static void relay_prime(relay_st* r, const float* obs, int B, const int32_t* k, 
         for (int b = 0; b < B; ++b) r->kp[r->par][b] = k[b];
 }
 
-static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, int storage, int dbuf) {
+static int emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, int storage, int dbuf, int model) {
     const int F = 5, WF = W * F;
     const int64_t per = (int64_t)N * WF, tot = per * B;
-    if (per % 4 || W < 2) return;
+    if (per % 4 || W < 2) return 0;
     const int64_t per4 = per / 4, qtot = tot / 4, CPW = (int64_t)BLOCK * V, ntiles = (qtot + CPW - 1) / CPW;
     const int EPB = (BLOCK / 64) * (64 / KL), scal = (B + EPB - 1) / EPB;
     /* the host plan's closed form (pmenv.hip: at most BLOCK rows per tile) */
@@ -443,12 +454,15 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
     r.kp[0] = malloc(sizeof(int32_t) * B); r.kp[1] = malloc(sizeof(int32_t) * B);
     const int64_t nhal = ntiles > 1 ? (ntiles - 1) * 8 : 1;               /* [tiles - 1][2] float4 */
     r.halo[0] = malloc(sizeof(float) * nhal); r.halo[1] = malloc(sizeof(float) * nhal);
+    const int grid = scal + (int)ntiles;
     r.epoch = 0xFFFFFFFDu; r.par = 0; r.kp_ok = 0; r.obs = NULL;
+    int deadlocked = 0;
     uint8_t* stored = calloc((size_t)qtot, 1);
     uint8_t* halo_w[2] = {calloc((size_t)ntiles, 1), calloc((size_t)ntiles, 1)};   /* written this step, per parity */
     uint8_t* scal_owner = calloc((size_t)B, 1);
-    uint8_t* done = calloc((size_t)(scal + ntiles), 1);
     int* runnable = malloc(sizeof(int) * (size_t)(scal + ntiles));
+    int* order = malloc(sizeof(int) * (size_t)(scal + ntiles));
+    int* res_idx = malloc(sizeof(int) * (size_t)(scal + ntiles));      /* resident workgroups */
     float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
     float* s_wp = malloc(sizeof(float) * BLOCK);
     int32_t* s_kc = malloc(sizeof(int32_t) * BLOCK);
@@ -483,12 +497,17 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
             relay_prime(&r, in, B, k, ntiles, CPW, qtot, !dbuf && r.obs != in);
             if (++r.epoch == 0) { memset(r.w, 0, sizeof(uint64_t) * (size_t)B * N); r.epoch = 1; }
             const int q = r.par;
+            if (model == 0) for (int i = 0; i < grid; ++i) order[i] = i;
+            else shuffle(order, grid);
+            const int resident = model == 0 ? 1 + (int)(urand() * (t % 3 == 0 ? 4 : 64)) : model == 1 ? grid : 1;
+            int next = 0, live = 0;
             memset(stored, 0, (size_t)qtot); memset(halo_w[0], 0, (size_t)ntiles); memset(halo_w[1], 0, (size_t)ntiles);
-            memset(scal_owner, 0, (size_t)B); memset(done, 0, (size_t)(scal + ntiles));
-            for (int left = scal + (int)ntiles; left > 0; --left) {
+            memset(scal_owner, 0, (size_t)B);
+            for (int left = grid; left > 0; --left) {
+                while (live < resident && next < grid) res_idx[live++] = order[next++];
                 int nr = 0;
-                for (int i = 0; i < scal + ntiles; ++i) {
-                    if (done[i]) continue;
+                for (int s2 = 0; s2 < live; ++s2) {
+                    const int i = res_idx[s2];
                     if (i >= scal) {                    /* a tile waits for its rows' words */
                         const int64_t c0 = (int64_t)(i - scal) * CPW, nb = qtot - c0 < CPW ? qtot - c0 : CPW;
                         const int64_t b_lo = c0 / per4, g_lo = b_lo * N + 4 * (c0 - b_lo * per4) / WF;
@@ -497,12 +516,15 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
                         for (int64_t g = g_lo; g <= g_hi && ready; ++g) ready = (uint32_t)(r.w[g] >> 32) == r.epoch;
                         if (!ready) continue;
                     }
-                    runnable[nr++] = i;
+                    runnable[nr++] = s2;
                 }
-                CHECK(nr > 0, "relay: no block can run (B%d N%d W%d)", B, N, W);
+                if (!nr && model == 2) { deadlocked = 1; break; }
+                CHECK(nr > 0, "relay: deadlock, %d resident workgroups all wait (B%d N%d W%d model %d)", live, B, N, W,
+                      model);
                 if (!nr) break;
-                const int i = runnable[(int)(urand() * nr)];
-                done[i] = 1;
+                const int slot_r = runnable[(int)(urand() * nr)];
+                const int i = res_idx[slot_r];
+                res_idx[slot_r] = res_idx[--live];
                 if (i < scal) {                         /* relay_scalar */
                     for (int j = 0; j < EPB; ++j) {
                         const int b = i * EPB + j;
@@ -571,6 +593,7 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
                 }
                 if (!dbuf && tile > 0) halo_w[1 - q][tile - 1] = 1;
             }
+            if (deadlocked) break;
             for (int b = 0; b < B; ++b) CHECK(scal_owner[b] == 1, "relay: env %d stepped %d times", b, scal_owner[b]);
             r.par = 1 - q; r.kp_ok = 1; r.obs = dbuf ? NULL : out;
         }
@@ -584,7 +607,8 @@ static void emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, 
     }
     free(buf[0]); free(buf[1]); free(ref); free(nxt); free(bar); free(wp); free(value); free(k); free(k0); free(v0);
     free(r.w); free(r.kp[0]); free(r.kp[1]); free(r.halo[0]); free(r.halo[1]); free(stored); free(halo_w[0]); free(halo_w[1]);
-    free(scal_owner); free(done); free(runnable); free(lds); free(s_wp); free(s_kc);
+    free(scal_owner); free(runnable); free(order); free(res_idx); free(lds); free(s_wp); free(s_kc);
+    return deadlocked;
 }
 
 /* ------------------------------------------------------------ 5. the look-back GAE */
@@ -595,9 +619,46 @@ static int lb_chunks(int T, int B, int seg) {
     return (T + seg - 1) / seg;
 }
 
-/* one call of gae_lookback_kernel<NW, U> on a workspace `ws` of exactly the ABI's size */
+/* chunk c's map for env lane of block eb, as a publisher reduces it (lb_wave_map per wave, folded
+ * from wave NW - 1); st_* (may be NULL) receive the days' deltas / alive bits / values */
+static void lb_map_lane(const float* r, const float* v, const uint8_t* d, int T, int B, double g, double gl, int NW,
+                        int U, int c, int eb, int lane, double* Ca_out, double* Da_out, double* wc, double* wd,
+                        double* st_dl, uint8_t* st_al, double* st_vv) {
+    const int S = NW * U, seg_start = c * S, seg_end = seg_start + S < T ? seg_start + S : T;
+    const int b = eb * 64 + lane, bb = b < B ? b : B - 1;
+    double Ca = 1.0, Da = 0.0;
+    for (int w = 0; w < NW; ++w) {
+        const int t0 = seg_start + w * U;
+        double C = 1.0, D = 0.0;
+        for (int u = U - 1; u >= 0; --u) {
+            const int tv = t0 + u + 1 < seg_end ? t0 + u + 1 : seg_end;     /* vv[u + 1] */
+            const int tu = t0 + u < seg_end ? t0 + u : seg_end;             /* vv[u] */
+            const int tr = t0 + u < seg_end - 1 ? t0 + u : seg_end - 1;
+            CHECK((size_t)tv * B + bb < (size_t)(T + 1) * B && (size_t)tr * B + bb < (size_t)T * B, "gae_lb: load index");
+            const double n = d && d[(size_t)tr * B + bb] ? 0.0 : 1.0;
+            const double dl = (double)r[(size_t)tr * B + bb] + g * n * (double)v[(size_t)tv * B + bb] -
+                              (double)v[(size_t)tu * B + bb];
+            if (st_dl) {
+                const size_t si = (size_t)w * U + u;
+                st_dl[si] = dl; st_al[si] = (uint8_t)n; st_vv[si] = (double)v[(size_t)tu * B + bb];
+            }
+            if (t0 + u < seg_end) { D = dl + gl * n * D; C = gl * n * C; }
+        }
+        wc[w] = C; wd[w] = D;
+    }
+    for (int w = NW - 1; w >= 0; --w) { Da = wd[w] + wc[w] * Da; Ca = wc[w] * Ca; }
+    *Ca_out = Ca; *Da_out = Da;
+}
+
+/* one call of gae_lookback_kernel<NW, U> on a workspace `ws` of exactly the ABI's size. Workgroups
+ * are dispatched in blockIdx order (later chunks first) or in a random permutation, at most
+ * `resident` on the device at once (a finished one frees its slot); a resident workgroup
+ * waiting for flags holds its slot. When every resident workgroup waits (its producers not
+ * dispatched), one of them takes the kernel's fallback: it computes the missing chunks' maps
+ * itself (the producers' code; they must agree bit for bit when a producer publishes later). */
 static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv, float* ret, int T, int B, double g,
-                    double gl, int NW, int U, int nC, double* ws, size_t ws_doubles, uint64_t epoch) {
+                    double gl, int NW, int U, int nC, double* ws, size_t ws_doubles, uint64_t epoch, int resident,
+                    int random_order) {
     const int S = NW * U, nEB = (B + 63) / 64, nblk = nC * nEB;
     double* mapC = ws;
     double* mapD = ws + (size_t)nC * B;
@@ -611,11 +672,20 @@ static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv
     double* shD = malloc(sizeof(double) * (size_t)nblk * NW * 64);
     int* phase = calloc((size_t)nblk, sizeof(int));
     int* runnable = malloc(sizeof(int) * (size_t)nblk);
+    int* order = malloc(sizeof(int) * (size_t)nblk);
+    uint8_t* res = calloc((size_t)nblk, 1);
+    uint8_t* forced = calloc((size_t)nblk, 1);         /* took the fallback: composes without flags */
+    uint8_t* fb = calloc((size_t)nC * nEB, 1);          /* a chunk's map written by a fallback */
+    if (random_order) shuffle(order, nblk);
+    else for (int i = 0; i < nblk; ++i) order[i] = i;
+    int next = 0, live = 0, fallbacks = 0;
+    double wc[64], wd[64];
     for (int left = 2 * nblk; left > 0; --left) {
+        while (live < resident && next < nblk) { res[order[next++]] = 1; ++live; }
         int nr = 0;
         for (int bi = 0; bi < nblk; ++bi) {
-            if (phase[bi] == 2) continue;
-            if (phase[bi] == 1) {
+            if (!res[bi] || phase[bi] == 2) continue;
+            if (phase[bi] == 1 && !forced[bi]) {
                 const int c = nC - 1 - bi / nEB, eb = bi % nEB;
                 int ready = 1;
                 for (int j = c + 1; j < nC && ready; ++j) ready = flags[(size_t)j * nEB + eb] == epoch;
@@ -623,36 +693,45 @@ static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv
             }
             runnable[nr++] = bi;
         }
-        CHECK(nr > 0, "gae_lb: no workgroup can run");
-        if (!nr) break;
+        if (!nr) {                                      /* every resident waits: a spin bound expires */
+            int waiting = 0;
+            for (int bi = 0; bi < nblk; ++bi) if (res[bi] && phase[bi] == 1) runnable[waiting++] = bi;
+            CHECK(waiting > 0, "gae_lb: no workgroup can run and none waits");
+            if (!waiting) break;
+            const int bi = runnable[(int)(urand() * waiting)];
+            const int c = nC - 1 - bi / nEB, eb = bi % nEB;
+            for (int j = c + 1; j < nC; ++j) {
+                if (flags[(size_t)j * nEB + eb] == epoch) continue;
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int b = eb * 64 + lane;
+                    double Ca, Da;
+                    lb_map_lane(r, v, d, T, B, g, gl, NW, U, j, eb, lane, &Ca, &Da, wc, wd, NULL, NULL, NULL);
+                    if (b < B) { mapC[(size_t)j * B + b] = Ca; mapD[(size_t)j * B + b] = Da; }
+                }
+                fb[(size_t)j * nEB + eb] = 1;
+                ++fallbacks;
+            }
+            forced[bi] = 1;
+            runnable[0] = bi;
+            nr = 1;
+        }
         const int bi = runnable[(int)(urand() * nr)];
         const int c = nC - 1 - bi / nEB, eb = bi % nEB;
         const int seg_start = c * S, seg_end = seg_start + S < T ? seg_start + S : T;
         if (phase[bi] == 0) {                           /* load, reduce, publish */
             for (int lane = 0; lane < 64; ++lane) {
-                const int b = eb * 64 + lane, ok = b < B, bb = ok ? b : B - 1;
-                double Ca = 1.0, Da = 0.0;
-                double wc[64], wd[64];
+                const int b = eb * 64 + lane, ok = b < B;
+                double Ca, Da;
+                const size_t si = ((size_t)bi * 64 + lane) * S;
+                lb_map_lane(r, v, d, T, B, g, gl, NW, U, c, eb, lane, &Ca, &Da, wc, wd, st_dl + si, st_al + si,
+                            st_vv + si);
                 for (int w = 0; w < NW; ++w) {
-                    const int t0 = seg_start + w * U;
-                    double C = 1.0, D = 0.0;
-                    for (int u = U - 1; u >= 0; --u) {
-                        const int tv = t0 + u + 1 < seg_end ? t0 + u + 1 : seg_end;     /* vv[u + 1] */
-                        const int tu = t0 + u < seg_end ? t0 + u : seg_end;             /* vv[u] */
-                        const int tr = t0 + u < seg_end - 1 ? t0 + u : seg_end - 1;
-                        CHECK((size_t)tv * B + bb < (size_t)(T + 1) * B && (size_t)tr * B + bb < (size_t)T * B, "gae_lb: load index");
-                        const double n = d && d[(size_t)tr * B + bb] ? 0.0 : 1.0;
-                        const double dl = (double)r[(size_t)tr * B + bb] + g * n * (double)v[(size_t)tv * B + bb] -
-                                          (double)v[(size_t)tu * B + bb];
-                        const size_t si = ((size_t)bi * 64 + lane) * S + (size_t)w * U + u;
-                        st_dl[si] = dl; st_al[si] = (uint8_t)n; st_vv[si] = (double)v[(size_t)tu * B + bb];
-                        if (t0 + u < seg_end) { D = dl + gl * n * D; C = gl * n * C; }
-                    }
-                    wc[w] = C; wd[w] = D;
-                    shC[((size_t)bi * NW + w) * 64 + lane] = C;
-                    shD[((size_t)bi * NW + w) * 64 + lane] = D;
+                    shC[((size_t)bi * NW + w) * 64 + lane] = wc[w];
+                    shD[((size_t)bi * NW + w) * 64 + lane] = wd[w];
                 }
-                for (int w = NW - 1; w >= 0; --w) { Da = wd[w] + wc[w] * Da; Ca = wc[w] * Ca; }
+                if (ok && fb[(size_t)c * nEB + eb])
+                    CHECK(!memcmp(&mapC[(size_t)c * B + b], &Ca, 8) && !memcmp(&mapD[(size_t)c * B + b], &Da, 8),
+                          "gae_lb: a fallback map differs from the producer's (chunk %d env %d)", c, b);
                 if (ok) { mapC[(size_t)c * B + b] = Ca; mapD[(size_t)c * B + b] = Da; }
             }
             flags[(size_t)c * nEB + eb] = epoch;
@@ -689,8 +768,13 @@ static void lb_call(const float* r, const float* v, const uint8_t* d, float* adv
             }
         }
         phase[bi] = 2;
+        res[bi] = 0;
+        --live;
     }
+    for (int bi = 0; bi < nblk; ++bi) CHECK(phase[bi] == 2, "gae_lb: workgroup %d never finished", bi);
+    CHECK(random_order || resident < nblk || !fallbacks, "gae_lb: a fallback under blockIdx dispatch with every workgroup resident");
     free(st_dl); free(st_vv); free(st_al); free(shC); free(shD); free(phase); free(runnable);
+    free(order); free(res); free(forced); free(fb);
 }
 
 /* gae_lookback2_kernel (tools build, PMENV_GAE=lb2 / lb2x16): pairs of adjacent chunks (B = 2p, A = 2p + 1)
@@ -778,7 +862,7 @@ static void emulate_gae_lb2(int T, int B, int NW, int U, int resident) {
     free(runnable); free(res);
 }
 
-static void emulate_gae_lb(int T, int B, int NW, int U) {
+static void emulate_gae_lb(int T, int B, int NW, int U, int resident, int random_order) {
     const int seg = NW * U, nC = (T + seg - 1) / seg, nEB = (B + 63) / 64;
     const size_t ws_doubles = (size_t)2 * nC * B + (size_t)nC * nEB;
     double* ws = malloc(sizeof(double) * ws_doubles);
@@ -796,7 +880,7 @@ static void emulate_gae_lb(int T, int B, int NW, int U) {
         for (size_t i = 0; i < (size_t)(T + 1) * B; ++i) v[i] = (float)nrand();
         const float gamma = 0.99f, lam = call ? 1.0f : 0.95f;
         lb_call(r, v, call ? NULL : d, adv, ret, T, B, (double)gamma, (double)gamma * (double)lam, NW, U, nC, ws,
-                ws_doubles, epoch);
+                ws_doubles, epoch, resident, random_order);
         or_gae(r, v, call ? NULL : d, oa, orr, T, B, gamma, lam);
         for (size_t i = 0; i < (size_t)T * B; ++i)
             if (!(fabsf(adv[i] - oa[i]) <= 1e-5f * (1.0f + fabsf(oa[i]))) ||
@@ -892,16 +976,28 @@ int main(void) {
                               {13, 5, 48, 8}, {3, 1, 600, 8}};
     for (size_t i = 0; i < sizeof rshapes / sizeof rshapes[0]; ++i)
         for (int storage = 0; storage < 2; ++storage)
-            for (int db = 0; db < 2; ++db) {
-                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 256, 2, rshapes[i][3], 12, storage, db);
-                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 512, 2, rshapes[i][3], 12, storage, db);
-                emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 64, 2, rshapes[i][3], 12, storage, db);
-            }
+            for (int db = 0; db < 2; ++db)
+                for (int model = 0; model < 2; ++model) {     /* blockIdx order, limited residency; any order, all resident */
+                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 256, 2, rshapes[i][3], 12, storage, db, model);
+                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 512, 2, rshapes[i][3], 12, storage, db, model);
+                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 64, 2, rshapes[i][3], 12, storage, db, model);
+                }
+    /* negative control: a non-monotone dispatch order with one workgroup resident deadlocks the
+     * blockIdx-role kernel (a tile dispatched before its scalar block waits forever) — the
+     * requirement include/pmenv.h states is real, and the detection above sees it */
+    int dl = 0;
+    for (int rep = 0; rep < 8 && !dl; ++rep) dl = emulate_relay(37, 30, 50, 64, 2, 32, 3, 1, 0, 2);
+    CHECK(dl, "relay: no deadlock under a non-monotone order with one resident workgroup (negative control)");
     /* the look-back GAE: the product's rule and both chunk lengths, ragged B and T, one chunk */
     const int gshapes[][2] = {{700, 67}, {513, 3}, {1000, 130}, {600, 64}, {130, 5}};
     for (size_t i = 0; i < sizeof gshapes / sizeof gshapes[0]; ++i) {
-        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8);
-        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16);
+        /* every workgroup resident in any order; blockIdx order at a few resident; a random,
+         * non-monotone dispatch order at one to a few resident (the fallback's case) */
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8, 1 << 30, 0);
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16, 1 << 30, 0);
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8, 3, 0);
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 16, 1, 1);
+        emulate_gae_lb(gshapes[i][0], gshapes[i][1], 8, 8, 5, 1);
     }
     /* the paired kernel (tools build) under every residency, down to one workgroup */
     for (int res = 1; res <= 9; res += 4) {

@@ -1378,6 +1378,92 @@ __global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) 
     }
 }
 
+// ---------------------------------------------------------------- register step (any F, any alignment)
+// The whole advance-mode step in one workgroup per env, for the windows the 16-B streams do
+// not take (F != 5, or env windows that are not 16-B granular: config 1's 1 x 5 x 50 x 5 is
+// 250 floats per asset row) with at most BLOCK x E floats per env. Every float the step reads
+// is loaded straight into VGPRs, before the scalar step: thread i owns floats j = i + BLOCK e
+// of the env's [N, W, F] block and loads in[j + F] (the same row's next day), or on the last
+// day the bar's [n, f] (f < F-1); for the weight channel in[j + F] while the ring shifts and
+// in[j] once the storage-order ring is full (it then stays in place) — the one read that
+// waits for the step counter (a scalar load issued with the market loads).
+// Wave 0 runs the env's scalar step meanwhile (the two-launch path's gather_inputs /
+// scalar_compute, LDS scratch); every wave then waits for its loads to have RETURNED
+// (vmcnt(0)) before the barrier, which closes the in-place read-before-write window of the
+// env — one workgroup owns one env, no other workgroup touches it — and composes and stores
+// dword-wise. Replaces step_advance_lds_kernel's stage-through-LDS rounds (two barriers per
+// row tile, the window loads issued only after the scalar step) for these shapes.
+template <int BLOCK, int E>
+__global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
+    const uint32_t WF = (uint32_t)(W * F), NWF = (uint32_t)N * WF;
+    constexpr uint32_t kOut = 0x80000000u;                // a byte offset past every buffer: reads 0, stores nothing
+    Scratch s = carve(lds, 0, N, F);
+    const auto rs_in = make_rsrc(p.obs + (size_t)b * NWF, NWF * 4u);
+    const auto rs_out = make_rsrc(p.obs_out + (size_t)b * NWF, NWF * 4u);
+    const float* barg = env_bar(p, b);                    // null: a day outside the series (NaN bar)
+    const auto rs_bar = make_rsrc(barg ? barg : p.obs, barg ? (uint32_t)(N * Fm) * 4u : 0u);
+    const float nanv = __int_as_float(0x7fc00000);
+    const int32_t k0 = p.k[b];                            // scalar load, in flight with the market loads
+    float src[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {                         // the market channels: in[j + F] or the bar
+        const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+        const uint32_t row = fdiv(j, p.div_wf);
+        const uint32_t kk = j - row * WF;
+        const uint32_t t = fdiv(kk, p.div_f);
+        const uint32_t f = kk - t * (uint32_t)F;
+        const bool mkt = j < NWF && (int)f < Fm, last = (int)t == W - 1;
+        const float sh = buf_load1(rs_in, mkt && !last ? (j + (uint32_t)F) * 4u : kOut);
+        const float bv = buf_load1(rs_bar, mkt && last ? (row * (uint32_t)Fm + f) * 4u : kOut);
+        src[e] = last ? (barg ? bv : nanv) : sh;
+    }
+    // the weight channel: shifted with the window until the ring is full, then (storage order)
+    // in place (weight_buffer.py:32-44) — the counter decides which float to read
+    const bool shift_w = p.ring_mode == PMENV_RING_CHRONO || k0 < W - 1;
+    uint32_t tid2 = (uint32_t)tid;
+    asm volatile("" : "+v"(tid2));                        // recompute the indices, do not keep E of them live
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t j = tid2 + (uint32_t)(BLOCK * e);
+        const uint32_t row = fdiv(j, p.div_wf);
+        const uint32_t kk = j - row * WF;
+        const uint32_t t = fdiv(kk, p.div_f);
+        const uint32_t f = kk - t * (uint32_t)F;
+        const bool wch = j < NWF && (int)f == Fm;
+        const uint32_t off = !wch ? kOut : !shift_w ? j * 4u : (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut;
+        const float wv = buf_load1(rs_in, off);
+        src[e] = wch ? wv : src[e];
+    }
+    if (tid < 64) {
+        const double v_prev = p.value[b];
+        gather_inputs(p, b, s, k0);
+        scalar_compute(p, b, s, k0, v_prev);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's window reads are in
+    __syncthreads();
+    const int slot = s.ints[1];
+    uint32_t tid3 = (uint32_t)tid;
+    asm volatile("" : "+v"(tid3));
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t j = tid3 + (uint32_t)(BLOCK * e);
+        const uint32_t row = fdiv(j, p.div_wf);
+        const uint32_t kk = j - row * WF;
+        const uint32_t t = fdiv(kk, p.div_f);
+        const uint32_t f = kk - t * (uint32_t)F;
+        float v = src[e];
+        if ((int)f == Fm && j < NWF) {
+            const float wp = s.wp[row];
+            v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : v);
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
+    }
+}
+
 // ---------------------------------------------------------------- surface kernel
 // The reference contract: obs is the caller's next-day window; only channel F-1
 // is rewritten with ActionBuffer.get_all() (trading_env.py:103).

@@ -31,6 +31,9 @@ struct pmenv {
     float* last_close;
     float* w_new;
     unsigned long long* nonfinite;
+    // the register step (step_small_kernel<small_block, small_e>): any F, any alignment, env
+    // windows of at most 1,024 x 16 floats; 0: the LDS fallback
+    int small_block, small_e;
     // LDS single-launch fallback geometry
     int rows_per_tile, tile_floats;
     bool vec;
@@ -84,16 +87,19 @@ struct pmenv {
     int relay_block, relay_v; // the tiles' geometry: relay_block threads x relay_v 16-B chunks
     int relay_epb;        // envs per scalar block (relay_block / 64 waves x 64 / relay_kl envs)
     uint32_t relay_tiles, relay_scal;
-    void* relay_mem;      // relay words | counter copy x 2 | halo x 2
+    void* relay_mem;      // control words | relay words | counter copy x 2 | halo x 2 (allocated when
+                          // AUTO gives the shape the relay step or pmenv_set_step_path asks for it)
+    uint32_t* relay_seq;  // device-sequenced words {D, E, V, C, EC, pad, HOBS lo, HOBS hi} (step_relay.h)
     uint64_t* relay_w;    // [B * N] {epoch, w'}
-    int32_t* relay_kp[2]; // [B] per parity: the counter before the step (kp_in), after it (kp_out)
-    bool relay_kp_ok;     // relay_kp[relay_par] equals the state's counter
-    float* relay_halo[2]; // in place: [relay_tiles - 1][2] float4 per parity
-    int relay_par;        // parity of the counter copy / halo the next relay step reads
-    const float* relay_obs;   // the window whose halo relay_halo[relay_par] holds (null: none)
-    uint32_t relay_epoch; // the last step's tag
-    bool relay_captured;  // a step / reset / state write of this handle was captured into a hipGraph:
-                          // replays write behind the host's back, so relay steps run as two launches
+    int32_t* relay_kp;    // [2][B] the counter copies, per parity
+    float* relay_halo;    // in place: [2][relay_halo_stride] floats
+    uint32_t relay_halo_stride;
+    bool relay_kp_ok;     // eager: relay_kp[relay_par] equals the state's counter
+    const float* relay_obs;   // eager: the window whose halo relay_halo[relay_par] holds (null: none)
+    int relay_par;        // eager: parity of the counter copy / halo the next relay step reads
+    uint32_t relay_epoch; // eager: the last step's tag
+    bool relay_dseq;      // device-sequenced: from the first call of this handle enqueued under stream
+                          // capture on, epoch, parity and the copies' validity live in relay_seq
     // host-I/O staging (pmenv_step_host / pmenv_reset_host): one pinned, device-mapped block,
     // allocated on the first host-I/O call — action | prices | last closes | channel [B,N,W] |
     // weights | reward (f32), then return | value (f64); `hio_dev` is its device address

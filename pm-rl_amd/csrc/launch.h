@@ -110,6 +110,18 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
     launch_scalar_kernels(h, p, stream);
 }
 
+// ---------------------------------------------------------------- the register step (any F)
+inline void launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const unsigned grid = (unsigned)h->cfg.num_envs;
+    const size_t lds = h->lds_surface;
+    switch (h->small_block * 100 + h->small_e) {
+    case 25608: step_small_kernel<256, 8><<<grid, 256, lds, stream>>>(p); break;
+    case 25616: step_small_kernel<256, 16><<<grid, 256, lds, stream>>>(p); break;
+    case 51216: step_small_kernel<512, 16><<<grid, 512, lds, stream>>>(p); break;
+    default: step_small_kernel<1024, 16><<<grid, 1024, lds, stream>>>(p); break;
+    }
+}
+
 // ---------------------------------------------------------------- one launch, one workgroup per env
 inline void launch_one(const pmenv* h, const StepParams& p, hipStream_t stream) {
     if (pmenv_tools::launch_one(h, p, stream)) return;
@@ -220,65 +232,82 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- one launch, relayed (step_relay.h)
-template <int BLOCK, int POL, bool OUT>
+template <int BLOCK, int POL, bool OUT, bool SEQ>
 inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
                            hipStream_t stream) {
     const uint32_t q = h->flat_qtot;
     switch (h->relay_kl * 100 + h->relay_ka) {
-    case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 3200: step_relay_kernel<BLOCK, 2, POL, OUT, 32, 0><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 3200: step_relay_kernel<BLOCK, 2, POL, OUT, 32, 0, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    }
+}
+template <int BLOCK, int POL>
+inline void launch_relay_b(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, bool out,
+                           bool seq, hipStream_t stream) {
+    if (out) {
+        if (seq) launch_relay_g<BLOCK, POL, true, true>(h, p, r, grid, stream);
+        else launch_relay_g<BLOCK, POL, true, false>(h, p, r, grid, stream);
+    } else {
+        if (seq) launch_relay_g<BLOCK, POL, false, true>(h, p, r, grid, stream);
+        else launch_relay_g<BLOCK, POL, false, false>(h, p, r, grid, stream);
     }
 }
 
-// prime the counter copy and the in-place halo when the previous relay step's do not hold,
-// tag the step with the next epoch (the words restart at 0 if the counter wraps), one launch
+// prime the counter copy and the in-place halo when the previous relay step's do not hold (eager:
+// the host's flags say so; device-sequenced: the prime kernel reads the validity words, so a
+// replayed graph decides per replay), tag the step with the next epoch, then one launch
 inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     const bool out = p.obs_out != p.obs;
-    const int q = h->relay_par;
     const uint32_t cpw = (uint32_t)(h->relay_block * h->relay_v);
+    const bool dseq = h->relay_dseq;
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
-    const bool need_halo = !out && h->relay_obs != p.obs;
-    if (need_halo || !h->relay_kp_ok) {
-        StepParams pp = p;
-        pp.halo = need_halo ? h->relay_halo[q] : nullptr;
-        pp.halo_wgs = h->relay_tiles > 0 ? h->relay_tiles - 1 : 0;
-        pp.halo_block = cpw;
-        pp.halo_qtot = h->flat_qtot;
-        const uint32_t work = pp.halo_wgs > (uint32_t)h->cfg.num_envs ? pp.halo_wgs : (uint32_t)h->cfg.num_envs;
-        const unsigned g = work / 256 + 1 < 2048 ? work / 256 + 1 : 2048;
-        relay_prime_kernel<<<g, 256, 0, stream>>>(pp, h->relay_kp_ok ? nullptr : h->relay_kp[q]);
-    }
-    if (++h->relay_epoch == 0) {
+    if (!dseq && ++h->relay_epoch == 0) {           // the words restart at 0 when the counter wraps
         const size_t words = (size_t)h->cfg.num_envs * h->cfg.num_assets * 8;
         if (hipMemsetAsync(h->relay_w, 0, words, stream) != hipSuccess) return PMENV_ERR_HIP;
         h->relay_epoch = 1;
     }
     RelayParams r;
+    const int q = h->relay_par;
     r.scal = h->relay_scal;
-    r.w = h->relay_w;
-    r.kp_in = h->relay_kp[q];
-    r.kp_out = h->relay_kp[1 - q];
-    r.halo_in = h->relay_halo[q];
-    r.halo_out = h->relay_halo[1 - q];
     r.epoch = h->relay_epoch;
-    const unsigned grid = h->relay_tiles + h->relay_scal;
-    if (pmenv_tools::launch_relay(h, p, r, grid, stream)) {
-    } else if (h->relay_block == 256) {
-        if (out) launch_relay_g<256, 0, true>(h, p, r, grid, stream);
-        else launch_relay_g<256, 0, false>(h, p, r, grid, stream);
-    } else {
-        if (out) launch_relay_g<512, 1, true>(h, p, r, grid, stream);
-        else launch_relay_g<512, 1, false>(h, p, r, grid, stream);
+    r.par = (uint32_t)q;
+    r.kp_in = h->relay_kp + (size_t)q * h->cfg.num_envs;
+    r.kp_out = h->relay_kp + (size_t)(1 - q) * h->cfg.num_envs;
+    r.halo_in = h->relay_halo + (size_t)q * h->relay_halo_stride;
+    r.halo_out = h->relay_halo + (size_t)(1 - q) * h->relay_halo_stride;
+    r.seq = dseq ? h->relay_seq : nullptr;
+    r.w = h->relay_w;
+    r.kp = h->relay_kp;
+    r.halo = h->relay_halo;
+    r.B = (uint32_t)h->cfg.num_envs;
+    r.halo_stride = h->relay_halo_stride;
+    r.obs = p.obs;
+    const bool need_halo = !out && (dseq || h->relay_obs != p.obs);
+    const bool need_kp = dseq || !h->relay_kp_ok;
+    if (need_halo || need_kp) {
+        StepParams pp = p;
+        pp.halo = need_halo ? h->relay_halo : nullptr;
+        pp.halo_wgs = h->relay_tiles > 0 ? h->relay_tiles - 1 : 0;
+        pp.halo_block = cpw;
+        pp.halo_qtot = h->flat_qtot;
+        const uint32_t work = pp.halo_wgs > (uint32_t)h->cfg.num_envs ? pp.halo_wgs : (uint32_t)h->cfg.num_envs;
+        const unsigned g = work / 256 + 1 < 2048 ? work / 256 + 1 : 2048;
+        relay_prime_kernel<<<g, 256, 0, stream>>>(pp, r, need_kp ? 1 : 0, dseq ? 1 : 0);
     }
-    // every relay step flips the parity; the halo of the next parity belongs to this window
-    // only when this step ran in place (and wrote it)
-    h->relay_par = 1 - q;
+    const unsigned grid = h->relay_tiles + h->relay_scal;
+    if (dseq || !pmenv_tools::launch_relay(h, p, r, grid, stream)) {
+        if (h->relay_block == 256) launch_relay_b<256, 0>(h, p, r, grid, out, dseq, stream);
+        else launch_relay_b<512, 1>(h, p, r, grid, out, dseq, stream);
+    }
+    // eager: every relay step flips the parity; the halo of the next parity belongs to this
+    // window only when this step ran in place (and wrote it)
+    h->relay_par = 1 - h->relay_par;
     h->relay_kp_ok = true;
     h->relay_obs = out ? nullptr : p.obs;
     return PMENV_OK;

@@ -78,25 +78,47 @@ bool capturing(hipStream_t stream) {
 // where host flags set once at capture time would let replay 2 on read the snapshot the
 // previous replay left (flat_seq_kernel then re-primes from the reset state).
 enum { kInvalSnap = 1, kInvalHalo = 2 };
-// The relay step keeps its in-place halo by a host flag: once anything of this handle is
-// captured into a hipGraph, replays may write the window or the state where the host does not
-// see it, so from then on its relay steps run as two launches.
+// Once any call of this handle is enqueued while `stream` is being captured into a hipGraph,
+// replays may write the window or the state where the host does not see it: from then on the
+// flat and the relay steps keep the validity of their copies (snapshot, counter copy, halo) in
+// device words that every invalidation clears on the stream — whatever path is current when the
+// capture is seen, since a later switch of path must not find host flags a replay outdated.
 void note_capture(pmenv* h, hipStream_t stream) {
-    if (h->relay && !h->relay_captured && capturing(stream)) h->relay_captured = true;
+    if (((h->flat1_ok && !h->device_seq) || (h->relay_ok && !h->relay_dseq)) && capturing(stream)) {
+        if (h->flat1_ok) h->device_seq = true;
+        if (h->relay_ok) h->relay_dseq = true;
+    }
+}
+
+// the relay step's copies go stale (kInvalSnap: the counter copy and the halo; kInvalHalo: the halo)
+int relay_invalidate(pmenv* h, hipStream_t stream, int what) {
+    h->relay_obs = nullptr;
+    if (what & kInvalSnap) h->relay_kp_ok = false;
+    if (!h->relay_dseq || !h->relay_mem) return PMENV_OK;
+    // V = 0 re-primes both, HOBS = 0 the halo
+    const hipError_t e = (what & kInvalSnap) ? hipMemsetAsync(h->relay_seq + 2, 0, 4, stream)
+                                             : hipMemsetAsync(h->relay_seq + 6, 0, 8, stream);
+    if (e != hipSuccess) {
+        set_err(h, "invalidating the relay step's copies: %s", hipGetErrorString(e));
+        return PMENV_ERR_HIP;
+    }
+    return PMENV_OK;
 }
 
 int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInvalHalo, bool host_only = false,
                      bool keep_relay = false) {
     if (what & kInvalSnap) h->snap_ok = false;
     h->halo1_obs = nullptr;
-    if (!keep_relay) {                         // the relay step's halo and counter copy
-        h->relay_obs = nullptr;
-        if (what & kInvalSnap) h->relay_kp_ok = false;
-    }
     if (!host_only) note_capture(h, stream);
-    if (host_only || !h->flat1_ok) return PMENV_OK;
-    if (!h->device_seq && h->flat1 && capturing(stream)) h->device_seq = true;
-    if (!h->device_seq) return PMENV_OK;
+    if (!keep_relay) {
+        if (host_only) {
+            h->relay_obs = nullptr;
+            if (what & kInvalSnap) h->relay_kp_ok = false;
+        } else if (const int rc = relay_invalidate(h, stream, what)) {
+            return rc;
+        }
+    }
+    if (host_only || !h->device_seq) return PMENV_OK;
     // V = 0 clears both (a stale V re-primes the halo too); HOBS = 0 only the halo
     const hipError_t e = (what & kInvalSnap) ? hipMemsetAsync(h->seq + 2, 0, 4, stream)
                                              : hipMemsetAsync(h->seq + 4, 0, 8, stream);
@@ -104,6 +126,43 @@ int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInva
         set_err(h, "invalidating the flat step's snapshot: %s", hipGetErrorString(e));
         return PMENV_ERR_HIP;
     }
+    return PMENV_OK;
+}
+
+// The relay step's memory (zeroed: the device-sequenced words, no relay word of any epoch), allocated
+// when AUTO gives the shape the relay step or pmenv_set_step_path asks for it — not on a step.
+int relay_alloc(pmenv* h) {
+    if (h->relay_mem || !h->relay_ok) return PMENV_OK;
+    const pmenv_cfg& c = h->cfg;
+    const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
+    auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
+    const size_t ctl_b = 64, words_b = up16(BN * 8), kp_b = up16(B * 4);
+    const size_t hal = up16((size_t)h->relay_tiles * 32);
+    const size_t bytes = ctl_b + words_b + 2 * kp_b + 2 * hal;
+    DeviceGuard g(h->device);
+    void* m = nullptr;
+    hipError_t ae = hipMalloc(&m, bytes);
+    if (ae != hipSuccess) {
+        set_err(h, "hipMalloc(relay) failed: %s", hipGetErrorString(ae));
+        return PMENV_ERR_HIP;
+    }
+    ae = hipMemset(m, 0, ctl_b + words_b);
+    if (ae != hipSuccess) {
+        (void)hipFree(m);
+        set_err(h, "relay words: %s", hipGetErrorString(ae));
+        return PMENV_ERR_HIP;
+    }
+    char* b = (char*)m;
+    h->relay_mem = m;
+    h->relay_seq = (uint32_t*)b;
+    h->relay_w = (uint64_t*)(b + ctl_b);
+    h->relay_kp = (int32_t*)(b + ctl_b + words_b);
+    h->relay_halo = (float*)(b + ctl_b + words_b + 2 * kp_b);
+    h->relay_halo_stride = (uint32_t)(hal / 4);
+    h->relay_obs = nullptr;
+    h->relay_kp_ok = false;
+    h->relay_par = 0;
+    h->relay_epoch = 0;
     return PMENV_OK;
 }
 
@@ -243,6 +302,12 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     }
     h->rows_per_tile = R;
     h->vec = vec;
+    // the register step: the env's window within BLOCK x E floats (one workgroup per env)
+    {
+        const int64_t nwf = (int64_t)c.num_assets * WF;
+        h->small_block = nwf <= 256 * 16 ? 256 : nwf <= 512 * 16 ? 512 : nwf <= 1024 * 16 ? 1024 : 0;
+        h->small_e = nwf <= 256 * 8 ? 8 : 16;
+    }
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
@@ -481,37 +546,11 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
     }
     if (h->relay_ok) {
-        // the relay words (zero: no epoch yet), the counter copy's and the in-place halo's
-        // two parities
         const uint32_t cpw = (uint32_t)(h->relay_block * h->relay_v);
-        const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
         h->relay_epb = (h->relay_block / 64) * (64 / h->relay_kl);
         h->relay_tiles = (h->flat_qtot + cpw - 1) / cpw;
-        h->relay_scal = (uint32_t)((B + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
-        auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
-        const size_t words_b = BN * 8, kp_b = up16(B * 4);
-        const size_t hal = up16((size_t)h->relay_tiles * 32);
-        hipError_t ae = hipMalloc(&h->relay_mem, up16(words_b) + 2 * kp_b + 2 * hal);
-        if (ae != hipSuccess) {
-            set_err(h, "hipMalloc(relay) failed: %s", hipGetErrorString(ae));
-            h->relay_mem = nullptr;
-            return fail(PMENV_ERR_HIP);
-        }
-        char* m = (char*)h->relay_mem;
-        h->relay_w = (uint64_t*)m;
-        h->relay_kp[0] = (int32_t*)(m + up16(words_b));
-        h->relay_kp[1] = (int32_t*)(m + up16(words_b) + kp_b);
-        h->relay_halo[0] = (float*)(m + up16(words_b) + 2 * kp_b);
-        h->relay_halo[1] = (float*)(m + up16(words_b) + 2 * kp_b + hal);
-        ae = hipMemset(h->relay_w, 0, words_b);
-        if (ae != hipSuccess) {
-            set_err(h, "relay words: %s", hipGetErrorString(ae));
-            return fail(PMENV_ERR_HIP);
-        }
-        h->relay_epoch = 0;
-        h->relay_par = 0;
-        h->relay_obs = nullptr;
-        h->relay_kp_ok = false;
+        h->relay_scal = (uint32_t)(((uint64_t)c.num_envs + (uint64_t)h->relay_epb - 1) / (uint64_t)h->relay_epb);
+        if (h->relay && relay_alloc(h) != PMENV_OK) return fail(PMENV_ERR_HIP);
     }
     (void)flat1_invalidate(h, nullptr, kInvalSnap | kInvalHalo, true);   // no device sequencing yet
     char* base = (char*)h->state;
@@ -527,6 +566,10 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         {(const void*)step_advance_lds_kernel<true>, h->lds_tile},
         {(const void*)step_advance_lds_kernel<false>, h->lds_tile},
         {(const void*)step_surface_kernel, h->lds_surface},
+        {(const void*)step_small_kernel<256, 8>, h->lds_surface},
+        {(const void*)step_small_kernel<256, 16>, h->lds_surface},
+        {(const void*)step_small_kernel<512, 16>, h->lds_surface},
+        {(const void*)step_small_kernel<1024, 16>, h->lds_surface},
         {(const void*)scalar_step_kernel, h->lds_scalar},
     };
     for (const auto& a : attrs)   // only needed above 64 KiB; failures surface at launch
@@ -577,6 +620,7 @@ int pmenv_set_step_path(pmenv* h, int32_t path) {
                    "W >= 2, 16-B granular env windows, N <= 512)", path);
         return PMENV_ERR_ARG;
     }
+    if (rbits && relay_alloc(h) != PMENV_OK) return PMENV_ERR_HIP;
     h->path = path;
     h->one = bits;
     h->flat1 = fbits;
@@ -633,15 +677,14 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         // a step captured into a hipGraph replays with frozen arguments: from then on this
         // handle sequences its flat steps on the device (flat_seq_kernel + the kernel)
         if (!h->device_seq && capturing(stream)) h->device_seq = true;
-        h->relay_obs = nullptr;                // the relay step's halo and counter copy go stale
-        h->relay_kp_ok = false;
         note_capture(h, stream);
+        // the relay step's halo and counter copy go stale
+        if (const int rc = relay_invalidate(h, stream, kInvalSnap | kInvalHalo)) return rc;
         launch_flat1(h, p, stream);
         return check_launch(h, "step_flat_kernel");
     }
-    if (a->bar && h->streaming && obs16 && (h->relay & fuse_bit) && !h->relay_captured && !capturing(stream)) {
-        // one launch, the scalar blocks relaying to the stream tiles (a captured step runs as
-        // two launches: the relay epoch is a host counter; note_capture marks the handle)
+    if (a->bar && h->streaming && obs16 && (h->relay & fuse_bit)) {
+        // one launch, the scalar work relaying to the stream tiles (captured: device-sequenced)
         const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
         if (!(ph & PMENV_PHASE_SCALAR)) return PMENV_OK;
         if (const int rc = flat1_invalidate(h, stream, kInvalSnap | kInvalHalo, false, true)) return rc;
@@ -677,6 +720,10 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         return PMENV_OK;
     }
     if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single-launch path: all done in the scalar phase
+    if (h->small_block) {
+        launch_small(h, p, stream);
+        return check_launch(h, "step_small_kernel");
+    }
     if (h->vec && obs16)
         step_advance_lds_kernel<true><<<B, kBlock, h->lds_tile, stream>>>(p);
     else
@@ -820,7 +867,7 @@ size_t pmenv_state_bytes(const pmenv* h) { return h ? h->state_bytes : 0; }
 
 const char* pmenv_step_path(const pmenv* h) {
     if (!h) return "";
-    if (!h->streaming) return "step_advance_lds_kernel";
+    if (!h->streaming) return h->small_block ? "step_small_kernel" : "step_advance_lds_kernel";
     // per window mode: the one-launch kernel, or the scalar step (K1) then the stream
     const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
                    : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
@@ -830,7 +877,7 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* part[2];
     for (int m = 0; m < 2; ++m) {          // 0 = double-buffered (obs_out), 1 = in place
         const int bit = m ? PMENV_FUSE_INPLACE : PMENV_FUSE_DB;
-        if ((h->relay & bit) && !h->relay_captured) part[m] = "step_relay_kernel";
+        if (h->relay & bit) part[m] = "step_relay_kernel";
         else if (h->flat1 & bit) part[m] = h->cfg.num_assets > 64 ? "step_flat_vec_kernel" : "step_flat_kernel";
         else if (h->one & bit) part[m] = "step_env_kernel";
         else {
@@ -838,8 +885,9 @@ const char* pmenv_step_path(const pmenv* h) {
             part[m] = buf[m];
         }
     }
-    snprintf(out, sizeof out, "%s (obs_out) | %s (in place)%s", part[0], part[1],
-             h->device_seq && h->flat1 ? " [flat steps device-sequenced]" : "");
+    snprintf(out, sizeof out, "%s (obs_out) | %s (in place)%s%s", part[0], part[1],
+             h->device_seq && h->flat1 ? " [flat steps device-sequenced]" : "",
+             h->relay_dseq && h->relay ? " [relay steps device-sequenced]" : "");
     return out;
 }
 

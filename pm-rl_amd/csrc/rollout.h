@@ -247,8 +247,57 @@ __global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const fl
 // chunks, waiting for their flags and reading their maps through agent-scope atomic loads,
 // and the parts are composed in order through LDS — and walks its registers writing adv /
 // ret (nt stores: written once, read by the learner later). Inputs are read once (17 B
-// per element, against 26 for the maps + apply split) and a workgroup only waits for
-// chunks dispatched before it, which never wait for it, so every wait ends.
+// per element, against 26 for the maps + apply split).
+//
+// Forward progress does not rest on dispatch order: a wave that has waited kLbSpin polls for
+// a later chunk's flag computes that chunk's map itself, from the inputs, with the producer's
+// own code and association order (lb_wave_map folded as the publisher folds), so the bits are
+// the producer's and the wait always ends — whatever order the hardware dispatches workgroups
+// in (with the usual later-chunks-first dispatch the fallback never runs).
+constexpr int kLbSpin = 4096;
+
+template <int U>
+__device__ __forceinline__ void lb_load_wave(const __amdgpu_buffer_rsrc_t& rs_r, const __amdgpu_buffer_rsrc_t& rs_v,
+                                             const __amdgpu_buffer_rsrc_t& rs_d, uint32_t voff, uint32_t row, int B,
+                                             int t0, int seg_end, float* vv, float* rr, uint32_t& alive) {
+    alive = 0;
+#pragma unroll
+    for (int u = 0; u <= U; ++u) {                // v has T + 1 rows: row seg_end closes the chunk
+        const uint32_t t = (uint32_t)min(t0 + u, seg_end);
+        vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
+        rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
+        const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
+        alive |= (dn ? 0u : 1u) << u;
+    }
+}
+
+// one wave's U days reduced to its map (C, D) and the days' deltas
+template <int U>
+__device__ __forceinline__ void lb_wave_map(const float* vv, const float* rr, uint32_t alive, int t0, int seg_end,
+                                            double g, double gl, double* dl, double& C, double& D) {
+    C = 1.0;
+    D = 0.0;
+#pragma unroll
+    for (int u = U - 1; u >= 0; --u) {
+        const double n = (alive >> u) & 1u ? 1.0 : 0.0;
+        dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
+        if (t0 + u < seg_end) {
+            D = dl[u] + gl * n * D;
+            C = gl * n * C;
+        }
+    }
+}
+
+// the publisher's fold of the NW waves' maps (wave NW-1 first)
+__device__ __forceinline__ void lb_fold(double Cj, double Dj, double& Ca, double& Da) {
+    Da = Dj + Cj * Da;
+    Ca = Cj * Ca;
+}
+
 template <int NW, int U>
 __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, const float* v, const uint8_t* dones,
                                                               float* adv, float* ret, int T, int B, float gamma,
@@ -276,30 +325,11 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, c
     const int seg_start = c * S, seg_end = min(T, seg_start + S);
     const int t0 = seg_start + w * U;
     float vv[U + 1], rr[U];
-    uint32_t alive = 0;
-#pragma unroll
-    for (int u = 0; u <= U; ++u) {                // v has T + 1 rows: row seg_end closes the chunk
-        const uint32_t t = (uint32_t)min(t0 + u, seg_end);
-        vv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, voff, t * row, 0));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t t = (uint32_t)min(t0 + u, seg_end - 1);
-        rr[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_r, voff, t * row, 0));
-        const uint32_t dn = __builtin_amdgcn_raw_buffer_load_b8(rs_d, voff >> 2, t * (uint32_t)B, 0);
-        alive |= (dn ? 0u : 1u) << u;
-    }
+    uint32_t alive;
+    lb_load_wave<U>(rs_r, rs_v, rs_d, voff, row, B, t0, seg_end, vv, rr, alive);
     double dl[U];
-    double C = 1.0, D = 0.0;
-#pragma unroll
-    for (int u = U - 1; u >= 0; --u) {
-        const double n = (alive >> u) & 1u ? 1.0 : 0.0;
-        dl[u] = (double)rr[u] + g * n * (double)vv[u + 1] - (double)vv[u];
-        if (t0 + u < seg_end) {
-            D = dl[u] + gl * n * D;
-            C = gl * n * C;
-        }
-    }
+    double C, D;
+    lb_wave_map<U>(vv, rr, alive, t0, seg_end, g, gl, dl, C, D);
     shC[w][lane] = C;
     shD[w][lane] = D;
     __syncthreads();
@@ -307,10 +337,7 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, c
     double* mapD = maps + (size_t)nC * B;
     if (w == 0) {                                 // publish the chunk's map
         double Ca = 1.0, Da = 0.0;
-        for (int j = NW - 1; j >= 0; --j) {
-            Da = shD[j][lane] + shC[j][lane] * Da;
-            Ca = shC[j][lane] * Ca;
-        }
+        for (int j = NW - 1; j >= 0; --j) lb_fold(shC[j][lane], shD[j][lane], Ca, Da);
         if (ok) {
             __hip_atomic_store(mapC + (size_t)c * B + b, Ca, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(mapD + (size_t)c * B + b, Da, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -329,7 +356,34 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, c
             const int j = base + lane;
             bool ready = j >= j1 || __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT) == epoch;
-            while (!__all(ready)) {
+            for (int spin = 0; !__all(ready); ++spin) {
+                if (spin >= kLbSpin) {
+                    // the producers of the chunks still missing may not be running: compute
+                    // their maps here (all 64 lanes, one chunk at a time), as they would
+                    uint64_t miss = __ballot(!ready);
+                    while (miss) {
+                        const int jm = base + (int)__builtin_ctzll(miss);
+                        miss &= miss - 1;
+                        double Ca = 1.0, Da = 0.0;
+                        const int s0 = jm * S, s1 = min(T, s0 + S);
+                        for (int jw = NW - 1; jw >= 0; --jw) {
+                            float fv[U + 1], fr[U];
+                            uint32_t fa;
+                            double fdl[U], Cj, Dj;
+                            lb_load_wave<U>(rs_r, rs_v, rs_d, voff, row, B, s0 + jw * U, s1, fv, fr, fa);
+                            lb_wave_map<U>(fv, fr, fa, s0 + jw * U, s1, g, gl, fdl, Cj, Dj);
+                            lb_fold(Cj, Dj, Ca, Da);
+                        }
+                        if (ok) {                 // the producer's values: a race of equal stores
+                            __hip_atomic_store(mapC + (size_t)jm * B + b, Ca, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(mapD + (size_t)jm * B + b, Da, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    ready = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 if (!ready)
                     ready = __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,

@@ -19,12 +19,26 @@
 //     (the pattern rocPRIM's look-back scan state uses on gfx942 / gfx950: atomic loads /
 //     stores that bypass the non-coherent L2).
 // A tile only ever waits for scalar blocks, which come before every tile in dispatch order
-// and never wait, so every wait ends. Scalar blocks placed only `lead` tiles ahead of their
-// first consumer measured slower at every lead tried: 4,096 x 30 in place 41.2 us at 8,192
-// tiles against 40.7 with every scalar block first, 8,192 x 30 80.4 at 16,384 against 78.6,
-// 16-27 % slower at a 1,024-tile lead (profiles/ab_r04/relay_lead2_r04t.err,
-// relay_lead_r04l.err, relay_r04r.err): the first tiles wait for a scalar block either way,
-// and the ones that come later find their w' relayed.
+// and never wait, so every wait ends. That is a property of the hardware, not a HIP guarantee:
+// the command processor dispatches a grid's workgroups in blockIdx order (round-robin over the
+// XCDs, in order within each), and the product relies on it here (include/pmenv.h states it as
+// a requirement of the relay step). The alternative that does not — an ordered ticket, one
+// agent-scope fetch-add per workgroup on one counter (rocPRIM's ordered block id) — measured
+// 4.7x slower: the ~15,900 same-address atomics of a 4,096 x 30 step serialise at ~10 ns each
+// (194.9 against 41.0 us in place, 383.0 against 80.4 at 8,192 x 30; profiles/ab_r05/). Scalar
+// blocks placed only `lead` tiles ahead of their first consumer measured slower at every lead
+// tried: 4,096 x 30 in place 41.2 us at 8,192 tiles against 40.7 with every scalar block first,
+// 8,192 x 30 80.4 at 16,384 against 78.6, 16-27 % slower at a 1,024-tile lead
+// (profiles/ab_r04/relay_lead2_r04t.err, relay_lead_r04l.err, relay_r04r.err): the first tiles
+// wait for a scalar block either way, and the ones that come later find their w' relayed.
+//
+// Epoch and parity: eager steps take them from the host (launch arguments). A handle seen under
+// stream capture sequences its relay steps on the device instead (graph replays must not
+// replay frozen arguments): relay_prime_kernel, launched before every such step, reads the
+// device words {D, E, V, HOBS}, re-primes the copies of parity D when V / HOBS say so, and
+// publishes {C = D, EC = E + 1} for the step, which reads only C and EC and writes D = 1 - C,
+// E = EC, V = 1 and HOBS for the next one (no launch reads a word it or a concurrent block
+// writes).
 //
 // In place, the two chunks past a tile belong to the next tile, which may already have
 // stored them: they come from a halo the next tile wrote in the previous step (its first
@@ -42,13 +56,25 @@ namespace pmenv_dev {
 
 struct RelayParams {
     uint32_t scal;           // scalar blocks (the first `scal` blocks of the grid)
+    uint32_t epoch;          // eager: this step's tag (never 0: the words start zeroed)
     uint64_t* w;             // [B * N] {epoch, w' bits}
-    const int32_t* kp_in;    // [B] the counter before this step (parity p: written by the last relay step or primed)
-    int32_t* kp_out;         // [B] the counter after it (parity 1 - p: the next relay step's kp_in)
-    const float* halo_in;    // in place: [tiles - 1][2] float4, this step's input chunks past each tile
-    float* halo_out;         // in place: the same for the next step (written by the tiles)
-    uint32_t epoch;          // this step's tag (never 0: the words start zeroed)
+    // eager: this step's copies (parity p: the counter before the step and, in place, its input
+    // chunks past each tile; parity 1 - p: the same for the next step, written by this one)
+    const int32_t* kp_in;
+    int32_t* kp_out;
+    const float* halo_in;    // [tiles - 1][2] float4
+    float* halo_out;
+    // device-sequenced (step_relay_kernel<..., SEQ = true>): the parity-0 bases, parity 1 at
+    // +B / +halo_stride, and the words {D, E, V, C, EC, pad, HOBS lo, HOBS hi}
+    uint32_t* seq;
+    int32_t* kp;
+    float* halo;
+    uint32_t B;
+    uint32_t halo_stride;
+    const float* obs;        // the window (HOBS of a device-sequenced in-place step)
+    uint32_t par;            // eager: this step's parity (relay_prime_kernel's copies)
 };
+enum { kSeqD = 0, kSeqE = 1, kSeqV = 2, kSeqC = 3, kSeqEC = 4, kSeqHobs = 6 };
 
 __device__ __forceinline__ void relay_put(uint64_t* w, uint32_t epoch, uint32_t bits) {
     __hip_atomic_store(w, ((uint64_t)epoch << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -63,7 +89,8 @@ __device__ __forceinline__ uint64_t relay_get(const uint64_t* w) {
 // through the relay words; the counter of the next step goes to kp_out (read after this
 // launch has ended).
 template <int BLOCK, int KL, int KA>
-__device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayParams& r, int s) {
+__device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayParams& r, int s, uint32_t epoch,
+                                             int32_t* kp_out) {
     constexpr int EPW = 64 / KL, EPB = (BLOCK / 64) * EPW;
     const int lane = threadIdx.x & 63;
     const int b = s * EPB + (int)(threadIdx.x >> 6) * EPW + lane / KL;
@@ -73,8 +100,8 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
     if constexpr (KA == 0) {
         const ScalarIn in = scalar_load<KL>(p, b, lane);
         const ScalarMid m = scalar_core<KL>(p, b, lane, in);
-        if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, r.epoch, __float_as_uint(m.wp));
-        if (env_ok && j == 0) r.kp_out[b] = m.k + 1;
+        if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, epoch, __float_as_uint(m.wp));
+        if (env_ok && j == 0) kp_out[b] = m.k + 1;
         scalar_tail<KL>(p, b, lane, in, m);
     } else {
         const VecIn<KA> in = vec_load<KL, KA, true>(p, b, lane);
@@ -82,9 +109,9 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
 #pragma unroll
         for (int e = 0; e < KA; ++e) {
             const int n = j + e * KL;
-            if (env_ok && n < N) relay_put(r.w + (size_t)b * N + n, r.epoch, __float_as_uint(m.wp[e]));
+            if (env_ok && n < N) relay_put(r.w + (size_t)b * N + n, epoch, __float_as_uint(m.wp[e]));
         }
-        if (env_ok && j == 0) r.kp_out[b] = in.k + 1;
+        if (env_ok && j == 0) kp_out[b] = in.k + 1;
         vec_tail<KL, KA, true>(p, b, lane, in, m);
     }
 }
@@ -94,11 +121,11 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
 // needing neither bar nor w' before reading the relay words, and the last-day / slot chunks
 // after, ran 1.1-1.4x slower: the deferred 16-B chunks leave partly written lines between the
 // two store waves — profiles/ab_r04/relay_split_r04s.err.)
-// OUT: double-buffered (the chunks past the tile read straight from obs). WAIT = false (tools
-// ablation only: the stream's cost inside this kernel, wrong results): no wait for the words.
-template <int BLOCK, int V, int POL, bool OUT, bool WAIT = true, int ABL = 0>
+// OUT: double-buffered (the chunks past the tile read straight from obs).
+template <int BLOCK, int V, int POL, bool OUT>
 __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
-                                           f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
+                                           uint32_t epoch, const int32_t* kp_in, const float* halo_in,
+                                           float* halo_out, f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -110,7 +137,7 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
     const uint32_t ntiles = (qtot + CPW - 1) / CPW;
     const uint32_t nh = t + 1 < ntiles ? min(2u, qtot - c0 - nblk) : 0u;
-    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : r.halo_in + (size_t)t * 8;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : halo_in + (size_t)t * 8;
     const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
     __builtin_amdgcn_sched_barrier(0);
     // the tile's rows g_lo .. g_hi (global row = b N + n): thread i stages row g_lo + i
@@ -129,18 +156,16 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     f4 xb = f4{nanv, nanv, nanv, nanv};
     int32_t kc = 0;
     uint64_t ww = 0;
-    if (!(ABL & 1) || mine) {                                       // ABL & 1 (tools): only the staging threads load
-        if (barb) xb = *reinterpret_cast<const f4*>(barb + (size_t)n * 4);
-        kc = r.kp_in[b];
-        // w': relayed by the scalar blocks placed before this tile
-        ww = relay_get(r.w + g);
-    }
-    bool ready = !WAIT || !mine || (uint32_t)(ww >> 32) == r.epoch;
+    if (barb) xb = *reinterpret_cast<const f4*>(barb + (size_t)n * 4);
+    kc = kp_in[b];
+    // w': relayed by the scalar blocks placed before this tile
+    ww = relay_get(r.w + g);
+    bool ready = !mine || (uint32_t)(ww >> 32) == epoch;
     while (!__all(ready)) {
         __builtin_amdgcn_s_sleep(2);
         if (!ready) {
             ww = relay_get(r.w + g);
-            ready = (uint32_t)(ww >> 32) == r.epoch;
+            ready = (uint32_t)(ww >> 32) == epoch;
         }
     }
     if (mine) {
@@ -171,7 +196,7 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
             xwp = sh_wp[i];
         });
         buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
-        if (!(ABL & 2) && first_out && j < 2) reinterpret_cast<f4*>(r.halo_out)[2 * (t - 1) + j] = o;   // ABL & 2: timing only
+        if (first_out && j < 2) reinterpret_cast<f4*>(halo_out)[2 * (t - 1) + j] = o;
     }
 }
 
@@ -179,23 +204,69 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
 // policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar), OCC the waves
 // per SIMD the kernel is held to (the 8-assets-per-lane form would otherwise take 84 VGPRs
 // and cut the tiles to 5 waves per SIMD)
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1>
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1, bool SEQ = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void step_relay_kernel(
     StepParams p, RelayParams r, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
     __shared__ f4 sh_bar[BLOCK];
     __shared__ float sh_wp[BLOCK];
     __shared__ int32_t sh_kc[BLOCK];
-    if (blockIdx.x < r.scal) relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
-    else relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
+    uint32_t epoch = r.epoch;
+    const int32_t* kp_in = r.kp_in;
+    int32_t* kp_out = r.kp_out;
+    const float* halo_in = r.halo_in;
+    float* halo_out = r.halo_out;
+    if constexpr (SEQ) {                         // relay_prime_kernel published C and EC
+        const uint32_t par = __builtin_amdgcn_readfirstlane(r.seq[kSeqC]);
+        epoch = __builtin_amdgcn_readfirstlane(r.seq[kSeqEC]);
+        kp_in = r.kp + (size_t)par * r.B;
+        kp_out = r.kp + (size_t)(par ^ 1u) * r.B;
+        halo_in = r.halo + (size_t)par * r.halo_stride;
+        halo_out = r.halo + (size_t)(par ^ 1u) * r.halo_stride;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {   // what the next step finds
+            const uint64_t hobs = OUT ? 0ull : (uint64_t)(uintptr_t)r.obs;
+            r.seq[kSeqD] = par ^ 1u;
+            r.seq[kSeqE] = epoch;
+            r.seq[kSeqV] = 1u;
+            r.seq[kSeqHobs] = (uint32_t)hobs;
+            r.seq[kSeqHobs + 1] = (uint32_t)(hobs >> 32);
+        }
+    }
+    if (blockIdx.x < r.scal)
+        relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x, epoch, kp_out);
+    else
+        relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, epoch, kp_in, halo_in, halo_out, sh4, sh_bar,
+                                       sh_wp, sh_kc);
 }
 
-// the relay step's copies when the previous relay step's do not hold: kp <- the state's
-// counter, and in place halo[i] <- chunks (i + 1) * CPW and + 1 of the window
-static __global__ __launch_bounds__(256) void relay_prime_kernel(StepParams p, int32_t* kp) {
-    copy_halo(p);
-    if (kp)
-        for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < p.B; b += gridDim.x * blockDim.x) kp[b] = p.k[b];
+// The relay step's copies of parity D (eager: r.par; device-sequenced: the word D): kp[D] <- the
+// state's counter (when `prime_kp`), and in place halo[D][i] <- chunks (i + 1) * CPW and + 1 of
+// the window (when p.halo, the parity-0 base). Device-sequenced (`seq`): V == 0 re-primes both,
+// HOBS != this window the halo, and block 0 publishes C = D and EC = E + 1 for the step.
+static __global__ __launch_bounds__(256) void relay_prime_kernel(StepParams p, RelayParams r, int prime_kp, int seq) {
+    uint32_t d = r.par;
+    bool kp = prime_kp != 0, halo = p.halo != nullptr;
+    if (seq) {
+        d = __builtin_amdgcn_readfirstlane(r.seq[kSeqD]);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(r.seq[kSeqE]);
+        const uint32_t v = __builtin_amdgcn_readfirstlane(r.seq[kSeqV]);
+        const uint64_t hobs = (uint64_t)__builtin_amdgcn_readfirstlane(r.seq[kSeqHobs]) |
+                              ((uint64_t)__builtin_amdgcn_readfirstlane(r.seq[kSeqHobs + 1]) << 32);
+        kp = v == 0;
+        halo = halo && (v == 0 || hobs != (uint64_t)(uintptr_t)p.obs);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            r.seq[kSeqC] = d;
+            r.seq[kSeqEC] = e + 1u == 0u ? 1u : e + 1u;     // never the zeroed words' 0
+        }
+    }
+    if (halo) {
+        p.halo += (size_t)d * r.halo_stride;
+        copy_halo(p);
+    }
+    if (kp) {
+        int32_t* kpd = r.kp + (size_t)d * r.B;
+        for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < p.B; b += gridDim.x * blockDim.x) kpd[b] = p.k[b];
+    }
 }
 
 }  // namespace pmenv_dev

@@ -62,25 +62,33 @@ def allreduce_grads(params, loss_sum, count, group=None):
     f64 bucket: the gradients of a small policy are a few hundred KB, one latency-bound
     exchange over xGMI), then every gradient is divided by the global count. Returns
     (global loss sum, global count) as python floats."""
-    # every parameter, in order, on every rank: a parameter without a gradient (a rank with
-    # no envs, a branch unused there) contributes zeros, so the buckets line up over ranks
+    # every parameter, in order, on every rank: a parameter without a gradient here (a rank
+    # with no envs, a branch unused there) contributes zeros, so the buckets line up over
+    # ranks, and a has-gradient flag per parameter rides in the same bucket: a gradient is
+    # written back only to trainable parameters some rank produced one for, so frozen or
+    # unused parameters keep grad None and optimizers skip them as they would on one rank
     ps = list(params)
     if not ps:
         raise ValueError("allreduce_grads needs the replicated parameters")
     dev = ps[0].device
-    for p in ps:
-        if p.grad is None:
-            p.grad = torch.zeros_like(p)
-    parts = [p.grad.detach().reshape(-1).to(device=dev, dtype=torch.float64) for p in ps]
+    parts = [(p.grad.detach().reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device))
+             .to(device=dev, dtype=torch.float64) for p in ps]
+    has = torch.tensor([1.0 if p.grad is not None else 0.0 for p in ps], dtype=torch.float64, device=dev)
     extra = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64).reshape(()).to(dev),
                          torch.tensor(float(count), dtype=torch.float64, device=dev)])
-    bucket = torch.cat(parts + [extra])
+    bucket = torch.cat(parts + [has, extra])
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     total, n = float(bucket[-2]), float(bucket[-1])
+    flags = bucket[-2 - len(ps):-2].tolist()
     off = 0
-    for p in ps:
-        k = p.grad.numel()
-        p.grad.copy_((bucket[off:off + k] / n).reshape(p.grad.shape).to(device=p.grad.device, dtype=p.grad.dtype))
+    for p, f in zip(ps, flags):
+        k = p.numel()
+        if f > 0 and p.requires_grad:
+            g = (bucket[off:off + k] / n).reshape(p.shape).to(device=p.device, dtype=p.dtype)
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.copy_(g)
         off += k
     return total, n

@@ -177,18 +177,22 @@ def _grads_worker(rank, world, port, root, q):
     x = torch.arange(6, dtype=torch.float64).reshape(2, 3) * (rank + 1)
     # rank 0 uses both heads; rank 1 (say, a shard without envs of one kind) only the first:
     # its second head's grads stay None
+    # c: no rank uses it; a's bias frozen — both must keep grad None (optimizers then skip them)
+    c = torch.nn.Linear(3, 1).double()
     loss = a(x).sum() + (b(x).sum() if rank == 0 else 0.0)
+    a.bias.requires_grad_(False)
     loss.backward()
-    params = list(a.parameters()) + list(b.parameters())
+    params = list(a.parameters()) + list(b.parameters()) + list(c.parameters())
     total, n = allreduce_grads(params, loss.detach(), 2.0)
-    q.put((rank, total, n, [p.grad.clone().numpy() for p in params]))
+    q.put((rank, total, n, [None if p.grad is None else p.grad.clone().numpy() for p in params]))
     dist.destroy_process_group()
 
 
 def test_allreduce_grads_aligns_buckets_when_a_rank_has_no_grad():
     """A parameter without a gradient on one rank contributes zeros: the ranks' buckets keep
     the same length and order (a mismatch would hang or mix gradients), and every rank ends
-    with the same averaged gradients."""
+    with the same averaged gradients; parameters no rank has a gradient for, and frozen
+    ones, keep grad None."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -201,7 +205,10 @@ def test_allreduce_grads_aligns_buckets_when_a_rank_has_no_grad():
         p.join(timeout=60)
     (_, t0, n0, g0), (_, t1, n1, g1) = res
     assert n0 == n1 == 4.0 and t0 == t1
+    # a.weight, a.bias (frozen), b.weight, b.bias, c.weight, c.bias (unused everywhere)
+    assert g0[1] is None and g1[1] is None and g0[4] is None and g0[5] is None and g1[4] is None
     for x, y in zip(g0, g1):
-        assert np.array_equal(x, y)
-    # the second head's bias: rank 0's sum d/db = 2 rows, rank 1 none -> 2 / 4
-    assert np.allclose(g0[-1], [0.5])
+        assert (x is None and y is None) or np.array_equal(x, y)
+    # the second head's bias: rank 0's sum d/db = 2 rows, rank 1 none -> 2 / 4 (and rank 1,
+    # which had no gradient for it, receives the average)
+    assert np.allclose(g0[3], [0.5]) and np.allclose(g1[3], [0.5])

@@ -62,7 +62,7 @@ def replay_gpu(g, mode, host=False, impl="auto", direct=True):
                 out["rets"][i] = float(env.info["returns"][-1][0])
                 out["wpost"][i] = env.info["actions"][-1][0].cpu().numpy()
         out["values"][i] = float(env.value)
-        out["chans"][i] = obs[:, :, -1].cpu().numpy()
+        out["chans"][i] = obs[:, :, -1].cpu().numpy().copy()     # host windows advance in place
     return out
 
 
@@ -499,7 +499,7 @@ def test_gpu_step_impl_selection_rules():
     assert TradingEnv(num_envs=2, num_assets=64, window=47, device=DEV).step_path.count("step_env_kernel") == 2
     assert "step_env_kernel" not in TradingEnv(num_envs=2, num_assets=65, window=4, device=DEV).step_path
     odd = TradingEnv(num_envs=2, num_assets=5, window=50, device=DEV)           # not 16-B granular
-    assert odd.step_path == "step_advance_lds_kernel"
+    assert odd.step_path == "step_small_kernel"
     for impl in ("one_launch", "two_launch"):
         with pytest.raises(ValueError):
             odd.set_step_impl(impl)
@@ -529,6 +529,27 @@ def test_gpu_out_must_not_overlap():
 def test_gpu_vs_oracle_shapes(N, W, F, B):
     kw = {} if F == 5 else {"close_channel": F - 2}
     _run_both(kw, B=B, N=N, W=W, T=2 * W + 3, kind="mixed", F=F, seed=N * 1000 + W)
+
+
+@pytest.mark.parametrize("N,W,F,B,path", [
+    (5, 50, 5, 3, "step_small_kernel"),        # config 1: 250-float rows, 256 x 8
+    (8, 50, 8, 3, "step_small_kernel"),        # 3,200 floats: 256 x 16
+    (32, 32, 8, 5, "step_small_kernel"),       # config/base.py with F = 8: 8,192 floats, 512 x 16
+    (30, 50, 8, 4, "step_small_kernel"),       # 12,000 floats: 1,024 x 16
+    (3, 7, 5, 9, "step_small_kernel"),         # 105 floats, most lanes idle
+    (7, 10, 3, 6, "step_small_kernel"),
+    (30, 50, 12, 3, "step_advance_lds_kernel"),   # 18,000 floats: past the register step
+])
+@pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
+                         ids=["storage", "chrono", "commission"])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_register_step_vs_oracle(N, W, F, B, path, kw, db):
+    """step_small_kernel (one workgroup per env, the window in VGPRs, any F and alignment)
+    and the LDS fallback past its 16,384 floats, against the oracle past the ring's wrap."""
+    from pmenv import TradingEnv
+    kw = dict(kw, **({} if F == 5 else {"close_channel": F - 2}))
+    assert TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, **kw).step_path == path
+    _run_both(kw, B=B, N=N, W=W, T=2 * W + 3, kind="mixed", F=F, seed=N * 100 + W * 10 + F, double_buffer=db)
 
 
 def test_gpu_masked_reset_mid_run():

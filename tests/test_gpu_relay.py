@@ -131,41 +131,118 @@ def test_gpu_relay_caller_edits_between_steps():
         assert torch.equal(envs[0].value, envs[1].value), f"step {t}: values"
 
 
-def test_gpu_relay_graph_capture_runs_two_launches():
-    """Under stream capture the relay epoch (a host counter) would be frozen in the graph:
-    a captured RELAY step runs as the two-launch path, and eager relay steps before and
-    after the replays keep the same bits as a two-launch env."""
+def _capture(fn):
+    """fn() captured into a CUDA/HIP graph on a side stream."""
+    s = torch.cuda.Stream(DEV)
+    s.wait_stream(torch.cuda.current_stream(DEV))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        out = fn()
+    torch.cuda.current_stream(DEV).wait_stream(s)
+    return g, out
+
+
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_relay_graph_capture_replays_the_relay_step(db):
+    """A captured RELAY step stays step_relay_kernel: its epoch and parity come from the
+    launch counter on the device (the ordered ticket), and the validity of its counter copy
+    and halo from device words the captured invalidations clear. Eager relay steps, replays
+    of a one-step graph and replays of a [reset, step, step] graph interleave, each bitwise
+    equal to an eager two-launch env driven with the same inputs."""
     from pmenv import TradingEnv, synth
-    B, N, W, T = 512, 30, 20, 12
-    ser = synth.series(W + T, B, N, seed=31, device=DEV)
-    act = synth.actions(T, B, N, seed=32, device=DEV)
+    B, N, W, T = 512, 30, 20, 16
+    ser = synth.series(W + T + 8, B, N, seed=31, device=DEV)
+    act = synth.actions(T + 8, B, N, seed=32, device=DEV)
+    er = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="relay")
+    et = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
+    o_r, o_t = synth.window_from_series(ser, W), synth.window_from_series(ser, W)
+    nx_r, nx_t = torch.empty_like(o_r), torch.empty_like(o_t)
+    er.reset(o_r)
+    et.reset(o_t)
+
+    def step(e, a, o, bar, nx):
+        if db:
+            r, _ = e.step(a, o, bar=bar, out=nx)
+            o.copy_(nx)
+            return r
+        return e.step(a, o, bar=bar)[0]
+
+    a_buf, b_buf = act[0].clone(), ser[W].clone()
+    for t in range(3):                                   # eager relay steps
+        step(er, act[t], o_r, ser[W + t], nx_r)
+        step(et, act[t], o_t, ser[W + t], nx_t)
+    g1, r_cap = _capture(lambda: step(er, a_buf, o_r, b_buf, nx_r))
+    assert "step_relay_kernel" in er.step_path and "relay steps device-sequenced" in er.step_path, er.step_path
+    w_buf = synth.window_from_series(ser, W)             # graph 2's reset window
+
+    def reset_and_two():
+        er.reset(o_r)
+        step(er, a_buf, o_r, b_buf, nx_r)
+        return step(er, a_buf, o_r, b_buf, nx_r)
+    g2, r2_cap = _capture(reset_and_two)
+    # the capture ran nothing: re-sync the relay env to the two-launch env's state and window
+    er.load_state_dict(et.state_dict())
+    o_r.copy_(o_t)
+    for t in range(3, T):
+        a_buf.copy_(act[t])
+        b_buf.copy_(ser[W + t])
+        if t % 4 == 0:                                   # graph 2: reset, then two steps (same inputs)
+            o_r.copy_(w_buf)
+            o_t.copy_(w_buf)
+            g2.replay()
+            et.reset(o_t)
+            step(et, act[t], o_t, ser[W + t], nx_t)
+            rt = step(et, act[t], o_t, ser[W + t], nx_t)
+            rr = r2_cap
+        elif t % 4 == 1:                                 # eager relay step
+            rr = step(er, act[t], o_r, ser[W + t], nx_r)
+            rt = step(et, act[t], o_t, ser[W + t], nx_t)
+        else:                                            # graph 1: one relay step
+            g1.replay()
+            rr = r_cap
+            rt = step(et, act[t], o_t, ser[W + t], nx_t)
+        torch.cuda.synchronize(DEV)
+        assert torch.equal(rr, rt), f"t {t}: rewards"
+        assert torch.equal(o_r, o_t), f"t {t}: windows"
+        assert torch.equal(er.value, et.value), f"t {t}: values"
+
+
+def test_gpu_relay_after_replays_of_another_path():
+    """A handle captured while another path was current, its graph replayed (state and window
+    written where the host does not see it), then switched to RELAY: the relay step re-primes
+    its copies from the device words the replays cleared (no stale host flag), bitwise equal
+    to a two-launch env throughout."""
+    from pmenv import TradingEnv, synth
+    B, N, W, T = 1024, 30, 20, 14
+    ser = synth.series(W + T, B, N, seed=41, device=DEV)
+    act = synth.actions(T, B, N, seed=42, device=DEV)
     er = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="relay")
     et = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="two_launch")
     o_r, o_t = synth.window_from_series(ser, W), synth.window_from_series(ser, W)
     er.reset(o_r)
     et.reset(o_t)
-    a_buf, b_buf = act[0].clone(), ser[W].clone()
-    for t in range(3):                                   # eager relay steps
+    for t in range(2):                                   # eager relay steps: the host flags hold
         er.step(act[t], o_r, bar=ser[W + t])
         et.step(act[t], o_t, bar=ser[W + t])
-    s = torch.cuda.Stream(DEV)
-    s.wait_stream(torch.cuda.current_stream(DEV))
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
-        r_cap, _ = er.step(a_buf, o_r, bar=b_buf)
-    torch.cuda.current_stream(DEV).wait_stream(s)
-    for t in range(3, 8):                                # replays
+    er.set_step_impl("two_launch")
+    a_buf, b_buf = act[0].clone(), ser[W].clone()
+    snap = er.state_dict(), o_r.clone()
+    g, r_cap = _capture(lambda: er.step(a_buf, o_r, bar=b_buf)[0])
+    er.load_state_dict(snap[0])
+    o_r.copy_(snap[1])
+    er.set_step_impl("relay")
+    for t in range(2, T):
         a_buf.copy_(act[t])
         b_buf.copy_(ser[W + t])
-        g.replay()
-        rt, _ = et.step(act[t], o_t, bar=ser[W + t])
+        if t in (5, 6, 9):                               # replays of the captured two-launch step
+            g.replay()
+            rr = r_cap
+        else:
+            rr = er.step(act[t], o_r, bar=ser[W + t])[0]
+        rt = et.step(act[t], o_t, bar=ser[W + t])[0]
         torch.cuda.synchronize(DEV)
-        assert torch.equal(r_cap, rt), f"replay {t}"
-        assert torch.equal(o_r, o_t), f"replay {t}: windows"
-    for t in range(8, T):                                # eager relay steps again
-        rr, _ = er.step(act[t], o_r, bar=ser[W + t])
-        rt, _ = et.step(act[t], o_t, bar=ser[W + t])
-        assert torch.equal(rr, rt) and torch.equal(o_r, o_t), f"step {t}"
+        assert torch.equal(rr, rt), f"t {t}: rewards"
+        assert torch.equal(o_r, o_t), f"t {t}: windows"
 
 
 @pytest.mark.parametrize("B,N", [(8192, 30), (4096, 30), (65536, 30), (8192, 500)])

@@ -408,21 +408,6 @@ __global__ __launch_bounds__(64 * NW) void gae_chunk_kernel(const float* r, cons
     }
 }
 
-// step_relay_kernel whose scalar role raises its waves' issue priority (PMENV_RELAY_PRIO), so
-// the chains the first tiles wait for are not slowed by the tiles' waves on the same CUs
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int PRIO>
-__global__ __launch_bounds__(BLOCK) void step_relay_prio_kernel(StepParams p, RelayParams r, uint32_t qtot) {
-    __shared__ f4 sh4[BLOCK * V + 2];
-    __shared__ f4 sh_bar[BLOCK];
-    __shared__ float sh_wp[BLOCK];
-    __shared__ int32_t sh_kc[BLOCK];
-    if (blockIdx.x < r.scal) {
-        __builtin_amdgcn_s_setprio(PRIO);
-        relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
-    } else {
-        relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
-    }
-}
 
 // the look-back pieces (tools copies of rollout.h gae_lookback_kernel's steps) and the paired form
 template <int NW, int U>
@@ -616,29 +601,5 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback2_kernel(const float* r, 
     lb_walk<NW, U>(kB, dl, a, adv, ret, T, B, cB, w, ok, voff, gl);
 }
 
-// timing-only ablation of the relayed step (PMENV_RELAY_PRIO=2): the scalar blocks exit at
-// once and the tiles do not wait for the relay words — the stream's own cost inside the
-// relay kernel (wrong results: a measurement of the wait, never a path)
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA>
-__global__ __launch_bounds__(BLOCK) void step_relay_nowait_kernel(StepParams p, RelayParams r, uint32_t qtot) {
-    __shared__ f4 sh4[BLOCK * V + 2];
-    __shared__ f4 sh_bar[BLOCK];
-    __shared__ float sh_wp[BLOCK];
-    __shared__ int32_t sh_kc[BLOCK];
-    if (blockIdx.x < r.scal) return;
-    relay_tile<BLOCK, V, POL, OUT, false>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
-}
-
-// relay_tile ablations (PMENV_RELAY_PRIO = 4 + ABL): ABL 1 only the staging threads issue the
-// side loads (the same results), 2 no halo_out stores (timing only), 3 both
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int ABL>
-__global__ __launch_bounds__(BLOCK) void step_relay_abl_kernel(StepParams p, RelayParams r, uint32_t qtot) {
-    __shared__ f4 sh4[BLOCK * V + 2];
-    __shared__ f4 sh_bar[BLOCK];
-    __shared__ float sh_wp[BLOCK];
-    __shared__ int32_t sh_kc[BLOCK];
-    if (blockIdx.x < r.scal) relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x);
-    else relay_tile<BLOCK, V, POL, OUT, true, ABL>(p, r, qtot, blockIdx.x - r.scal, sh4, sh_bar, sh_wp, sh_kc);
-}
 
 }  // namespace pmenv_dev

@@ -34,7 +34,6 @@ int knob_int(const char* name, int dflt) {
 // the knob state of one handle (pmenv::tools)
 struct Tools {
     int k1_occ = 0;             // PMENV_K1_OCC: the 8-asset packed scalar step held to 6 / 8 waves per SIMD
-    int relay_prio = 0;         // PMENV_RELAY_PRIO: the relay step's scalar waves at issue priority 3
     int ablate = 0;             // PMENV_ABLATE: timing-only variants (64 + SKIP: flat stream, 128 + ABL: step_env)
     bool one_nocap = false;     // PMENV_ONE_NOCAP: step_env_kernel without the 80-SGPR cap
     bool flat_s80 = false;      // PMENV_FLAT_S80: the in-place flat stream held to 80 SGPRs
@@ -337,7 +336,6 @@ void plan(pmenv* h) {
     }
     t->ablate = knob_int("PMENV_ABLATE", 0);
     t->k1_occ = knob_int("PMENV_K1_OCC", 0);
-    t->relay_prio = knob_int("PMENV_RELAY_PRIO", 0);
     if (const char* k = knob("PMENV_RELAY_GEOM")) {   // BLOCK x V of relay_geom's table: N <= 64 forms only
         int bk = 0, v = 0;
         const int g = sscanf(k, "%dx%d", &bk, &v) == 2 ? bk * 10 + v : 0;
@@ -560,31 +558,6 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     const int g = h->relay_block * 10 + h->relay_v;
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
-    const Tools* t = tools(h);
-    if (t && t->relay_prio >= 5 && t->relay_prio <= 7 && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {
-        const int abl = t->relay_prio - 4;
-        if (abl == 1) {
-            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 1><<<grid, 256, 0, stream>>>(p, r, q);
-            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 1><<<grid, 256, 0, stream>>>(p, r, q);
-        } else if (abl == 2) {
-            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 2><<<grid, 256, 0, stream>>>(p, r, q);
-            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 2><<<grid, 256, 0, stream>>>(p, r, q);
-        } else {
-            if (out) step_relay_abl_kernel<256, 2, 0, true, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
-            else step_relay_abl_kernel<256, 2, 0, false, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
-        }
-        return true;
-    }
-    if (t && t->relay_prio == 2 && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {   // the no-wait ablation
-        if (out) step_relay_nowait_kernel<256, 2, 0, true, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
-        else step_relay_nowait_kernel<256, 2, 0, false, 32, 0><<<grid, 256, 0, stream>>>(p, r, q);
-        return true;
-    }
-    if (t && t->relay_prio && g == 2562 && h->relay_kl * 100 + h->relay_ka == 3200) {   // PMENV_RELAY_PRIO
-        if (out) step_relay_prio_kernel<256, 2, 0, true, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
-        else step_relay_prio_kernel<256, 2, 0, false, 32, 0, 3><<<grid, 256, 0, stream>>>(p, r, q);
-        return true;
-    }
     switch (g) {
     case 1282: relay_geom<128, 2>(h, p, r, q, grid, out, stream); return true;
     case 1284: relay_geom<128, 4>(h, p, r, q, grid, out, stream); return true;
