@@ -1387,15 +1387,17 @@ __global__ __launch_bounds__(kBlock) void step_advance_lds_kernel(StepParams p) 
 // day the bar's [n, f] (f < F-1); for the weight channel in[j + F] while the ring shifts and
 // in[j] once the storage-order ring is full (it then stays in place) — the one read that
 // waits for the step counter (a scalar load issued with the market loads).
-// Wave 0 runs the env's scalar step meanwhile (the two-launch path's gather_inputs /
-// scalar_compute, LDS scratch); every wave then waits for its loads to have RETURNED
+// Wave 0 runs the env's scalar step meanwhile (N <= 64: the register form, one asset per lane,
+// its state writes and reward after the window's stores as in step_env_kernel; wider envs the
+// LDS-scratch form of gather_inputs / scalar_compute); every wave then waits for its loads to have RETURNED
 // (vmcnt(0)) before the barrier, which closes the in-place read-before-write window of the
 // env — one workgroup owns one env, no other workgroup touches it — and composes and stores
 // dword-wise. Replaces step_advance_lds_kernel's stage-through-LDS rounds (two barriers per
 // row tile, the window loads issued only after the scalar step) for these shapes.
-template <int BLOCK, int E>
+template <int BLOCK, int E, bool REG>
 __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ float sh_wp[REG ? 64 : 1];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
@@ -1408,6 +1410,8 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     const auto rs_bar = make_rsrc(barg ? barg : p.obs, barg ? (uint32_t)(N * Fm) * 4u : 0u);
     const float nanv = __int_as_float(0x7fc00000);
     const int32_t k0 = p.k[b];                            // scalar load, in flight with the market loads
+    ScalarIn sin;
+    if (REG && tid < 64) sin = scalar_load<64>(p, b, tid);   // N <= 64: the register form, one asset per lane
     float src[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {                         // the market channels: in[j + F] or the bar
@@ -1422,7 +1426,11 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
         src[e] = last ? (barg ? bv : nanv) : sh;
     }
     // the weight channel: shifted with the window until the ring is full, then (storage order)
-    // in place (weight_buffer.py:32-44) — the counter decides which float to read
+    // in place (weight_buffer.py:32-44). Small E: both candidates are read at once (no wait for
+    // the counter, one memory round trip); large E: the counter picks the one float to read
+    // (half the registers, the weight loads a round trip later)
+    constexpr bool BOTH = E <= 8;
+    float cur[BOTH ? E : 1];
     const bool shift_w = p.ring_mode == PMENV_RING_CHRONO || k0 < W - 1;
     uint32_t tid2 = (uint32_t)tid;
     asm volatile("" : "+v"(tid2));                        // recompute the indices, do not keep E of them live
@@ -1434,18 +1442,31 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
         const uint32_t t = fdiv(kk, p.div_f);
         const uint32_t f = kk - t * (uint32_t)F;
         const bool wch = j < NWF && (int)f == Fm;
-        const uint32_t off = !wch ? kOut : !shift_w ? j * 4u : (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut;
-        const float wv = buf_load1(rs_in, off);
-        src[e] = wch ? wv : src[e];
+        if constexpr (BOTH) {
+            const float ws = buf_load1(rs_in, wch && (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut);
+            cur[e] = buf_load1(rs_in, wch ? j * 4u : kOut);
+            src[e] = wch ? ws : src[e];
+        } else {
+            const uint32_t off = !wch ? kOut : !shift_w ? j * 4u : (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut;
+            const float wv = buf_load1(rs_in, off);
+            src[e] = wch ? wv : src[e];
+        }
     }
-    if (tid < 64) {
+    ScalarMid mid;
+    if (REG) {
+        if (tid < 64) {
+            mid = scalar_core<64>(p, b, tid, sin);
+            sh_wp[tid] = mid.wp;
+        }
+    } else if (tid < 64) {
         const double v_prev = p.value[b];
         gather_inputs(p, b, s, k0);
         scalar_compute(p, b, s, k0, v_prev);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's window reads are in
     __syncthreads();
-    const int slot = s.ints[1];
+    const int slot = (int)((1 + (int64_t)k0) % W);
+    const float* wps = REG ? sh_wp : s.wp;
     uint32_t tid3 = (uint32_t)tid;
     asm volatile("" : "+v"(tid3));
 #pragma unroll
@@ -1457,11 +1478,14 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
         const uint32_t f = kk - t * (uint32_t)F;
         float v = src[e];
         if ((int)f == Fm && j < NWF) {
-            const float wp = s.wp[row];
-            v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : v);
+            const float wp = wps[row];
+            if constexpr (BOTH) v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : cur[e]);
+            else v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : v);
         }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
     }
+    // the state writes and the reward after the window's stores (the barrier waited for the core only)
+    if (REG && tid < 64) scalar_tail<64>(p, b, tid, sin, mid);
 }
 
 // ---------------------------------------------------------------- surface kernel

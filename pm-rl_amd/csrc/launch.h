@@ -111,15 +111,21 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- the register step (any F)
-inline void launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
+template <bool REG>
+inline void launch_small_r(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const unsigned grid = (unsigned)h->cfg.num_envs;
-    const size_t lds = h->lds_surface;
+    const size_t lds = REG ? 0 : h->lds_surface;
     switch (h->small_block * 100 + h->small_e) {
-    case 25608: step_small_kernel<256, 8><<<grid, 256, lds, stream>>>(p); break;
-    case 25616: step_small_kernel<256, 16><<<grid, 256, lds, stream>>>(p); break;
-    case 51216: step_small_kernel<512, 16><<<grid, 512, lds, stream>>>(p); break;
-    default: step_small_kernel<1024, 16><<<grid, 1024, lds, stream>>>(p); break;
+    case 6432: step_small_kernel<64, 32, REG><<<grid, 64, lds, stream>>>(p); break;
+    case 25608: step_small_kernel<256, 8, REG><<<grid, 256, lds, stream>>>(p); break;
+    case 25616: step_small_kernel<256, 16, REG><<<grid, 256, lds, stream>>>(p); break;
+    case 51216: step_small_kernel<512, 16, REG><<<grid, 512, lds, stream>>>(p); break;
+    default: step_small_kernel<1024, 16, REG><<<grid, 1024, lds, stream>>>(p); break;
     }
+}
+inline void launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    if (h->cfg.num_assets <= 64) launch_small_r<true>(h, p, stream);
+    else launch_small_r<false>(h, p, stream);
 }
 
 // ---------------------------------------------------------------- one launch, one workgroup per env

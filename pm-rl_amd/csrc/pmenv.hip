@@ -566,10 +566,11 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         {(const void*)step_advance_lds_kernel<true>, h->lds_tile},
         {(const void*)step_advance_lds_kernel<false>, h->lds_tile},
         {(const void*)step_surface_kernel, h->lds_surface},
-        {(const void*)step_small_kernel<256, 8>, h->lds_surface},
-        {(const void*)step_small_kernel<256, 16>, h->lds_surface},
-        {(const void*)step_small_kernel<512, 16>, h->lds_surface},
-        {(const void*)step_small_kernel<1024, 16>, h->lds_surface},
+        {(const void*)step_small_kernel<64, 32, false>, h->lds_surface},
+        {(const void*)step_small_kernel<256, 8, false>, h->lds_surface},
+        {(const void*)step_small_kernel<256, 16, false>, h->lds_surface},
+        {(const void*)step_small_kernel<512, 16, false>, h->lds_surface},
+        {(const void*)step_small_kernel<1024, 16, false>, h->lds_surface},
         {(const void*)scalar_step_kernel, h->lds_scalar},
     };
     for (const auto& a : attrs)   // only needed above 64 KiB; failures surface at launch

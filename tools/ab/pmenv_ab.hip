@@ -42,6 +42,7 @@ struct Tools {
     int flat1_pol = 0;          // PMENV_FLAT1_POL: 3 nt loads only, 4 nt stores only, 5 sc0 nt, 6 sc1 nt, 7 nt + sc1 nt
     int fused = 0, fused_vec = 4;   // PMENV_FUSED: advance_rows_kernel<fused> (db | all)
     int stream_block = 512;     // PMENV_STREAM_BLOCK: row-kernel workgroup (128 | 256)
+    bool relay_env = false;     // PMENV_RELAY_ENV: the relay step's env-aligned tiles (step_relay_env_kernel)
     int stream_pol = 0;         // PMENV_STREAM_POL: 0 | 1 (nt) | 2 (sc0 nt)
     int flat_block = 512;       // PMENV_FLAT_BLOCK: the ds_bpermute stream's workgroup
     bool flat_db_wg = true;     // PMENV_FLAT_DB_WG=0: the ds_bpermute double-buffered stream
@@ -347,6 +348,17 @@ void plan(pmenv* h) {
             h->relay_v = v;
         }
     }
+    t->relay_env = knob_int("PMENV_RELAY_ENV", 0) != 0 && h->one_ok && c.num_assets <= 64 && h->one_waves <= 8;
+    if (const char* k = knob("PMENV_SMALL_GEOM")) {   // step_small_kernel's BLOCK x E: 64x32 | 256x8 | 256x16 | ...
+        int bk = 0, e = 0;
+        const int64_t nwf = (int64_t)c.num_assets * c.window * c.features;
+        if (sscanf(k, "%dx%d", &bk, &e) == 2 && (int64_t)bk * e >= nwf &&
+            (bk * 100 + e == 6432 || bk * 100 + e == 25608 || bk * 100 + e == 25616 || bk * 100 + e == 51216 ||
+             bk * 100 + e == 102416)) {
+            h->small_block = bk;
+            h->small_e = e;
+        }
+    }
     t->one_nocap = knob_int("PMENV_ONE_NOCAP", 0) != 0;
     t->flat1_lds_pad = knob_int("PMENV_FLAT1_LDS_PAD", 0);
     t->flat_s80 = knob_int("PMENV_FLAT_S80", 0) != 0;
@@ -554,8 +566,47 @@ static void relay_geom(const pmenv* h, const StepParams& p, const RelayParams& r
     if (out) relay_geom_o<BK, V, true>(h, p, r, q, grid, stream);
     else relay_geom_o<BK, V, false>(h, p, r, q, grid, stream);
 }
+template <int BLOCK, int POL, bool OUT, bool SEQ>
+static void launch_relay_env_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
+                               hipStream_t stream) {
+    const size_t lds = ((size_t)BLOCK * kOneV + 2) * 16;
+    const uint32_t q = h->per4;
+    switch (h->relay_kl * 100 + h->relay_ka) {
+    case 801: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 8, 1, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
+    case 1601: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 16, 1, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
+    case 3200: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 32, 0, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
+    default: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 64, 0, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
+    }
+}
+template <int BLOCK>
+static void launch_relay_env_b(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, bool out,
+                               bool seq, int pol, hipStream_t stream) {
+#define PMENV_RE(POL, OUT, SEQ) launch_relay_env_g<BLOCK, POL, OUT, SEQ>(h, p, r, grid, stream)
+    if (pol == 1) {
+        if (out) { if (seq) PMENV_RE(1, true, true); else PMENV_RE(1, true, false); }
+        else { if (seq) PMENV_RE(1, false, true); else PMENV_RE(1, false, false); }
+    } else {
+        if (out) { if (seq) PMENV_RE(0, true, true); else PMENV_RE(0, true, false); }
+        else { if (seq) PMENV_RE(0, false, true); else PMENV_RE(0, false, false); }
+    }
+#undef PMENV_RE
+}
+
 bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, hipStream_t stream) {
     const int g = h->relay_block * 10 + h->relay_v;
+    const Tools* tt = tools(h);
+    if (tt && tt->relay_env) {     // one tile per env (no halo used; the product primes it anyway)
+        const int block = h->one_waves <= 4 ? 256 : 512;
+        const int epb = (block / 64) * (64 / h->relay_kl);
+        RelayParams re = r;
+        re.scal = (uint32_t)((h->cfg.num_envs + epb - 1) / epb);
+        const unsigned genv = (unsigned)h->cfg.num_envs + re.scal;
+        const bool out = p.obs_out != p.obs;
+        const int pol = out ? h->flat_pol : h->flat_ip_pol;
+        if (block == 256) launch_relay_env_b<256>(h, p, re, genv, out, false, pol, stream);
+        else launch_relay_env_b<512>(h, p, re, genv, out, false, pol, stream);
+        return true;
+    }
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
     switch (g) {

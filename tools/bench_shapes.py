@@ -75,7 +75,8 @@ def main():
             times.append(e0.elapsed_time(e1) * 1e3 / K)
         us = statistics.median(times)
         by = step_bytes(N, W, F) * B
-        path = env.step_path.split(" | ")[1 if ip else 0]
+        parts = env.step_path.split(" | ")         # one name for the non-streaming shapes
+        path = parts[-1] if ip else parts[0]
         out[name] = {"path": path, "us_per_step": us, "env_steps_per_s": B / us * 1e6,
                      "bytes_per_step": by, "achieved_GBps": by / us / 1e3, "frac": by / (us * 1e-6) / PEAK}
         print(name, json.dumps(out[name]), file=sys.stderr, flush=True)
