@@ -1503,7 +1503,20 @@ struct HostIO {
     const float* close_in;   // [B, N] obs[b, n, W-1, close] gathered by the host
     float* chan;             // [B, N, W] channel F-1 out
     double* value_out;       // [B] the value after the step (TradingEnv.value)
+    uint32_t* done;          // [B] completion words: env b's outputs are all in host memory once
+    uint32_t seq;            //     done[b] == seq (written last, system scope)
 };
+
+// the host-I/O kernels' last act: every wave's stores into the mapped staging have completed
+// (vmcnt(0)) before the barrier, then one system-scope release and the env's completion word
+__device__ __forceinline__ void hostio_done(const HostIO& io, int b) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && io.done) {
+        __threadfence_system();
+        __hip_atomic_store(io.done + b, io.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 template <bool HOST>
 __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& io) {
@@ -1521,7 +1534,10 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
         if (HOST && tid == 0) io.value_out[b] = p.value[b];
     }
     __syncthreads();
-    if (HOST ? !io.chan : !p.obs) return;
+    if (HOST ? !io.chan : !p.obs) {
+        if (HOST) hostio_done(io, b);
+        return;
+    }
     const int slot = s.ints[1];
     const int32_t k1 = s.ints[2];                 // updates since reset, after this step
     const int idx = (int)((1 + (int64_t)k1) % W);
@@ -1542,6 +1558,7 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
     for (int n = tid; n < N; n += kBlock)
         p.last_close[(size_t)b * N + n] = HOST ? io.close_in[(size_t)b * N + n]
                                                : obs[((size_t)n * W + (W - 1)) * F + p.close_ch];
+    if (HOST) hostio_done(io, b);
 }
 
 static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
@@ -1574,6 +1591,9 @@ static __global__ __launch_bounds__(kBlock) void reset_kernel(StepParams p, floa
         float* ch = io.chan + (size_t)b * N * W;   // the same channel, dense, for the host to scatter
         for (int i = tid; i < N * W; i += kBlock) ch[i] = i == W - 1 ? 1.0f : 0.0f;
         for (int n = tid; n < N; n += kBlock) p.last_close[(size_t)b * N + n] = io.close_in[(size_t)b * N + n];
+    }
+    if (io.done) {                                 // host I/O: the completion word
+        hostio_done(io, b);
         return;
     }
     if (!obs) return;

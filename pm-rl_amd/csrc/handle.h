@@ -102,10 +102,12 @@ struct pmenv {
                           // capture on, epoch, parity and the copies' validity live in relay_seq
     // host-I/O staging (pmenv_step_host / pmenv_reset_host): one pinned, device-mapped block,
     // allocated on the first host-I/O call — action | prices | last closes | channel [B,N,W] |
-    // weights | reward (f32), then return | value (f64); `hio_dev` is its device address
+    // weights | reward (f32), then return | value (f64), then the completion words (u32);
+    // `hio_dev` is its device address
     char* hio;
     char* hio_dev;
-    size_t hio_off[8];
+    size_t hio_off[9];
+    uint32_t hio_seq;     // the last host-I/O call's completion tag
     int path;             // pmenv_step_path_kind
     void* tools;        // tools build: its knob state (null in the product library)
     char err[512];

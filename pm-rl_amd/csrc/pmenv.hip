@@ -751,8 +751,9 @@ int hio_ensure(pmenv* h) {
     const size_t B = (size_t)h->cfg.num_envs, BN = B * (size_t)h->cfg.num_assets;
     auto up64 = [](size_t x) { return (x + 63) / 64 * 64; };
     size_t o = 0;
-    const size_t sizes[8] = {BN * 4, BN * 4, BN * 4, BN * (size_t)h->cfg.window * 4, BN * 4, B * 4, B * 8, B * 8};
-    for (int i = 0; i < 8; ++i) {
+    const size_t sizes[9] = {BN * 4, BN * 4, BN * 4, BN * (size_t)h->cfg.window * 4, BN * 4, B * 4, B * 8, B * 8,
+                             B * 4};
+    for (int i = 0; i < 9; ++i) {
         h->hio_off[i] = o;
         o = up64(o + sizes[i]);
     }
@@ -773,9 +774,11 @@ int hio_ensure(pmenv* h) {
     }
     h->hio = (char*)p;
     h->hio_dev = (char*)d;
+    memset(h->hio + h->hio_off[8], 0, B * 4);      // completion words: no call yet (tags start at 1)
+    h->hio_seq = 0;
     return PMENV_OK;
 }
-enum { kHioAct, kHioPri, kHioClose, kHioChan, kHioW, kHioRew, kHioRet, kHioVal };
+enum { kHioAct, kHioPri, kHioClose, kHioChan, kHioW, kHioRew, kHioRet, kHioVal, kHioDone };
 template <class T>
 T* hio_host(const pmenv* h, int f) { return reinterpret_cast<T*>(h->hio + h->hio_off[f]); }
 template <class T>
@@ -798,8 +801,28 @@ void hio_scatter_channel(const pmenv* h, float* obs) {
     float* dst = obs + (F - 1);
     for (size_t i = 0; i < BNW; ++i) dst[i * F] = src[i];
 }
+// The call's completion: every env's completion word carries the call's tag once its outputs
+// are in host memory (the kernels write it last, at system scope, after every store of the
+// workgroup has completed). The host spins on the words — they turn a few us after the
+// launch — instead of synchronising the stream: 12.3 / 14.8 us per pmenv_step_host call
+// against 18.2 / 20.1 with hipStreamSynchronize at 1 x 5 x 50 x 5 / 1 x 32 x 32 x 5
+// (profiles/hostio_r05/hostio_r05h*.json). Past ~2 ms (a large batch, or a kernel that
+// failed) it synchronises the stream, which also reports an error.
 int hio_sync(pmenv* h, hipStream_t stream, const char* what) {
     if (const int rc = check_launch(h, what)) return rc;
+    const volatile uint32_t* done = hio_host<volatile uint32_t>(h, kHioDone);
+    const uint32_t seq = h->hio_seq;
+    const int B = h->cfg.num_envs;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 0;; ++it) {
+        int b = 0;
+        while (b < B && done[b] == seq) ++b;
+        if (b == B) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);        // the outputs are read after the words
+            return PMENV_OK;
+        }
+        if ((it & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
     const hipError_t e = hipStreamSynchronize(stream);
     if (e != hipSuccess) {
         set_err(h, "%s: %s", what, hipGetErrorString(e));
@@ -833,6 +856,8 @@ int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* o
     io.close_in = hio_dev<float>(h, kHioClose);
     io.chan = obs ? hio_dev<float>(h, kHioChan) : nullptr;
     io.value_out = hio_dev<double>(h, kHioVal);
+    io.done = hio_dev<uint32_t>(h, kHioDone);
+    io.seq = h->hio_seq = h->hio_seq + 1u == 0u ? 1u : h->hio_seq + 1u;
     step_surface_host_kernel<<<c.num_envs, kBlock, h->lds_surface, stream>>>(p, io);
     if (const int rc = hio_sync(h, stream, "step_surface_host_kernel")) return rc;
     if (obs) hio_scatter_channel(h, obs);
@@ -854,6 +879,8 @@ int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream) {
     io.close_in = hio_dev<float>(h, kHioClose);
     io.chan = obs ? hio_dev<float>(h, kHioChan) : nullptr;
     io.value_out = hio_dev<double>(h, kHioVal);
+    io.done = hio_dev<uint32_t>(h, kHioDone);
+    io.seq = h->hio_seq = h->hio_seq + 1u == 0u ? 1u : h->hio_seq + 1u;
     reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, nullptr, nullptr, io);
     if (const int rc = hio_sync(h, stream, "reset_kernel (host I/O)")) return rc;
     if (obs) hio_scatter_channel(h, obs);

@@ -180,6 +180,8 @@ class TradingEnv:
         self.weights = RingView(self)
         self._obs_shape = (B, N, W, self.cfg.features)
         self._obs_size = torch.Size(self._obs_shape)
+        self._obs_size_unb = torch.Size(self._obs_shape[1:]) if B == 1 else None
+        self._bn = B * N
         self._dev_index = self.device.index
         self._args = _abi.PmenvStepArgs()          # reused: every field is set on every step
         self.track_info = (B == 1) if self._track_info_arg is None else bool(self._track_info_arg)
@@ -424,10 +426,10 @@ class TradingEnv:
         """
         if self._free:
             self._fit(features)
-        unb = self._obs_check(features)
         if not features.is_cuda and bar is None and series is None and out is None and weights_out is None \
                 and prices is not None and self._HOST_DIRECT:
-            return self._step_host(action, features, prices, unb)
+            return self._step_host(action, features, prices)
+        unb = self._obs_check(features)
         if not features.is_cuda:                    # the reference's CPU tensors: staged through the GPU
             if out is not None and out.device.type != "cpu":
                 raise ValueError("out must live where features does")
@@ -454,11 +456,12 @@ class TradingEnv:
 
     def _host_vec(self, x, name):
         """action / prices as a host float32 contiguous tensor of B*N elements."""
-        n = self.cfg.num_envs * self.cfg.num_assets
+        n = self._bn
+        if type(x) is torch.Tensor and x.dtype is torch.float32 and not x.is_cuda and x.numel() == n \
+                and x.is_contiguous():
+            return x                                # the common case: as is (only its data pointer is used)
         if not torch.is_tensor(x):
             x = torch.as_tensor(x)
-        if x.dtype is torch.float32 and not x.is_cuda and x.numel() == n and x.is_contiguous():
-            return x
         if x.numel() != n:
             # weight_buffer.py:18-19 raises ValueError on a mis-shaped action
             raise ValueError(f"{name} must have {self.cfg.num_envs} x {self.cfg.num_assets} elements, "
@@ -481,7 +484,16 @@ class TradingEnv:
         self._rec_i = i + 1
         return i
 
-    def _step_host(self, action, features, prices, unb):
+    def _step_host(self, action, features, prices):
+        shp = features.shape
+        if shp == self._obs_size:
+            unb = False
+        elif shp == self._obs_size_unb:
+            unb = True
+        else:
+            unb = self._obs_check(features)         # raises with the expected shapes
+        if features.dtype is not torch.float32 or not features.is_contiguous():
+            self._obs_check(features)               # raises
         a = self._host_vec(action, "action")
         p = self._host_vec(prices, "prices")
         track = self.track_info and self._info is not None
@@ -492,9 +504,11 @@ class TradingEnv:
                                        rp[3] + i * sz[3] if track else None, self._stream())
         if rc:
             _abi.check(rc, self._h, "pmenv_step_host")
-        rew, ret, val, w = (x[i] for x in self._rec_blk)
-        if unb:
-            rew, ret, val, w = rew[0, ...], ret[0, ...], val[0, ...], w[0]
+        blk = self._rec_blk
+        if unb:                                    # 0-dim / [N] entries, as the reference's .cpu().numpy()
+            rew, ret, val, w = blk[0][i, 0, ...], blk[1][i, 0, ...], blk[2][i, 0, ...], blk[3][i, 0]
+        else:
+            rew, ret, val, w = blk[0][i], blk[1][i], blk[2][i], blk[3][i]
         r = torch.from_numpy(rew)                  # r and info["rewards"][-1] share memory, as :99-100
         v = torch.from_numpy(val)
         self._hval, self._hval_ver = v, _version(self._state)

@@ -105,6 +105,26 @@ def main():
             res["oracle_b1"] = {"us_per_step_median": statistics.median(times), "threads": 1}
         except ImportError as e:
             res["oracle_b1"] = {"error": str(e)}
+        # the C ABI alone: pmenv_step_host on prebuilt host pointers (ctypes call included)
+        import ctypes
+        env = TradingEnv()
+        env.reset(datas[0])
+        lib, h = env._lib, env._h
+        rew, val = np.empty(1, np.float32), np.empty(1, np.float64)
+        ptrs = [(acts[t].data_ptr(), prices[t].data_ptr(), datas[t].data_ptr()) for t in range(T + 1)]
+        rp, vp = rew.ctypes.data, val.ctypes.data
+        sp = env._stream()
+        fn = lib.pmenv_step_host
+        times = []
+        for rep in range(REPS):
+            t0 = time.perf_counter()
+            for step in range(1, T + 1):
+                a, p_, d = ptrs[step]
+                if fn(h, a, p_, d, rp, vp, None, None, sp):
+                    raise RuntimeError("pmenv_step_host failed")
+            times.append((time.perf_counter() - t0) / T * 1e6)
+        res["c_abi_us_per_step"] = statistics.median(times)
+        env.close()
         # one direct step, timed alone (reset, 50 steps warm, then per call)
         env = TradingEnv()
         env.reset(datas[0])
