@@ -1238,6 +1238,16 @@ int pmenv_batch_reward_forward(const float* a, const float* v_prev, const float*
     if (pmenv_tools::batch_reward_forward(a, v_prev, p, B, N, reward_kind, norm, scale, work, reward_out, ret_out,
                                           stream, &rc))
         return rc;
+    // at most 64 rows (the agents' BATCH_SIZE, config/pg.py:7): one workgroup, one launch
+    if (B <= kQuadRows && N <= kQuadMaxN) {
+        if (N <= 32)
+            batch_reward_small_kernel<8><<<1, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, scale,
+                                                                         work, reward_out, ret_out);
+        else
+            batch_reward_small_kernel<16><<<1, kTrainBlock, 0, stream>>>(a, v_prev, p, B, N, reward_kind, norm, scale,
+                                                                          work, reward_out, ret_out);
+        return hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+    }
     // two launches: the row blocks' partials, then the final fold (a one-launch form with a
     // last-block ticket measured slower at every shape: DESIGN.md §7 f2)
     int nparts;

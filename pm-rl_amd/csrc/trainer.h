@@ -273,7 +273,7 @@ __device__ __forceinline__ RowQuad<EPL> load_row_quad(const float* a, const floa
 template <int EPL, bool COH = false>
 __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v_prev, const float* p, int B, int N,
                                                   int kind, int norm, double* work, double (*rec_w)[kPartStride],
-                                                  int blk, int nblk) {
+                                                  int blk, int nblk, double* rec_dst = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid & 3;
     const int r0 = blk * kQuadRows;
     const int nrows = min(kQuadRows, B - r0);
@@ -343,7 +343,7 @@ __device__ __forceinline__ void rows_quad_partial(const float* a, const float* v
     double acc[kPartStride];
     for (int i = 0; i < kPartStride; ++i) acc[i] = rec_w[0][i];
     for (int w = 1; w < 4; ++w) fold_record(kind, norm, acc, rec_w[w]);
-    double* part = work + (size_t)6 * B + 8 + blk;        // field-major: coalesced final fold
+    double* part = rec_dst ? rec_dst + blk : work + (size_t)6 * B + 8 + blk;   // field-major: coalesced final fold
     for (int i = 0; i < kPartStride; ++i) {
         if (COH) __hip_atomic_store(part + (size_t)i * nblk, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else part[(size_t)i * nblk] = acc[i];
@@ -436,11 +436,11 @@ __global__ __launch_bounds__(kTrainBlock) void batch_reward_grad_quad_kernel(con
 // order, then a fixed-shape LDS tree folds the 256 threads: deterministic.
 template <bool COH = false>
 __device__ __forceinline__ void final_fold(int B, int kind, int norm, double scale, double* work, float* reward_out,
-                                           int nparts) {
+                                           int nparts, const double* parts_src = nullptr, int* glob_out = nullptr) {
     __shared__ double sh[4][kPartStride];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t nblk = (size_t)nparts;
-    const double* parts = work + (size_t)6 * B + 8;
+    const double* parts = parts_src ? parts_src : work + (size_t)6 * B + 8;
     double acc[kPartStride];
     acc[0] = 0.0; acc[1] = INFINITY; acc[2] = 0.0;
     for (int c = 0; c < 3; ++c) { acc[3 + 4 * c] = 0.0; acc[4 + 4 * c] = 0.0; acc[5 + 4 * c] = 0.0; acc[6 + 4 * c] = 0.0; }
@@ -501,6 +501,7 @@ __device__ __forceinline__ void final_fold(int B, int kind, int norm, double sca
     work[6 * (size_t)B + 3] = R;
     work[6 * (size_t)B + 4] = (double)norm;
     *reward_out = (float)R;
+    if (glob_out) *glob_out = glob ? 1 : 0;
 }
 
 // the second launch of the forward: one workgroup folds the row blocks' partials
@@ -510,6 +511,36 @@ static __global__ __launch_bounds__(kTrainBlock) void batch_reward_final_kernel(
     final_fold(B, kind, norm, scale, work, reward_out, nparts);
 }
 
+
+// The whole forward in ONE workgroup for a batch of at most 64 rows (N <= 64) — the PG / A2C
+// agents' own BATCH_SIZE = 64 (config/pg.py:7), where the two-launch forward is two kernel
+// latencies for a few KiB of work: the row block's partial record goes to LDS, the same
+// final_fold reads it from there (one record: the same folds, the same bits), and with
+// `ret_out` the rows' choice is made here too (no select launch).
+template <int EPL>
+__global__ __launch_bounds__(kTrainBlock) void batch_reward_small_kernel(const float* a, const float* v_prev,
+                                                                         const float* p, int B, int N, int kind,
+                                                                         int norm, double scale, double* work,
+                                                                         float* reward_out, float* ret_out) {
+    __shared__ double rec_w[4][kPartStride];
+    __shared__ double rec[kPartStride];
+    __shared__ int glob;
+    rows_quad_partial<EPL>(a, v_prev, p, B, N, kind, norm, work, rec_w, 0, 1, rec);
+    __syncthreads();
+    final_fold(B, kind, norm, scale, work, reward_out, 1, rec, &glob);
+    if (!ret_out) return;
+    __syncthreads();
+    const int b = threadIdx.x;                       // batch_reward_select_kernel's row, B <= 64
+    if (b >= B) return;
+    bool nb;
+    if (norm == PMENV_BNORM_GLOBAL_OR) nb = glob != 0;
+    else if (norm == PMENV_BNORM_ROW_OR) nb = row_normalises(work[(size_t)B + b], work[2 * (size_t)B + b]);
+    else nb = false;
+    const double r = nb ? work[4 * (size_t)B + b] : work[3 * (size_t)B + b];
+    work[b] = r;
+    work[5 * (size_t)B + b] = nb ? 1.0 : 0.0;
+    ret_out[b] = (float)r;
+}
 
 // elementwise: each row's chosen return and normalisation flag (for the backward)
 static __global__ __launch_bounds__(256) void batch_reward_select_kernel(int B, int norm, double* work, float* ret_out) {

@@ -46,7 +46,8 @@ def test_gpu_batch_reward_matches_reference_autograd():
                                        err_msg=f"{key} {tag}")
 
 
-@pytest.mark.parametrize("B,N", [(65536, 30), (4096, 500), (7, 64), (5, 65), (33, 129), (17, 256), (3, 700), (1, 3)])
+@pytest.mark.parametrize("B,N", [(65536, 30), (4096, 500), (7, 64), (5, 65), (33, 129), (17, 256), (3, 700), (1, 3),
+                                 (64, 30), (64, 8), (65, 30)])   # B <= 64, N <= 64: the one-workgroup forward
 @pytest.mark.parametrize("kind", ["log_returns", "returns", "sharpe_ratio"])
 @pytest.mark.parametrize("norm", ["global_or", "row_or", "none"])
 def test_gpu_batch_reward_vs_oracle(B, N, kind, norm):

@@ -164,10 +164,58 @@ def gae_ab(libs):
     return out
 
 
+def f2_ab(libs):
+    """The trainer op at the agents' batch sizes (config/pg.py:7 BATCH_SIZE = 64): forward +
+    backward per call (round 5: one workgroup, one launch for B <= 64; round 4: rows + fold)."""
+    out = {}
+    P = ctypes.c_void_p
+    for (B, N, kind) in ((64, 30, 0), (64, 8, 0), (32, 30, 2), (64, 64, 0), (128, 30, 0)):
+        g = torch.Generator(DEV).manual_seed(B * 100 + N)
+        a = torch.randn(B, N, device=DEV, generator=g)
+        v = torch.rand(B, device=DEV, generator=g) + 0.5
+        pr = torch.rand(B, N, device=DEV, generator=g) * 0.1 + 0.95
+        rew = torch.empty(1, device=DEV)
+        ret = torch.empty(B, device=DEV)
+        go = torch.ones(1, device=DEV)
+        ga = torch.empty(B, N, device=DEV)
+        calls, outs = {}, {}
+        for n, lib in libs.items():
+            work = torch.empty(lib.pmenv_batch_reward_workspace(B) // 8, dtype=torch.float64, device=DEV)
+
+            def call(lib=lib, work=work):
+                assert lib.pmenv_batch_reward_forward(P(a.data_ptr()), P(v.data_ptr()), P(pr.data_ptr()), B, N, kind, 0,
+                                                      1.0, P(work.data_ptr()), P(rew.data_ptr()), P(ret.data_ptr()),
+                                                      stream()) == 0
+                assert lib.pmenv_batch_reward_backward(P(a.data_ptr()), P(v.data_ptr()), P(pr.data_ptr()), B, N, kind,
+                                                       1.0, P(work.data_ptr()), P(go.data_ptr()), P(ga.data_ptr()),
+                                                       stream()) == 0
+            calls[n] = call
+        times = {n: [] for n in calls}
+        for n, f in calls.items():
+            for _ in range(20):
+                f()
+        for _ in range(R):
+            for n, f in calls.items():
+                times[n].append(timed(f, K))
+        for n, f in calls.items():
+            f()
+            torch.cuda.synchronize()
+            outs[n] = (rew.clone(), ret.clone(), ga.clone())
+        key = f"{B}x{N}_{['log', 'ret', 'sharpe'][kind]}"
+        out[key] = {n: statistics.median(t) for n, t in times.items()}
+        out[key]["bitwise_equal"] = all(torch.equal(x, y) for x, y in zip(outs["r05"], outs["r04"]))
+        print(key, json.dumps(out[key]), file=sys.stderr, flush=True)
+    return out
+
+
 def main():
     torch.cuda.set_device(DEV)
     libs = {n: load(p) for n, p in LIBS.items()}
-    res = {"K": K, "R": R, "relay": relay_ab(libs), "gae": gae_ab(libs), "graph": relay_graph(libs["r05"])}
+    if os.environ.get("AB_ONLY") == "f2":
+        print(json.dumps({"K": K, "R": R, "f2": f2_ab(libs)}))
+        return
+    res = {"K": K, "R": R, "relay": relay_ab(libs), "gae": gae_ab(libs), "graph": relay_graph(libs["r05"]),
+           "f2": f2_ab(libs)}
     print(json.dumps(res))
 
 
