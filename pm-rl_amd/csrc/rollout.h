@@ -253,7 +253,9 @@ __global__ __launch_bounds__(64) void gae_stream_kernel(const float* r, const fl
 // a later chunk's flag computes that chunk's map itself, from the inputs, with the producer's
 // own code and association order (lb_wave_map folded as the publisher folds), so the bits are
 // the producer's and the wait always ends — whatever order the hardware dispatches workgroups
-// in (with the usual later-chunks-first dispatch the fallback never runs).
+// in (with the usual later-chunks-first dispatch the fallback never runs; the tools build's
+// SPIN = 0 form takes it on the first poll that finds a flag missing, and gives the product's
+// bits: tools/ab_gae_fallback.py).
 constexpr int kLbSpin = 4096;
 
 template <int U>
@@ -298,7 +300,7 @@ __device__ __forceinline__ void lb_fold(double Cj, double Dj, double& Ca, double
     Ca = Cj * Ca;
 }
 
-template <int NW, int U>
+template <int NW, int U, int SPIN = kLbSpin>
 __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, const float* v, const uint8_t* dones,
                                                               float* adv, float* ret, int T, int B, float gamma,
                                                               float lam, int nC, double* maps, uint64_t* flags,
@@ -357,7 +359,7 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback_kernel(const float* r, c
             bool ready = j >= j1 || __hip_atomic_load(flags + (size_t)j * nEB + eb, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT) == epoch;
             for (int spin = 0; !__all(ready); ++spin) {
-                if (spin >= kLbSpin) {
+                if (spin >= SPIN) {
                     // the producers of the chunks still missing may not be running: compute
                     // their maps here (all 64 lanes, one chunk at a time), as they would
                     uint64_t miss = __ballot(!ready);

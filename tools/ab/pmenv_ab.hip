@@ -681,6 +681,26 @@ bool gae(const float* rewards, const float* values, const uint8_t* dones, float*
         *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
         return true;
     }
+    if (k && !strcmp(k, "lbfb")) {   // the product's look-back, its fallback taken on the first missing flag (SPIN = 0)
+        const int seg = (int64_t)((T + 127) / 128) * ((B + 63) / 64) >= 128 ? 128 : 64;
+        const int n = (T + seg - 1) / seg, neb = (B + 63) / 64;
+        static double* ws = nullptr;
+        static size_t ws_n = 0;
+        const size_t need = (size_t)2 * n * B + (size_t)n * neb;
+        if (need > ws_n) {
+            if (ws) (void)hipFree(ws);
+            if (hipMalloc(&ws, need * 8) != hipSuccess) { *rc = PMENV_ERR_HIP; return true; }
+            ws_n = need;
+        }
+        static uint64_t epoch = 0x7a13ull << 48;
+        ++epoch;
+        uint64_t* flags = reinterpret_cast<uint64_t*>(ws + (size_t)2 * n * B);
+        const unsigned g = (unsigned)(n * neb);
+        if (seg == 128) gae_lookback_kernel<8, 16, 0><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        else gae_lookback_kernel<8, 8, 0><<<g, 512, 0, stream>>>(rewards, values, dones, adv, ret, T, B, gamma, lam, n, ws, flags, epoch);
+        *rc = hipGetLastError() == hipSuccess ? PMENV_OK : PMENV_ERR_HIP;
+        return true;
+    }
     if (k && (!strcmp(k, "lb2") || !strcmp(k, "lb2x16"))) {   // two chunks per workgroup (64- / 128-day chunks)
         const int u = !strcmp(k, "lb2x16") ? 16 : 8;
         const int seg = 8 * u, n = (T + seg - 1) / seg, neb = (B + 63) / 64;
