@@ -102,6 +102,11 @@ __device__ __forceinline__ const float* env_bar(const StepParams& p, int b) {
     return (d >= 0 && d < p.series_days) ? p.bar + (size_t)d * row : nullptr;
 }
 
+// the ring slot (1 + k) % W of weight_buffer.py:32-44 for the step counter k >= 0 (it starts
+// at 0 on reset and only counts up): 32-bit unsigned arithmetic, the 64-bit remainder's
+// ~100 instructions were on the register step's critical path
+__device__ __forceinline__ int ring_slot(int32_t k, int W) { return (int)(((uint32_t)k + 1u) % (uint32_t)W); }
+
 // branch-free float select (bit masks: keeps element loops free of control flow)
 __device__ __forceinline__ float pick(bool c, float a, float b) {
     const int m = -(int)c;
@@ -126,6 +131,11 @@ __device__ __forceinline__ f4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 }
 __device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ double buf_load_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+    const u2v v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return __hiloint2double((int)v.y, (int)v.x);
 }
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store4(__amdgpu_buffer_rsrc_t r, uint32_t off, f4 v) {

@@ -159,12 +159,12 @@ __device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scrat
     const double value = wave_sum(part);
 
     // :83-84 w' = portfolio / value ; ring.update(w') at slot idx = (1 + k) % W
-    const int slot = (int)((1 + (int64_t)k) % W);
-    float* ring_slot = p.ring + (size_t)b * W * N + (size_t)slot * N;
+    const int slot = ring_slot(k, W);
+    float* ring_row = p.ring + (size_t)b * W * N + (size_t)slot * N;
     for (int n = lane; n < N; n += 64) {
         float w = (float)(s.wv[n] / value);
         s.wp[n] = w;
-        ring_slot[n] = w;
+        ring_row[n] = w;
         p.w_new[(size_t)b * N + n] = w;
         if (p.weights) p.weights[(size_t)b * N + n] = w;
     }
@@ -310,8 +310,13 @@ struct ScalarIn {
 // K1 form: L lanes per env, every load unconditional from a clamped (always
 // valid) address and masked afterwards, so several envs' loads can be in flight
 // together without control-flow joins between them
-template <int L>
-__device__ __forceinline__ ScalarIn scalar_load(const StepParams& p, int b, int lane) {
+//
+// LV (the register step, one env per workgroup): the env's counter, value and statistics are
+// read as lane values at a lane-varying zero offset `zoff` — a load the compiler sees as
+// uniform gets its value moved to an SGPR right after issue, and the wait for that would hold
+// every load issued after it back by a memory round trip
+template <int L, bool LV = false>
+__device__ __forceinline__ ScalarIn scalar_load(const StepParams& p, int b, int lane, uint32_t zoff = 0u) {
     const int n = lane % L;
     const int N = p.N, Fm = p.F - 1;
     const bool env_ok = b < p.B;
@@ -320,10 +325,17 @@ __device__ __forceinline__ ScalarIn scalar_load(const StepParams& p, int b, int 
     const int nc = act ? n : 0;
     const size_t i = (size_t)bc * N + nc;
     ScalarIn in;
-    in.k = p.k[bc];
-    in.v_prev = p.value[bc];
-    in.sa = p.sa[bc];
-    in.sb = p.sb[bc];
+    if constexpr (LV) {
+        in.k = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.k + bc, 4u), zoff, 0, 0);
+        in.v_prev = buf_load_f64(make_rsrc(p.value + bc, 8u), zoff);
+        in.sa = buf_load_f64(make_rsrc(p.sa + bc, 8u), zoff);
+        in.sb = buf_load_f64(make_rsrc(p.sb + bc, 8u), zoff);
+    } else {
+        in.k = p.k[bc];
+        in.v_prev = p.value[bc];
+        in.sa = p.sa[bc];
+        in.sb = p.sb[bc];
+    }
     const float a = p.action[i];
     const float wl = p.w_new[i];                                       // get_last() (weight_buffer.py:28-30)
     const float* barb = p.bar ? env_bar(p, bc) : nullptr;
@@ -491,7 +503,7 @@ __device__ __forceinline__ void scalar_tail(const StepParams& p, int b, int lane
     const int32_t k = m.k;
     const double value = m.value, V = m.V;
     // :83-84 ring.update(w') at slot idx = (1 + k) % W
-    const int slot = (int)((1 + (int64_t)k) % W);
+    const int slot = ring_slot(k, W);
     const bool wr = !SNAP || owner;
     if (act && wr) {
         const float wp = m.wp;
@@ -726,7 +738,7 @@ __global__ __launch_bounds__(BLOCK) void advance_rows_kernel(StepParams p) {
     }
 
     const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= W - 1);
-    const int slotF = (int)((1 + (int64_t)k) % W) * F;
+    const int slotF = ring_slot(k, W) * F;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const uint32_t q = (uint32_t)(tid + i * BLOCK);
@@ -1298,6 +1310,102 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
     }
 }
 
+// ---------------------------------------------------------------- K2 for F != 5: the generic stream
+// The two-launch step's window stream for the channel counts the F = 5 streams do not take
+// (2 <= F <= 8, F != 5; 16-B granular env windows): flat_wg_body_patch's workgroup layout —
+// BLOCK x V chunks of the flat [B, N, W, F] tensor staged in LDS, the two chunks past the
+// workgroup read from `halo` in place (copied by the scalar step of the same step) or from
+// obs double-buffered — with the shift by F floats read from LDS dword-wise and every
+// element composed from its own (day, channel) (weight_buffer.py:32-44, instrument.py:339-356):
+//   market f < F-1:  t < W-1 ? in[n, t+1, f] : bar[n, f]
+//   weight f = F-1:  shift order ? (t < W-1 ? in[n, t+1, F-1] : w'[n])
+//                                : (t == slot ? w'[n] : in[n, t, F-1])
+// The workgroup's rows' bar (F - 1 floats, NaN for a day outside the series), w' and
+// counter come into LDS before the barrier, one row per thread (at most BLOCK rows per
+// workgroup: the plan's rule 4 V BLOCK / (W F) + 2 <= BLOCK). An env window is a whole
+// number of chunks, so a chunk spans at most two rows of one env.
+template <int BLOCK, int V, bool OUT>
+__global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot) {
+    constexpr int CPW = BLOCK * V;
+    constexpr int kFm = 7;                                   // bar floats per staged row (F <= 8)
+    __shared__ f4 sh4[CPW + 2];
+    __shared__ float sh_bar[BLOCK * kFm];
+    __shared__ float sh_wp[BLOCK];
+    __shared__ int32_t sh_kc[BLOCK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = blockIdx.x * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    f4 own[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<0>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : p.halo + (size_t)blockIdx.x * 8;
+    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    __builtin_amdgcn_sched_barrier(0);
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1, WF = W * F;
+    const uint32_t per4 = (uint32_t)(N * WF) >> 2;
+    const uint32_t b_lo = fdiv(c0, p.div_units);
+    const uint32_t g_lo = b_lo * (uint32_t)N + fdiv(4u * (c0 - b_lo * per4), p.div_wf);
+    const uint32_t ql = c0 + nblk - 1u;
+    const uint32_t b_hi = fdiv(ql, p.div_units);
+    const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
+    if ((uint32_t)tid <= g_hi - g_lo) {
+        const uint32_t g = g_lo + (uint32_t)tid;
+        const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
+        const float* barb = env_bar(p, (int)b);                     // null: a day outside the series
+        const auto rb = make_rsrc(barb ? barb + (size_t)n * Fm : p.obs, barb ? (uint32_t)Fm * 4u : 0u);
+#pragma unroll
+        for (int f = 0; f < kFm; ++f) {
+            const float x = buf_load1(rb, f < Fm ? (uint32_t)f * 4u : 0x80000000u);
+            sh_bar[tid * kFm + f] = barb ? x : __int_as_float(0x7fc00000);
+        }
+        sh_wp[tid] = p.w_new[g];
+        sh_kc[tid] = p.k[b] - 1;                                     // the scalar step counted this step
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
+    if (tid < 2) sh4[CPW + tid] = hal;
+    __syncthreads();
+    const float* shf = reinterpret_cast<const float*>(sh4);
+    const bool storage = p.ring_mode == PMENV_RING_STORAGE;
+    const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
+        const uint32_t b = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - b * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const uint32_t kk = j0 - row * (uint32_t)WF;
+        int t = (int)fdiv(kk, p.div_f);
+        int f = (int)kk - t * F;
+        int r = (int)(b * (uint32_t)N + row - g_lo);                 // the element's row in the workgroup
+        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int32_t kc = sh_kc[r];
+            const float wp = sh_wp[r];
+            const float bf = sh_bar[r * kFm + min(f, kFm - 1)];
+            const float sh = shf[4 * j + e + F];
+            const bool last = t == W - 1;
+            const bool shift_w = !(storage && kc >= W - 1);
+            const int slot = (int)((uint32_t)(1 + kc) - fdiv((uint32_t)(1 + kc), p.div_w) * (uint32_t)W);
+            const float wv = shift_w ? (last ? wp : sh) : (t == slot ? wp : un[e]);
+            o[e] = f == Fm ? wv : (last ? bf : sh);
+            // the next element: channel, day, row
+            const bool fw = f == Fm;
+            f = fw ? 0 : f + 1;
+            t += fw ? 1 : 0;
+            const bool tw = t == W;
+            t = tw ? 0 : t;
+            r += tw ? 1 : 0;
+        }
+        buf_store4<0>(rd, (uint32_t)j * 16u, f4{o[0], o[1], o[2], o[3]});
+    }
+}
+
 // ---------------------------------------------------------------- single-launch fallback
 // The whole step in one workgroup per env with the obs staged through an LDS tile
 // (rows of any length up to kTileFloats, any F >= 2, any alignment).
@@ -1409,17 +1517,40 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     const float* barg = env_bar(p, b);                    // null: a day outside the series (NaN bar)
     const auto rs_bar = make_rsrc(barg ? barg : p.obs, barg ? (uint32_t)(N * Fm) * 4u : 0u);
     const float nanv = __int_as_float(0x7fc00000);
-    const int32_t k0 = p.k[b];                            // scalar load, in flight with the market loads
+    // the step counter as a lane value, read at a lane-varying zero offset: a load the compiler
+    // sees as uniform has its value moved to an SGPR right after it is issued, and the wait for
+    // that held every load below back by one memory round trip
+    uint32_t z = 0u;
+    asm volatile("" : "+v"(z));
     ScalarIn sin;
-    if (REG && tid < 64) sin = scalar_load<64>(p, b, tid);   // N <= 64: the register form, one asset per lane
+    int32_t k0;
+    if constexpr (REG) {
+        sin = scalar_load<64, true>(p, b, tid, z);        // every wave (lane % 64 = asset): no branch before the window loads
+        k0 = sin.k;
+    } else {
+        k0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.k + b, 4u), z, 0, 0);
+    }
+    // thread i owns floats j = i + BLOCK e; small E keeps their (row, day, channel) in registers
+    // for the stores, large E recomputes them (fewer live registers)
+    constexpr bool BOTH = E <= 8;
+    uint32_t xr[BOTH ? E : 1], xt[BOTH ? E : 1], xf[BOTH ? E : 1];
+    auto decomp = [&](uint32_t j, uint32_t& row, uint32_t& t, uint32_t& f) {
+        row = fdiv(j, p.div_wf);
+        const uint32_t kk = j - row * WF;
+        t = fdiv(kk, p.div_f);
+        f = kk - t * (uint32_t)F;
+    };
     float src[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {                         // the market channels: in[j + F] or the bar
         const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
-        const uint32_t row = fdiv(j, p.div_wf);
-        const uint32_t kk = j - row * WF;
-        const uint32_t t = fdiv(kk, p.div_f);
-        const uint32_t f = kk - t * (uint32_t)F;
+        uint32_t row, t, f;
+        decomp(j, row, t, f);
+        if constexpr (BOTH) {
+            xr[e] = row;
+            xt[e] = t;
+            xf[e] = f;
+        }
         const bool mkt = j < NWF && (int)f < Fm, last = (int)t == W - 1;
         const float sh = buf_load1(rs_in, mkt && !last ? (j + (uint32_t)F) * 4u : kOut);
         const float bv = buf_load1(rs_bar, mkt && last ? (row * (uint32_t)Fm + f) * 4u : kOut);
@@ -1429,24 +1560,23 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     // in place (weight_buffer.py:32-44). Small E: both candidates are read at once (no wait for
     // the counter, one memory round trip); large E: the counter picks the one float to read
     // (half the registers, the weight loads a round trip later)
-    constexpr bool BOTH = E <= 8;
     float cur[BOTH ? E : 1];
     const bool shift_w = p.ring_mode == PMENV_RING_CHRONO || k0 < W - 1;
     uint32_t tid2 = (uint32_t)tid;
     asm volatile("" : "+v"(tid2));                        // recompute the indices, do not keep E of them live
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const uint32_t j = tid2 + (uint32_t)(BLOCK * e);
-        const uint32_t row = fdiv(j, p.div_wf);
-        const uint32_t kk = j - row * WF;
-        const uint32_t t = fdiv(kk, p.div_f);
-        const uint32_t f = kk - t * (uint32_t)F;
-        const bool wch = j < NWF && (int)f == Fm;
         if constexpr (BOTH) {
-            const float ws = buf_load1(rs_in, wch && (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut);
+            const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+            const bool wch = j < NWF && (int)xf[e] == Fm;
+            const float ws = buf_load1(rs_in, wch && (int)xt[e] < W - 1 ? (j + (uint32_t)F) * 4u : kOut);
             cur[e] = buf_load1(rs_in, wch ? j * 4u : kOut);
             src[e] = wch ? ws : src[e];
         } else {
+            const uint32_t j = tid2 + (uint32_t)(BLOCK * e);
+            uint32_t row, t, f;
+            decomp(j, row, t, f);
+            const bool wch = j < NWF && (int)f == Fm;
             const uint32_t off = !wch ? kOut : !shift_w ? j * 4u : (int)t < W - 1 ? (j + (uint32_t)F) * 4u : kOut;
             const float wv = buf_load1(rs_in, off);
             src[e] = wch ? wv : src[e];
@@ -1465,24 +1595,29 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's window reads are in
     __syncthreads();
-    const int slot = (int)((1 + (int64_t)k0) % W);
+    const int slot = ring_slot(k0, W);
     const float* wps = REG ? sh_wp : s.wp;
     uint32_t tid3 = (uint32_t)tid;
     asm volatile("" : "+v"(tid3));
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const uint32_t j = tid3 + (uint32_t)(BLOCK * e);
-        const uint32_t row = fdiv(j, p.div_wf);
-        const uint32_t kk = j - row * WF;
-        const uint32_t t = fdiv(kk, p.div_f);
-        const uint32_t f = kk - t * (uint32_t)F;
-        float v = src[e];
-        if ((int)f == Fm && j < NWF) {
-            const float wp = wps[row];
-            if constexpr (BOTH) v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : cur[e]);
-            else v = shift_w ? ((int)t == W - 1 ? wp : v) : ((int)t == slot ? wp : v);
+        uint32_t j, row, t, f;
+        if constexpr (BOTH) {
+            j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+            row = xr[e];
+            t = xt[e];
+            f = xf[e];
+        } else {
+            j = tid3 + (uint32_t)(BLOCK * e);
+            decomp(j, row, t, f);
         }
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
+        // branch-free: every lane reads a w' (its row clamped), the selects pick
+        const float v = src[e];
+        const float wp = wps[min(row, (uint32_t)N - 1u)];
+        const float kept = BOTH ? cur[e] : v;
+        const float wv = pick(shift_w, pick((int)t == W - 1, wp, v), pick((int)t == slot, wp, kept));
+        const float o = pick((int)f == Fm && j < NWF, wv, v);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
     }
     // the state writes and the reward after the window's stores (the barrier waited for the core only)
     if (REG && tid < 64) scalar_tail<64>(p, b, tid, sin, mid);
@@ -1540,7 +1675,7 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
     }
     const int slot = s.ints[1];
     const int32_t k1 = s.ints[2];                 // updates since reset, after this step
-    const int idx = (int)((1 + (int64_t)k1) % W);
+    const int idx = ring_slot(k1, W);
     const bool full = (int64_t)k1 >= W - 1;
     const float* ringb = p.ring + (size_t)b * W * N;
     float* obs = HOST ? io.chan + (size_t)b * N * W : p.obs + (size_t)b * N * W * F;

@@ -51,6 +51,13 @@ struct pmenv {
     uint32_t halo_wgs, flat_qtot;
     int scalar_scratch_floats;
     size_t lds_scalar;
+    // two-launch path for F != 5 (2 <= F <= 8, 16-B granular env windows): the scalar step,
+    // then the generic stream (advance_gen_kernel<gen_block, gen_v>)
+    bool gen_ok;          // the shape fits the generic stream
+    int gen_auto;         // PMENV_FUSE_* bits the automatic choice gives it
+    int gen;              // PMENV_FUSE_* bits: which windows take it now
+    int gen_block, gen_v; // threads per workgroup, chunks per thread
+    uint32_t gen_qtot;    // chunks of the whole [B, N, W, F] window
     int k1_vec;           // scalar_step_vec_kernel shape 100 * L + A (+ kK1Str), 0: register / LDS form
     // one launch per step, one workgroup per env (step_env_kernel)
     bool one_ok;          // the shape fits step_env_kernel
@@ -253,6 +260,7 @@ void release(pmenv* h);
 bool launch_scalar(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_advance(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_one(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
+bool launch_small(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_fused(const pmenv* h, const pmenv_dev::StepParams& p, int fuse_bit, uint32_t phases, hipStream_t stream);
 bool launch_relay(const pmenv* h, const pmenv_dev::StepParams& p, const pmenv_dev::RelayParams& r, unsigned grid,
                   hipStream_t stream);

@@ -105,9 +105,30 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
         p.halo_wgs = h->halo_wgs;
         p.halo_block = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
         p.halo_qtot = h->flat_qtot;
+    } else if (p.obs_out == p.obs && (h->gen & PMENV_FUSE_INPLACE)) {   // the generic stream's halo
+        p.halo = h->halo;
+        p.halo_wgs = h->halo_wgs;
+        p.halo_block = (uint32_t)(h->gen_block * h->gen_v);
+        p.halo_qtot = h->gen_qtot;
     }
     if (pmenv_tools::launch_scalar(h, p, stream)) return;
     launch_scalar_kernels(h, p, stream);
+}
+
+// ---------------------------------------------------------------- the generic stream (F != 5)
+template <int BLOCK, int V>
+inline void launch_gen_g(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
+    if (p.obs_out == p.obs) advance_gen_kernel<BLOCK, V, false><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+    else advance_gen_kernel<BLOCK, V, true><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+}
+inline void launch_gen(const pmenv* h, StepParams p, hipStream_t stream) {
+    p.div_units = make_fastdiv(h->per4);
+    switch (h->gen_block * 10 + h->gen_v) {
+    case 2562: launch_gen_g<256, 2>(h, p, stream); break;
+    case 5122: launch_gen_g<512, 2>(h, p, stream); break;
+    default: launch_gen_g<256, 4>(h, p, stream); break;
+    }
 }
 
 // ---------------------------------------------------------------- the register step (any F)
@@ -124,6 +145,7 @@ inline void launch_small_r(const pmenv* h, const StepParams& p, hipStream_t stre
     }
 }
 inline void launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    if (pmenv_tools::launch_small(h, p, stream)) return;
     if (h->cfg.num_assets <= 64) launch_small_r<true>(h, p, stream);
     else launch_small_r<false>(h, p, stream);
 }

@@ -169,7 +169,7 @@ int relay_alloc(pmenv* h) {
 // which windows take the one-launch steps under `path`
 int one_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_ONE_LAUNCH) return h->one_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
-    if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming ? 0 : -1;
+    if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->streaming || h->gen_ok ? 0 : -1;
     if (path == PMENV_STEP_PATH_FLAT) return h->flat1_ok ? 0 : -1;
     if (path == PMENV_STEP_PATH_RELAY) return h->relay_ok ? 0 : -1;
     return h->one_auto;
@@ -177,6 +177,11 @@ int one_bits(const pmenv* h, int path) {
 int relay_bits(const pmenv* h, int path) {
     if (path == PMENV_STEP_PATH_RELAY) return h->relay_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : -1;
     if (path == PMENV_STEP_PATH_AUTO) return h->relay_auto;
+    return 0;
+}
+int gen_bits(const pmenv* h, int path) {
+    if (path == PMENV_STEP_PATH_TWO_LAUNCH) return h->gen_ok ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
+    if (path == PMENV_STEP_PATH_AUTO) return h->gen_auto;
     return 0;
 }
 int flat1_bits(const pmenv* h, int path) {
@@ -461,6 +466,20 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->one_auto &= ~h->relay_auto;
         h->flat1_auto &= ~h->relay_auto;
     }
+    // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 8 (its halo is the two
+    // chunks past a workgroup), 16-B granular env windows, at most BLOCK rows per workgroup.
+    // AUTO gives it the windows above 32 MiB; below, the register step's one launch per step
+    // (one workgroup per env) wins
+    {
+        const int F = c.features;
+        h->gen_block = 256;
+        h->gen_v = 4;
+        const int64_t cpw = (int64_t)h->gen_block * h->gen_v;
+        h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
+                    (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= h->gen_block;
+        h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
+        h->gen_auto = h->gen_ok && win > (32ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
+    }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {
         h->units_per_env = (c.num_assets + h->unit_rows - 1) / h->unit_rows;
@@ -470,6 +489,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     h->one = h->one_auto;
     h->flat1 = h->flat1_auto;
     h->relay = h->relay_ok ? h->relay_auto : 0;
+    h->gen = h->gen_ok ? h->gen_auto : 0;
 
     h->scalar_scratch_floats = (int)((scratch_bytes(0, c.num_assets, c.features) / 4 + 3) / 4 * 4);
     h->lds_scalar = (size_t)kScalarWaves * h->scalar_scratch_floats * 4;
@@ -504,9 +524,10 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         }
         h->owns_state = true;
     }
-    if (h->flat_inplace) {
-        const uint32_t cpw = (uint32_t)(h->flat_ip_block * h->flat_ip_vec);
-        const uint32_t wgs = (h->flat_qtot + cpw - 1) / cpw;
+    if (h->flat_inplace || h->gen_ok) {
+        const uint32_t cpw = (uint32_t)(h->flat_inplace ? h->flat_ip_block * h->flat_ip_vec : h->gen_block * h->gen_v);
+        const uint32_t qtot = h->flat_inplace ? h->flat_qtot : h->gen_qtot;
+        const uint32_t wgs = (qtot + cpw - 1) / cpw;
         h->halo_wgs = wgs > 0 ? wgs - 1 : 0;
         hipError_t ae = hipMalloc(&h->halo, (size_t)(h->halo_wgs + 1) * 32);
         if (ae != hipSuccess) {
@@ -626,6 +647,7 @@ int pmenv_set_step_path(pmenv* h, int32_t path) {
     h->one = bits;
     h->flat1 = fbits;
     h->relay = rbits;
+    h->gen = gen_bits(h, path);
     return PMENV_OK;
 }
 
@@ -717,6 +739,20 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         if (ph & PMENV_PHASE_ADVANCE) {
             launch_advance(h, p, stream);
             return check_launch(h, "advance kernel");
+        }
+        return PMENV_OK;
+    }
+    if (h->gen_ok && (h->gen & fuse_bit) && obs16) {
+        // F != 5: the scalar step (copying the in-place stream's halo), then the generic stream
+        const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        if (ph & PMENV_PHASE_SCALAR) {
+            launch_scalar(h, p, stream);
+            const int rc = check_launch(h, "scalar_step_kernel");
+            if (rc) return rc;
+        }
+        if (ph & PMENV_PHASE_ADVANCE) {
+            launch_gen(h, p, stream);
+            return check_launch(h, "advance_gen_kernel");
         }
         return PMENV_OK;
     }
@@ -895,10 +931,19 @@ size_t pmenv_state_bytes(const pmenv* h) { return h ? h->state_bytes : 0; }
 
 const char* pmenv_step_path(const pmenv* h) {
     if (!h) return "";
-    if (!h->streaming) return h->small_block ? "step_small_kernel" : "step_advance_lds_kernel";
     // per window mode: the one-launch kernel, or the scalar step (K1) then the stream
     const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
                    : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
+    if (!h->streaming) {
+        const char* one = h->small_block ? "step_small_kernel" : "step_advance_lds_kernel";
+        if (!h->gen) return one;
+        static thread_local char gout[320];
+        char g2[96];
+        snprintf(g2, sizeof g2, "%s+advance_gen_kernel", k1);
+        snprintf(gout, sizeof gout, "%s (obs_out) | %s (in place)", (h->gen & PMENV_FUSE_DB) ? g2 : one,
+                 (h->gen & PMENV_FUSE_INPLACE) ? g2 : one);
+        return gout;
+    }
     const char* db2 = h->flat ? "advance_flat_wg_kernel" : "advance_rows_kernel";
     const char* ip2 = h->flat_inplace ? "advance_flat_inplace_kernel" : "advance_rows_kernel";
     static thread_local char buf[2][128], out[320];
@@ -1310,6 +1355,7 @@ __attribute__((weak, noinline)) void release(pmenv*) {}
 __attribute__((weak, noinline)) bool launch_scalar(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_advance(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_one(const pmenv*, const StepParams&, hipStream_t) { return false; }
+__attribute__((weak, noinline)) bool launch_small(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_fused(const pmenv*, const StepParams&, int, uint32_t, hipStream_t) {
     return false;
 }

@@ -256,7 +256,7 @@ __device__ __forceinline__ void vec_tail(const StepParams& p, int b, int lane, c
     const int32_t k = in.k;
     const double value = m.value, V = m.V;
     // :83-84 ring.update(w') at slot (1 + k) % W
-    const int slot = (int)((1 + (int64_t)k) % W);
+    const int slot = ring_slot(k, W);
     float* ring_row = p.ring + (size_t)bc * W * N + (size_t)slot * N;
 #pragma unroll
     for (int e = 0; e < A; ++e) {

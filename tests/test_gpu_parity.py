@@ -552,6 +552,46 @@ def test_gpu_register_step_vs_oracle(N, W, F, B, path, kw, db):
     _run_both(kw, B=B, N=N, W=W, T=2 * W + 3, kind="mixed", F=F, seed=N * 100 + W * 10 + F, double_buffer=db)
 
 
+@pytest.mark.parametrize("N,W,F,B", [
+    (30, 50, 8, 4),       # 12,000 floats per env: three 4,096-float workgroups per env
+    (8, 10, 3, 11),       # 240 floats: many envs per workgroup
+    (5, 12, 2, 9),        # one market channel
+    (9, 8, 4, 13),        # F = 4: every day a whole chunk
+    (3, 20, 6, 7),
+    (11, 4, 7, 5),        # W = 4: most chunks span two rows' days
+    (64, 16, 8, 3),
+    (65, 16, 4, 2),       # N > 64: the packed scalar step
+])
+@pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
+                         ids=["storage", "chrono", "commission"])
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_generic_stream_vs_oracle(N, W, F, B, kw, db):
+    """F != 5 on two launches: the scalar step, then advance_gen_kernel (the window staged in
+    LDS, the shift by F floats read dword-wise, the in-place halo copied by the scalar step),
+    against the oracle past the ring's wrap, with a masked reset midway."""
+    from pmenv import TradingEnv
+    kw = dict(kw, close_channel=F - 2)
+    e = TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, step_impl="two_launch", **kw)
+    assert e.step_path.count("advance_gen_kernel") == 2, e.step_path
+    rng = np.random.default_rng(N + W + F)
+    _run_both(kw, B=B, N=N, W=W, T=2 * W + 3, kind="mixed", F=F, seed=N * 100 + W * 10 + F, double_buffer=db,
+              impl="two_launch", resets={W // 2 + 1: rng.random(B) < 0.4})
+
+
+def test_gpu_generic_stream_auto_threshold():
+    """AUTO gives F != 5 windows above 32 MiB the generic stream and keeps the register step
+    below; F = 5, F > 8 and non-granular windows never take it."""
+    from pmenv import TradingEnv
+    big = TradingEnv(num_envs=1024, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    assert big.step_path.count("advance_gen_kernel") == 2, big.step_path
+    small = TradingEnv(num_envs=8, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    assert small.step_path == "step_small_kernel"
+    assert "advance_gen_kernel" not in TradingEnv(num_envs=4096, num_assets=30, window=50, device=DEV).step_path
+    wide = TradingEnv(num_envs=8, num_assets=30, window=50, features=12, close_channel=10, device=DEV)
+    with pytest.raises(ValueError):
+        wide.set_step_impl("two_launch")
+
+
 def test_gpu_masked_reset_mid_run():
     B = 20
     rng = np.random.default_rng(5)

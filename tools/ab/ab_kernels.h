@@ -710,4 +710,116 @@ __global__ __launch_bounds__(BLOCK) void step_relay_env_kernel(StepParams p, Rel
         relay_env_tile<BLOCK, V, POL, OUT>(p, r, per4, (int)(blockIdx.x - r.scal), epoch, kp_in);
 }
 
+// The register step (env_step.h step_small_kernel, REG form) with wall-clock stamps and
+// timing-only ablations (PMENV_SMALL_ABL): where config 1's 1 x 5 x 50 x 5 step spends its
+// time. Thread 0 reads s_memrealtime (100 MHz) at each phase and stores the stamps with one
+// vector store per stamp into g_small_stamps[slot][0..7]; the last wave stamps its entry in
+// [7]. ABL: 2 no scalar step (w' = 0, no tail), 4 no window loads / stores, 8 return at once,
+// 16 no tail. The stamps are read back by pmenv_tools_small_stamps (pmenv_ab.hip).
+__device__ uint64_t g_small_stamps[1024 * 8];
+
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    return t;
+}
+
+template <int BLOCK, int E, int ABL>
+__global__ __launch_bounds__(BLOCK) void small_stamp_kernel(StepParams p, uint32_t slot_id) {
+    static_assert(E <= 8, "the stamped copy keeps the product's small-E form only");
+    __shared__ float sh_wp[64];
+    uint64_t ts[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int tid = threadIdx.x;
+    if (tid == 0) ts[0] = stamp_now();
+    if (tid == BLOCK - 64) {
+        const uint64_t t = stamp_now();
+        g_small_stamps[(slot_id & 1023) * 8 + 7] = t;
+    }
+    if (ABL & 8) {
+        if (tid == 0) g_small_stamps[(slot_id & 1023) * 8] = ts[0];
+        return;
+    }
+    const int b = blockIdx.x;
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
+    const uint32_t WF = (uint32_t)(W * F), NWF = (uint32_t)N * WF;
+    constexpr uint32_t kOut = 0x80000000u;
+    const auto rs_in = make_rsrc(p.obs + (size_t)b * NWF, NWF * 4u);
+    const auto rs_out = make_rsrc(p.obs_out + (size_t)b * NWF, NWF * 4u);
+    const float* barg = env_bar(p, b);
+    const auto rs_bar = make_rsrc(barg ? barg : p.obs, barg ? (uint32_t)(N * Fm) * 4u : 0u);
+    const float nanv = __int_as_float(0x7fc00000);
+    uint32_t z = 0u;
+    asm volatile("" : "+v"(z));
+    const ScalarIn sin = scalar_load<64, true>(p, b, tid, z);
+    const int32_t k0 = sin.k;
+    uint32_t xr[E], xt[E], xf[E];
+    float src[E], cur[E];
+    if (!(ABL & 4)) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+            const uint32_t row = fdiv(j, p.div_wf);
+            const uint32_t kk = j - row * WF;
+            const uint32_t t = fdiv(kk, p.div_f);
+            const uint32_t f = kk - t * (uint32_t)F;
+            xr[e] = row;
+            xt[e] = t;
+            xf[e] = f;
+            const bool mkt = j < NWF && (int)f < Fm, last = (int)t == W - 1;
+            const float sh = buf_load1(rs_in, mkt && !last ? (j + (uint32_t)F) * 4u : kOut);
+            const float bv = buf_load1(rs_bar, mkt && last ? (row * (uint32_t)Fm + f) * 4u : kOut);
+            src[e] = last ? (barg ? bv : nanv) : sh;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+            const bool wch = j < NWF && (int)xf[e] == Fm;
+            const float ws = buf_load1(rs_in, wch && (int)xt[e] < W - 1 ? (j + (uint32_t)F) * 4u : kOut);
+            cur[e] = buf_load1(rs_in, wch ? j * 4u : kOut);
+            src[e] = wch ? ws : src[e];
+        }
+    }
+    const bool shift_w = p.ring_mode == PMENV_RING_CHRONO || k0 < W - 1;
+    ScalarMid mid{};
+    if (tid < 64) {
+        if (!(ABL & 2)) {
+            mid = scalar_core<64>(p, b, tid, sin);
+        } else {
+            mid.wp = sin.a;
+            mid.k = sin.k;
+        }
+        sh_wp[tid] = mid.wp;
+    }
+    if (tid == 0) {
+        asm volatile("" ::"v"(mid.wp));
+        ts[1] = stamp_now();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) ts[2] = stamp_now();
+    __syncthreads();
+    if (tid == 0) ts[3] = stamp_now();
+    const int slot = ring_slot(k0, W);
+    if (!(ABL & 4)) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+            const uint32_t row = xr[e], t = xt[e], f = xf[e];
+            const float v = src[e];
+            const float wp = sh_wp[min(row, (uint32_t)N - 1u)];
+            const float wv = pick(shift_w, pick((int)t == W - 1, wp, v), pick((int)t == slot, wp, cur[e]));
+            const float o = pick((int)f == Fm && j < NWF, wv, v);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
+        }
+    }
+    if (tid == 0) ts[4] = stamp_now();
+    if (!(ABL & 18) && tid < 64) scalar_tail<64>(p, b, tid, sin, mid);
+    if (tid == 0) ts[5] = stamp_now();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) {
+        ts[6] = stamp_now();
+        uint64_t* d = g_small_stamps + (slot_id & 1023) * 8;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) d[i] = ts[i];
+    }
+}
 }  // namespace pmenv_dev

@@ -54,6 +54,8 @@ struct Tools {
     int flat_direct = 0, flat_direct_abl = 0, stream_bare = 0;
     bool flat_lside = false;
     bool flat_perelem = false;  // PMENV_FLAT_PERELEM: the stream's per-element compose (flat_wg_body)
+    int small_abl = -1;         // PMENV_SMALL_ABL: small_stamp_kernel (stamps, + ablation bits), -1 = product
+    uint32_t small_slot = 0;    // its stamp slot, one per launch
 };
 
 Tools* tools(const pmenv* h) { return static_cast<Tools*>(h->tools); }
@@ -359,6 +361,16 @@ void plan(pmenv* h) {
             h->small_e = e;
         }
     }
+    t->small_abl = knob_int("PMENV_SMALL_ABL", -1);
+    if (knob_int("PMENV_GEN_OFF", 0)) h->gen_auto = 0;   // AUTO keeps the register step for F != 5
+    if (const char* k = knob("PMENV_GEN_GEOM")) {     // advance_gen_kernel's BLOCK x V: 256x4 | 256x2 | 512x2
+        int bk = 0, v = 0;
+        if (h->gen_ok && sscanf(k, "%dx%d", &bk, &v) == 2 && (bk * 10 + v == 2564 || bk * 10 + v == 2562 ||
+                                                               bk * 10 + v == 5122)) {
+            h->gen_block = bk;
+            h->gen_v = v;
+        }
+    }
     t->one_nocap = knob_int("PMENV_ONE_NOCAP", 0) != 0;
     t->flat1_lds_pad = knob_int("PMENV_FLAT1_LDS_PAD", 0);
     t->flat_s80 = knob_int("PMENV_FLAT_S80", 0) != 0;
@@ -479,6 +491,30 @@ bool launch_scalar(const pmenv* h, const StepParams& p, hipStream_t stream) {
         if (h->cfg.num_assets <= 32) scalar_reg_groups<32>(t->k1_groups, q, stream);
         else scalar_reg_groups<64>(t->k1_groups, q, stream);
     } else launch_scalar_kernels(h, q, stream);
+    return true;
+}
+
+template <int BLOCK, int E>
+void small_stamp(int abl, const StepParams& p, uint32_t slot, hipStream_t stream) {
+    const unsigned grid = (unsigned)p.B;
+    switch (abl) {
+    case 0: small_stamp_kernel<BLOCK, E, 0><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    case 2: small_stamp_kernel<BLOCK, E, 2><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    case 4: small_stamp_kernel<BLOCK, E, 4><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    case 6: small_stamp_kernel<BLOCK, E, 6><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    case 8: small_stamp_kernel<BLOCK, E, 8><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    default: small_stamp_kernel<BLOCK, E, 16><<<grid, BLOCK, 0, stream>>>(p, slot); break;
+    }
+}
+
+bool launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    Tools* t = tools(h);
+    if (t->small_abl < 0 || h->cfg.num_assets > 64) return false;
+    const uint32_t slot = t->small_slot++;
+    switch (h->small_block * 100 + h->small_e) {
+    case 25608: small_stamp<256, 8>(t->small_abl, p, slot, stream); break;
+    default: return false;
+    }
     return true;
 }
 
@@ -1024,3 +1060,9 @@ bool batch_reward_forward(const float* a, const float* v_prev, const float* p, i
 }
 
 }  // namespace pmenv_tools
+
+// the stamps of small_stamp_kernel (PMENV_SMALL_ABL), 1024 launches x 8 u64 (100 MHz ticks)
+extern "C" int pmenv_tools_small_stamps(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pmenv_dev::g_small_stamps), sizeof(uint64_t) * 1024 * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
