@@ -18,6 +18,8 @@
  *      - the one-launch step (step_env.h): a workgroup owns one env; its slots are the
  *        env's 1 KiB-aligned 64-chunk blocks, lanes outside the env read 0 and store
  *        nothing. Reads outside the env are checked never to feed a kept position.
+ *    - the generic stream for F != 5 (env_step.h advance_gen_kernel): the same workgroup
+ *      and halo, the shift by F floats, the element walk over rows and the staged rows.
  * 3. Emulates the flat one-launch step (step_flat.h) over consecutive steps: tiles in a
  *    random order, the halo and the state snapshot by parity, one owner per env (below).
  * 4. Emulates the relayed step (step_relay.h) over consecutive steps: workgroups dispatched
@@ -270,6 +272,92 @@ static void emulate(int B, int N, int W, int CPW, int shift_w, int slot) {
     for (int64_t i = 0; i < tot; ++i)
         if (memcmp(&mem[i], &ref[i], 4)) { CHECK(0, "one: float %lld differs (B%d N%d W%d)", (long long)i, B, N, W); break; }
     free(mem); free(init); free(ref); free(bar); free(wp); free(stored); free(halo); free(order); free(lds); free(img);
+}
+
+/* ------------------------------------------------------------ 2b. the generic stream (F != 5) */
+/* env_step.h advance_gen_kernel in place: workgroups of CPW chunks in a random order, every
+ * store visible at once; the two chunks past a workgroup from the halo (copied before any
+ * store), the shift by F floats read from the staged image (checked: never past it), the
+ * workgroup's rows g_lo .. g_hi staged one per thread (checked: at most BLOCK rows, and the
+ * element walk's row index inside them), and each element's (day, channel, row) from the
+ * chunk's first element plus the kernel's increments. Exact against the out-of-place advance. */
+static void emulate_gen(int B, int N, int W, int F, int BLOCK, int CPW, int shift_w, int slot) {
+    const int Fm = F - 1, WF = W * F;
+    const int64_t per = (int64_t)N * WF, tot = per * B;
+    if (per % 4) return;
+    const int64_t per4 = per / 4, qtot = tot / 4;
+    float* mem = malloc(sizeof(float) * tot);
+    float* ref = malloc(sizeof(float) * tot);
+    float* bar = malloc(sizeof(float) * B * N * Fm);
+    float* wp = malloc(sizeof(float) * B * N);
+    uint8_t* stored = calloc((size_t)qtot, 1);
+    for (int64_t i = 0; i < tot; ++i) mem[i] = (float)nrand();
+    for (int i = 0; i < B * N * Fm; ++i) bar[i] = (float)nrand();
+    for (int i = 0; i < B * N; ++i) wp[i] = (float)urand();
+    for (int64_t g = 0; g < (int64_t)B * N; ++g)         /* the out-of-place reference */
+        for (int t = 0; t < W; ++t)
+            for (int f = 0; f < F; ++f) {
+                const int64_t j = g * WF + t * F + f;
+                float v;
+                if (f == Fm) v = shift_w ? (t == W - 1 ? wp[g] : mem[j + F]) : (t == slot ? wp[g] : mem[j]);
+                else v = t == W - 1 ? bar[g * Fm + f] : mem[j + F];
+                ref[j] = v;
+            }
+    const int64_t nwg = (qtot + CPW - 1) / CPW;
+    float* halo = malloc(sizeof(float) * 8 * (size_t)nwg);
+    for (int64_t i = 0; i + 1 < nwg; ++i)                /* the scalar step's halo copy, before any store */
+        for (int h = 0; h < 2; ++h) {
+            const int64_t q = (i + 1) * CPW + h;
+            for (int e = 0; e < 4; ++e) halo[i * 8 + h * 4 + e] = q < qtot ? mem[q * 4 + e] : 0.0f;
+        }
+    int* order = malloc(sizeof(int) * (size_t)nwg);
+    shuffle(order, (int)nwg);
+    float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
+    for (int o = 0; o < nwg; ++o) {
+        const int64_t wg = order[o], c0 = wg * CPW;
+        const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
+        for (int64_t q = 0; q < CPW + 2; ++q) {
+            for (int e = 0; e < 4; ++e) lds[q * 4 + e] = 0.0f;
+            if (q < nblk) {
+                CHECK(!stored[c0 + q], "gen: chunk %lld read after a store", (long long)(c0 + q));
+                for (int e = 0; e < 4; ++e) lds[q * 4 + e] = mem[(c0 + q) * 4 + e];
+            } else if (q >= CPW && wg + 1 < nwg) {
+                for (int e = 0; e < 4; ++e) lds[q * 4 + e] = halo[wg * 8 + (q - CPW) * 4 + e];
+            }
+        }
+        const int64_t b_lo = c0 / per4, ql = c0 + nblk - 1, b_hi = ql / per4;
+        const int64_t g_lo = b_lo * N + (4 * (c0 - b_lo * per4)) / WF;
+        const int64_t g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
+        CHECK(g_hi - g_lo < BLOCK, "gen: %lld rows in a workgroup of %d threads", (long long)(g_hi - g_lo + 1), BLOCK);
+        for (int64_t q = 0; q < nblk; ++q) {
+            const int64_t gq = c0 + q, b = gq / per4;
+            const int64_t j0 = 4 * (gq - b * per4), row = j0 / WF, kk = j0 - row * WF;
+            int t = (int)(kk / F), f = (int)(kk - (int64_t)t * F);
+            int64_t r = b * N + row - g_lo;
+            for (int e = 0; e < 4; ++e) {
+                CHECK(r >= 0 && r <= g_hi - g_lo, "gen: row %lld outside the staged rows", (long long)r);
+                CHECK(q * 4 + e + F < 4 * (CPW + 2), "gen: shifted read past the image");
+                const int64_t g = g_lo + r;
+                const float sh = lds[q * 4 + e + F], un = lds[q * 4 + e];
+                const int last = t == W - 1;
+                const float wv = shift_w ? (last ? wp[g] : sh) : (t == slot ? wp[g] : un);
+                mem[gq * 4 + e] = f == Fm ? wv : (last ? bar[g * Fm + (f < Fm ? f : 0)] : sh);
+                const int fw = f == Fm;
+                f = fw ? 0 : f + 1;
+                t += fw;
+                const int tw = t == W;
+                t = tw ? 0 : t;
+                r += tw;
+            }
+            stored[gq] = 1;
+        }
+    }
+    for (int64_t i = 0; i < tot; ++i)
+        if (memcmp(&mem[i], &ref[i], 4)) {
+            CHECK(0, "gen: float %lld differs (B%d N%d W%d F%d CPW%d)", (long long)i, B, N, W, F, CPW);
+            break;
+        }
+    free(mem); free(ref); free(bar); free(wp); free(stored); free(halo); free(order); free(lds);
 }
 
 /* ------------------------------------------------------------ 3. the flat one-launch step */
@@ -959,6 +1047,18 @@ int main(void) {
             for (int cpw = 0; cpw < 2; ++cpw)
                 emulate(shapes[i][0], shapes[i][1], shapes[i][2], cpw ? 1024 : 96, mode == 0,
                         mode ? (int)(urand() * shapes[i][2]) : 0);
+    /* the generic stream (F != 5): the product's 256 x 4 tiles and 512 x 2, and small ones
+     * (64 threads x 1) that put many envs and rows in one tile, both weight-channel modes */
+    const int gshp[][4] = {{4, 30, 50, 8}, {11, 8, 10, 3}, {9, 5, 12, 2}, {13, 9, 8, 4}, {7, 3, 20, 6},
+                           {5, 11, 4, 7}, {3, 64, 16, 8}, {2, 65, 16, 4}, {40, 2, 10, 6}};
+    for (size_t i = 0; i < sizeof gshp / sizeof gshp[0]; ++i)
+        for (int mode = 0; mode < 2; ++mode) {
+            const int B = gshp[i][0], N = gshp[i][1], W = gshp[i][2], F = gshp[i][3];
+            const int sl = mode ? (int)(urand() * W) : 0;
+            if (4 * 1024 / (W * F) + 2 <= 256) emulate_gen(B, N, W, F, 256, 1024, mode == 0, sl);
+            if (4 * 1024 / (W * F) + 2 <= 512) emulate_gen(B, N, W, F, 512, 1024, mode == 0, sl);
+            if (4 * 64 / (W * F) + 2 <= 64) emulate_gen(B, N, W, F, 64, 64, mode == 0, sl);
+        }
     /* the flat one-launch step: the product's 1,024-chunk tiles (256 x 4 and 512 x 2) and
      * small tiles that put several tiles in one env and several envs in one tile, both ring
      * orders, through the wrap and a re-prime */
