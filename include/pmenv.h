@@ -214,15 +214,20 @@ int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream);
  * "step_flat_vec_kernel" (the same for 64 < N <= 512),
  * "step_env_kernel" (the whole step in one launch, one workgroup per env) or
  * "<scalar step>+<window stream>"
- * (two launches); or, for F != 5 or windows that are not 16-B granular, "step_small_kernel"
- * (one workgroup per env, the window in registers: env windows of at most 16,384 floats) or
- * "step_advance_lds_kernel" (the LDS-tiled fallback, any F). */
+ * (two launches; for F != 5 the stream is advance_gen_kernel); or, for F != 5 or windows that
+ * are not 16-B granular, "step_tiny_kernel" (one workgroup per env, the window staged in LDS:
+ * env windows of at most 2,048 floats, N <= 64), "step_small_kernel" (one workgroup per env,
+ * the window in registers: env windows of at most 16,384 floats) or "step_advance_lds_kernel" (the LDS-tiled
+ * fallback, any F). */
 const char* pmenv_step_path(const pmenv* h);
 
 /* Advance-mode step implementation. AUTO (the default) picks per shape and window
  * mode; ONE_LAUNCH forces step_env_kernel (one workgroup per env: F = 5, W >= 2,
  * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
- * kernel followed by the window stream (F = 5, 16-B granular env windows); FLAT forces
+ * kernel followed by the window stream (F = 5, 16-B granular env windows; or the generic
+ * stream advance_gen_kernel for 2 <= F <= 8, F != 5, 16-B granular env windows with
+ * W F >= 17, which AUTO also takes for such windows above 16 MiB of at most 16,384 floats
+ * per env); FLAT forces
  * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:
  * F = 5, W >= 2, env windows of >= 148 16-B chunks, N <= 64 — or, as step_flat_vec_kernel,
  * 64 < N <= 512 with W >= 14). Returns PMENV_ERR_ARG

@@ -490,6 +490,43 @@ __device__ __forceinline__ ScalarMid scalar_core(const StepParams& p, int b, int
     return m;
 }
 
+// trading_env.py:88 ret = value / self.value (gross: mu-scaled, excludes commission)
+__device__ __forceinline__ double step_ret(const StepParams& p, const ScalarIn& in, const ScalarMid& m) {
+    return p.ret_mode == PMENV_RET_GROSS ? m.value / m.V : m.value / in.v_prev;
+}
+
+// the step's reward from its return (trading_env.py:89-99, reward.py); the Sharpe forms
+// update their running statistics sa / sb (stats = true). k: the counter before the step
+__device__ __forceinline__ double step_reward(const StepParams& p, int32_t k, double ret, double& sa, double& sb,
+                                              bool& stats) {
+    switch (p.reward_kind) {
+    case PMENV_REWARD_RETURN:
+        return ret * p.scale;
+    case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
+        double mm = (double)(k + 1);
+        double mean = sa, m2 = sb;
+        double d = ret - mean;
+        mean += d / mm;
+        m2 += d * (ret - mean);
+        sa = mean;
+        sb = m2;
+        stats = true;
+        return mm < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (mm - 1.0)) * p.scale;
+    }
+    case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
+        double R = ret - 1.0, A = sa, Bm = sb;
+        double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
+        const double r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
+        sa = A + p.eta * dA;
+        sb = Bm + p.eta * dB;
+        stats = true;
+        return r;
+    }
+    default:
+        return log(ret) * p.scale;           // :99
+    }
+}
+
 // SNAP (step_flat_kernel): only the env's owner workgroup (`owner`) writes the state,
 // reward and ring slot, and it also writes the next step's snapshot (sv_out .. slc_out)
 template <int L, bool SNAP = false>
@@ -501,7 +538,7 @@ __device__ __forceinline__ void scalar_tail(const StepParams& p, int b, int lane
     const bool act = env_ok && n < N;
     const size_t i = (size_t)(env_ok ? b : 0) * N + (act ? n : 0);
     const int32_t k = m.k;
-    const double value = m.value, V = m.V;
+    const double value = m.value;
     // :83-84 ring.update(w') at slot idx = (1 + k) % W
     const int slot = ring_slot(k, W);
     const bool wr = !SNAP || owner;
@@ -518,33 +555,13 @@ __device__ __forceinline__ void scalar_tail(const StepParams& p, int b, int lane
     }
     if (env_ok && n == 0 && wr) {
         // :88 ret = value / self.value (mu-scaled: excludes commission) ; :89
-        const double ret = p.ret_mode == PMENV_RET_GROSS ? value / V : value / in.v_prev;
-        double r;
-        switch (p.reward_kind) {
-        case PMENV_REWARD_RETURN:
-            r = ret * p.scale;
-            break;
-        case PMENV_REWARD_SHARPE: {              // reward.py:26-31 as running moments
-            double mm = (double)(k + 1);
-            double mean = in.sa, m2 = in.sb;
-            double d = ret - mean;
-            mean += d / mm;
-            m2 += d * (ret - mean);
-            p.sa[b] = mean;
-            p.sb[b] = m2;
-            r = mm < 2.0 ? NAN : (mean - p.rf) / sqrt(m2 / (mm - 1.0)) * p.scale;
-            break;
-        }
-        case PMENV_REWARD_DIFF_SHARPE: {         // Moody & Saffell (1998)
-            double R = ret - 1.0, A = in.sa, Bm = in.sb;
-            double dA = R - A, dB = R * R - Bm, var = Bm - A * A;
-            r = var > 1e-12 ? (Bm * dA - 0.5 * A * dB) / (var * sqrt(var)) * p.scale : 0.0;
-            p.sa[b] = A + p.eta * dA;
-            p.sb[b] = Bm + p.eta * dB;
-            break;
-        }
-        default:
-            r = log(ret) * p.scale;              // :99
+        const double ret = step_ret(p, in, m);
+        double sa = in.sa, sb = in.sb;
+        bool stats = false;
+        const double r = step_reward(p, k, ret, sa, sb, stats);
+        if (stats) {
+            p.sa[b] = sa;
+            p.sb[b] = sb;
         }
         p.value[b] = value;
         p.k[b] = k + 1;
@@ -1331,7 +1348,7 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     __shared__ f4 sh4[CPW + 2];
     __shared__ float sh_bar[BLOCK * kFm];
     __shared__ float sh_wp[BLOCK];
-    __shared__ int32_t sh_kc[BLOCK];
+    __shared__ int32_t sh_sl[BLOCK];                         // the row's ring slot, or -1 while it shifts
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t c0 = blockIdx.x * CPW;
     const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
@@ -1339,8 +1356,9 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     f4 own[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) own[v] = buf_load4<0>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
-    const uint32_t nh = blockIdx.x + 1 < gridDim.x ? min(2u, qtot - c0 - nblk) : 0u;
-    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : p.halo + (size_t)blockIdx.x * 8;
+    // (no halo buffer in place: nothing is read, the two chunks stay 0)
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x && (OUT || p.halo) ? min(2u, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : (p.halo ? p.halo + (size_t)blockIdx.x * 8 : p.obs);
     const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
     __builtin_amdgcn_sched_barrier(0);
     const int N = p.N, W = p.W, F = p.F, Fm = F - 1, WF = W * F;
@@ -1361,14 +1379,15 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
             sh_bar[tid * kFm + f] = barb ? x : __int_as_float(0x7fc00000);
         }
         sh_wp[tid] = p.w_new[g];
-        sh_kc[tid] = p.k[b] - 1;                                     // the scalar step counted this step
+        const int32_t kc = p.k[b] - 1;                               // the scalar step counted this step
+        const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && kc >= W - 1);
+        sh_sl[tid] = shift_w ? -1 : (int)((uint32_t)(1 + kc) - fdiv((uint32_t)(1 + kc), p.div_w) * (uint32_t)W);
     }
 #pragma unroll
     for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
     if (tid < 2) sh4[CPW + tid] = hal;
     __syncthreads();
     const float* shf = reinterpret_cast<const float*>(sh4);
-    const bool storage = p.ring_mode == PMENV_RING_STORAGE;
     const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -1385,14 +1404,12 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int32_t kc = sh_kc[r];
+            const int slot = sh_sl[r];
             const float wp = sh_wp[r];
             const float bf = sh_bar[r * kFm + min(f, kFm - 1)];
             const float sh = shf[4 * j + e + F];
             const bool last = t == W - 1;
-            const bool shift_w = !(storage && kc >= W - 1);
-            const int slot = (int)((uint32_t)(1 + kc) - fdiv((uint32_t)(1 + kc), p.div_w) * (uint32_t)W);
-            const float wv = shift_w ? (last ? wp : sh) : (t == slot ? wp : un[e]);
+            const float wv = slot < 0 ? (last ? wp : sh) : (t == slot ? wp : un[e]);
             o[e] = f == Fm ? wv : (last ? bf : sh);
             // the next element: channel, day, row
             const bool fw = f == Fm;
@@ -1621,6 +1638,110 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
     }
     // the state writes and the reward after the window's stores (the barrier waited for the core only)
     if (REG && tid < 64) scalar_tail<64>(p, b, tid, sin, mid);
+}
+
+// The register step for the smallest windows (env windows of at most BLOCK x E floats, E <= 8,
+// N <= 64: config 1's 1 x 5 x 50 x 5), staged through LDS: every thread issues its 16-B loads
+// of the env block (dword-aligned: env windows need not be 16-B granular) and the bar, all
+// with the scalar step's loads and none waiting for another; wave 0 runs the whole scalar
+// step up to the reward while they are in flight (the return, log and statistics included:
+// only stores are left after the barrier); the window's floats then come from LDS — the
+// shifted source at j + F, the own weight float at j — and leave as coalesced dword stores,
+// followed by the state's stores. A quarter of step_small_kernel's load instructions per
+// wave, and no f64 tail after the window's stores. Same values, element by element.
+template <int BLOCK, int E>
+__global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
+    static_assert(E % 4 == 0 && E <= 8, "16-B chunks, at most two per thread");
+    constexpr int Q = E / 4;                               // chunks per thread
+    extern __shared__ __attribute__((aligned(16))) float lds[];   // [NWF + 8] window | [N (F-1)] bar
+    __shared__ float sh_wp[64];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
+    const uint32_t WF = (uint32_t)(W * F), NWF = (uint32_t)N * WF, nq = NWF >> 2;
+    constexpr uint32_t kOut = 0x80000000u;
+    const auto rs_in = make_rsrc(p.obs + (size_t)b * NWF, NWF * 4u);
+    const auto rs_out = make_rsrc(p.obs_out + (size_t)b * NWF, NWF * 4u);
+    const float* barg = env_bar(p, b);                     // null: a day outside the series (NaN bar)
+    const uint32_t nbar = (uint32_t)(N * Fm);
+    const auto rs_bar = make_rsrc(barg ? barg : p.obs, barg ? nbar * 4u : 0u);
+    uint32_t z = 0u;
+    asm volatile("" : "+v"(z));
+    const ScalarIn sin = scalar_load<64, true>(p, b, tid, z);   // every wave: no branch before the loads
+    f4 ch[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t c = (uint32_t)tid + (uint32_t)(BLOCK * q);
+        ch[q] = buf_load4<0>(rs_in, c < nq ? c * 16u : kOut);
+    }
+    const uint32_t jt = nq * 4u + (uint32_t)tid;            // the block's last NWF % 4 floats
+    const float tl = buf_load1(rs_in, jt < NWF ? jt * 4u : kOut);
+    const float bv = buf_load1(rs_bar, (uint32_t)tid < nbar ? (uint32_t)tid * 4u : kOut);
+    float* lbar = lds + NWF + 8;
+    const int32_t k0 = sin.k;
+    ScalarMid mid;
+    double ret = 0.0, rwd = 0.0, sa = sin.sa, sb = sin.sb;
+    bool stats = false;
+    if (tid < 64) {
+        mid = scalar_core<64>(p, b, tid, sin);
+        sh_wp[tid] = mid.wp;
+        ret = step_ret(p, sin, mid);
+        rwd = step_reward(p, mid.k, ret, sa, sb, stats);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const uint32_t c = (uint32_t)tid + (uint32_t)(BLOCK * q);
+        if (c < nq) reinterpret_cast<f4*>(lds)[c] = ch[q];
+    }
+    if (jt < NWF + 8u) lds[jt] = jt < NWF ? tl : 0.0f;      // and 8 floats past the block (read only by last days)
+    if ((uint32_t)tid < nbar) lbar[tid] = barg ? bv : __int_as_float(0x7fc00000);
+    // every load of every wave has returned before any store: the counter the waves past the
+    // first read (for the ring slot) is one wave 0 rewrites after the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool shift_w = p.ring_mode == PMENV_RING_CHRONO || k0 < W - 1;
+    const int slot = ring_slot(k0, W);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t j = (uint32_t)tid + (uint32_t)(BLOCK * e);
+        const uint32_t jc = j < NWF ? j : 0u;
+        const uint32_t row = fdiv(jc, p.div_wf);
+        const uint32_t kk = jc - row * WF;
+        const uint32_t t = fdiv(kk, p.div_f);
+        const int f = (int)(kk - t * (uint32_t)F);
+        const bool last = (int)t == W - 1;
+        const float sh = lds[jc + (uint32_t)F];
+        const float un = lds[jc];
+        const float wp = sh_wp[row];
+        const float bf = lbar[row * (uint32_t)Fm + (uint32_t)min(f, Fm - 1 < 0 ? 0 : Fm - 1)];
+        const float wv = shift_w ? (last ? wp : sh) : ((int)t == slot ? wp : un);
+        const float o = f == Fm ? wv : (last ? bf : sh);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rs_out, j < NWF ? j * 4u : kOut, 0, 0);
+    }
+    // the state's stores (scalar_tail's, the reward computed before the barrier)
+    if (tid < 64) {
+        const int n = tid;
+        const bool act = n < N;
+        const size_t i = (size_t)b * N + (act ? n : 0);
+        if (act) {
+            const float wp = mid.wp;
+            p.ring[(size_t)b * W * N + (size_t)ring_slot(mid.k, W) * N + n] = wp;
+            p.w_new[i] = wp;
+            if (p.weights) p.weights[i] = wp;
+            if (p.bar) p.last_close[i] = mid.cn;
+        }
+        if (n == 0) {
+            if (stats) {
+                p.sa[b] = sa;
+                p.sb[b] = sb;
+            }
+            p.value[b] = mid.value;
+            p.k[b] = mid.k + 1;
+            if (p.reward) p.reward[b] = (float)rwd;
+            if (p.ret) p.ret[b] = ret;
+            if (!isfinite(rwd) || !isfinite(mid.value)) atomicAdd(p.nonfinite, 1ull);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- surface kernel

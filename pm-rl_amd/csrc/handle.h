@@ -34,6 +34,7 @@ struct pmenv {
     // the register step (step_small_kernel<small_block, small_e>): any F, any alignment, env
     // windows of at most 1,024 x 16 floats; 0: the LDS fallback
     int small_block, small_e;
+    bool tiny;            // ... of at most 256 x 8 floats and N <= 64: step_tiny_kernel (LDS-staged)
     // LDS single-launch fallback geometry
     int rows_per_tile, tile_floats;
     bool vec;

@@ -124,6 +124,7 @@ inline void launch_gen_g(const pmenv* h, const StepParams& p, hipStream_t stream
 }
 inline void launch_gen(const pmenv* h, StepParams p, hipStream_t stream) {
     p.div_units = make_fastdiv(h->per4);
+    p.halo = h->halo;                      // in place: the two chunks past each workgroup (the scalar step's copy)
     switch (h->gen_block * 10 + h->gen_v) {
     case 2562: launch_gen_g<256, 2>(h, p, stream); break;
     case 5122: launch_gen_g<512, 2>(h, p, stream); break;
@@ -146,6 +147,12 @@ inline void launch_small_r(const pmenv* h, const StepParams& p, hipStream_t stre
 }
 inline void launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
     if (pmenv_tools::launch_small(h, p, stream)) return;
+    if (h->tiny) {
+        const pmenv_cfg& c = h->cfg;
+        const size_t lds = ((size_t)c.num_assets * c.window * c.features + 8 + (size_t)c.num_assets * (c.features - 1)) * 4;
+        step_tiny_kernel<256, 8><<<(unsigned)c.num_envs, 256, lds, stream>>>(p);
+        return;
+    }
     if (h->cfg.num_assets <= 64) launch_small_r<true>(h, p, stream);
     else launch_small_r<false>(h, p, stream);
 }

@@ -312,6 +312,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const int64_t nwf = (int64_t)c.num_assets * WF;
         h->small_block = nwf <= 256 * 16 ? 256 : nwf <= 512 * 16 ? 512 : nwf <= 1024 * 16 ? 1024 : 0;
         h->small_e = nwf <= 256 * 8 ? 8 : 16;
+        // config 1's 1 x 5 x 50 x 5: 4.1 us (step_small_kernel) -> see DESIGN.md §3
+        h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64;
     }
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
@@ -468,8 +470,11 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     }
     // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 8 (its halo is the two
     // chunks past a workgroup), 16-B granular env windows, at most BLOCK rows per workgroup.
-    // AUTO gives it the windows above 32 MiB; below, the register step's one launch per step
-    // (one workgroup per env) wins
+    // AUTO gives it the windows above 16 MiB that would take the register step: at 512 /
+    // 1,024 / 4,096 / 65,536 x 30 x 50 x 8 in place 17.3 / 29.3 / 80.0 / 1,272.9 us against
+    // 23.7 / 43.0 / 159.3 / 2,791.4, F = 3 at 1,024 envs 21.2 vs 22.8; at 256 x 30 x 50 x 8
+    // (12 MiB) the register step's one launch wins (13.7 vs 14.8), and past its 16,384 floats
+    // the LDS fallback held (16,384 x 64 x 50 x 6: 485.0 vs 546.6) — profiles/ab_r05/gen_r05t.*
     {
         const int F = c.features;
         h->gen_block = 256;
@@ -478,7 +483,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
                     (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= h->gen_block;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
-        h->gen_auto = h->gen_ok && win > (32ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
+        h->gen_auto = h->gen_ok && h->small_block && win > (16ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {
@@ -759,7 +764,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single-launch path: all done in the scalar phase
     if (h->small_block) {
         launch_small(h, p, stream);
-        return check_launch(h, "step_small_kernel");
+        return check_launch(h, h->tiny ? "step_tiny_kernel" : "step_small_kernel");
     }
     if (h->vec && obs16)
         step_advance_lds_kernel<true><<<B, kBlock, h->lds_tile, stream>>>(p);
@@ -935,7 +940,7 @@ const char* pmenv_step_path(const pmenv* h) {
     const char* k1 = h->k1_vec ? "scalar_step_vec_kernel"
                    : h->cfg.num_assets <= 64 ? "scalar_step_reg_kernel" : "scalar_step_kernel";
     if (!h->streaming) {
-        const char* one = h->small_block ? "step_small_kernel" : "step_advance_lds_kernel";
+        const char* one = h->tiny ? "step_tiny_kernel" : h->small_block ? "step_small_kernel" : "step_advance_lds_kernel";
         if (!h->gen) return one;
         static thread_local char gout[320];
         char g2[96];

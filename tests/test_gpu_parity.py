@@ -81,13 +81,16 @@ def test_gpu_every_step_path_matches_reference_goldens(name, impl):
     """The reference's recorded outputs replayed through each advance-step implementation
     forced (AUTO takes one_launch at one env). A path refuses exactly the shapes its
     contract excludes (include/pmenv.h: the one-launch forms need N <= 64 and 16-B
-    granular env windows); those cases check the refusal instead."""
+    granular env windows; two launches take F != 5 through the generic stream); those cases
+    check the refusal instead."""
     from pmenv import TradingEnv
     m = gu.load(name)["meta"]
     N, W, F = m["N"], m["W"], m["F"]
     # the shape rules of pmenv_set_step_path (include/pmenv.h)
     granular = F == 5 and (N * W * F) % 4 == 0
-    misfit = {"two_launch": not granular,
+    # F != 5: the generic stream (2 <= F <= 8, 16-B granular, the workgroup's rows fit)
+    generic = F != 5 and 2 <= F <= 8 and (N * W * F) % 4 == 0 and 4 * 1024 // (W * F) + 2 <= 256
+    misfit = {"two_launch": not (granular or generic),
               "one_launch": not (granular and W >= 2 and N <= 64 and N * W * F * 4 <= 64 * 1024),
               "flat": not (granular and W >= 2 and N <= 64 and N * W * F // 4 >= 148),
               "relay": not (granular and W >= 2 and N <= 512)}[impl]
@@ -499,7 +502,7 @@ def test_gpu_step_impl_selection_rules():
     assert TradingEnv(num_envs=2, num_assets=64, window=47, device=DEV).step_path.count("step_env_kernel") == 2
     assert "step_env_kernel" not in TradingEnv(num_envs=2, num_assets=65, window=4, device=DEV).step_path
     odd = TradingEnv(num_envs=2, num_assets=5, window=50, device=DEV)           # not 16-B granular
-    assert odd.step_path == "step_small_kernel"
+    assert odd.step_path == "step_tiny_kernel"
     for impl in ("one_launch", "two_launch"):
         with pytest.raises(ValueError):
             odd.set_step_impl(impl)
@@ -532,20 +535,23 @@ def test_gpu_vs_oracle_shapes(N, W, F, B):
 
 
 @pytest.mark.parametrize("N,W,F,B,path", [
-    (5, 50, 5, 3, "step_small_kernel"),        # config 1: 250-float rows, 256 x 8
+    (5, 50, 5, 3, "step_tiny_kernel"),         # config 1: 250-float rows, staged in LDS
     (8, 50, 8, 3, "step_small_kernel"),        # 3,200 floats: 256 x 16
     (32, 32, 8, 5, "step_small_kernel"),       # config/base.py with F = 8: 8,192 floats, 512 x 16
     (30, 50, 8, 4, "step_small_kernel"),       # 12,000 floats: 1,024 x 16
-    (3, 7, 5, 9, "step_small_kernel"),         # 105 floats, most lanes idle
-    (7, 10, 3, 6, "step_small_kernel"),
+    (3, 7, 5, 9, "step_tiny_kernel"),          # 105 floats, most lanes idle
+    (7, 10, 3, 6, "step_tiny_kernel"),
+    (64, 8, 4, 5, "step_tiny_kernel"),         # 2,048 floats: the tiny step's largest, 64 assets
+    (65, 6, 5, 3, "step_small_kernel"),        # N > 64: the LDS-scratch scalar step
     (30, 50, 12, 3, "step_advance_lds_kernel"),   # 18,000 floats: past the register step
 ])
 @pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
                          ids=["storage", "chrono", "commission"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 def test_gpu_register_step_vs_oracle(N, W, F, B, path, kw, db):
-    """step_small_kernel (one workgroup per env, the window in VGPRs, any F and alignment)
-    and the LDS fallback past its 16,384 floats, against the oracle past the ring's wrap."""
+    """step_tiny_kernel (env windows <= 2,048 floats, N <= 64: staged in LDS), step_small_kernel
+    (one workgroup per env, the window in VGPRs, any F and alignment) and the LDS fallback past
+    its 16,384 floats, against the oracle past the ring's wrap."""
     from pmenv import TradingEnv
     kw = dict(kw, **({} if F == 5 else {"close_channel": F - 2}))
     assert TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, **kw).step_path == path
@@ -579,17 +585,32 @@ def test_gpu_generic_stream_vs_oracle(N, W, F, B, kw, db):
 
 
 def test_gpu_generic_stream_auto_threshold():
-    """AUTO gives F != 5 windows above 32 MiB the generic stream and keeps the register step
+    """AUTO gives F != 5 windows above 16 MiB the generic stream and keeps the register step
     below; F = 5, F > 8 and non-granular windows never take it."""
     from pmenv import TradingEnv
-    big = TradingEnv(num_envs=1024, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    big = TradingEnv(num_envs=512, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
     assert big.step_path.count("advance_gen_kernel") == 2, big.step_path
-    small = TradingEnv(num_envs=8, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    small = TradingEnv(num_envs=256, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
     assert small.step_path == "step_small_kernel"
     assert "advance_gen_kernel" not in TradingEnv(num_envs=4096, num_assets=30, window=50, device=DEV).step_path
     wide = TradingEnv(num_envs=8, num_assets=30, window=50, features=12, close_channel=10, device=DEV)
     with pytest.raises(ValueError):
         wide.set_step_impl("two_launch")
+
+
+@pytest.mark.parametrize("N,W,F,B,path", [
+    (5, 50, 5, 4096, "step_tiny_kernel"),      # config 1's env, 4,096 of them (odd envs 8-B aligned)
+    (8, 50, 8, 1024, "step_small_kernel"),     # 3,200 floats: 256 x 16
+    (30, 50, 8, 96, "step_small_kernel"),      # 12,000 floats: 1,024 x 16
+    (7, 10, 3, 2048, "step_tiny_kernel"),
+])
+def test_gpu_register_step_many_envs(N, W, F, B, path):
+    """The one-workgroup-per-env steps with thousands of workgroups in flight, in place,
+    against the oracle past the ring's wrap."""
+    from pmenv import TradingEnv
+    kw = {} if F == 5 else {"close_channel": F - 2}
+    assert TradingEnv(num_envs=B, num_assets=N, window=W, features=F, device=DEV, **kw).step_path == path
+    _run_both(kw, B=B, N=N, W=W, T=W + 3, kind="mixed", F=F, seed=B + N * 100 + W * 10 + F)
 
 
 def test_gpu_masked_reset_mid_run():

@@ -55,6 +55,7 @@ struct Tools {
     bool flat_lside = false;
     bool flat_perelem = false;  // PMENV_FLAT_PERELEM: the stream's per-element compose (flat_wg_body)
     int small_abl = -1;         // PMENV_SMALL_ABL: small_stamp_kernel (stamps, + ablation bits), -1 = product
+    bool tiny_off = false;      // PMENV_TINY_OFF: step_small_kernel where the product runs step_tiny_kernel
     uint32_t small_slot = 0;    // its stamp slot, one per launch
 };
 
@@ -362,6 +363,7 @@ void plan(pmenv* h) {
         }
     }
     t->small_abl = knob_int("PMENV_SMALL_ABL", -1);
+    t->tiny_off = knob_int("PMENV_TINY_OFF", 0) != 0;
     if (knob_int("PMENV_GEN_OFF", 0)) h->gen_auto = 0;   // AUTO keeps the register step for F != 5
     if (const char* k = knob("PMENV_GEN_GEOM")) {     // advance_gen_kernel's BLOCK x V: 256x4 | 256x2 | 512x2
         int bk = 0, v = 0;
@@ -509,6 +511,10 @@ void small_stamp(int abl, const StepParams& p, uint32_t slot, hipStream_t stream
 
 bool launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
     Tools* t = tools(h);
+    if (t->tiny_off && h->tiny && t->small_abl < 0) {
+        step_small_kernel<256, 8, true><<<(unsigned)h->cfg.num_envs, 256, 0, stream>>>(p);
+        return true;
+    }
     if (t->small_abl < 0 || h->cfg.num_assets > 64) return false;
     const uint32_t slot = t->small_slot++;
     switch (h->small_block * 100 + h->small_e) {

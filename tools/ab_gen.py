@@ -1,5 +1,5 @@
 """A/B of the F != 5 step: the two-launch generic stream (scalar step + advance_gen_kernel,
-the product's AUTO above 32 MiB, or forced with PMENV_STEP_PATH_TWO_LAUNCH) against the
+the product's AUTO above 16 MiB, or forced with PMENV_STEP_PATH_TWO_LAUNCH) against the
 register step (step_small_kernel: the tools build with PMENV_GEN_OFF=1 keeps AUTO there),
 in ONE process, interleaved, per shape: us per step (HIP events over K steps, median of R),
 env-steps/s and the fraction of the 8 TB/s spec for the step's algorithmic bytes
@@ -101,9 +101,10 @@ def main():
         o["gen_vs_small_pct"] = 100.0 * (o["gen"]["us"] / o["small"]["us"] - 1.0)
         a, b = envs["gen"], envs["small"]
         o["same_steps"] = a.t == b.t
-        o["windows_equal"] = bool(torch.equal(a.window(), b.window()))
-        o["market_equal"] = bool(torch.equal(a.window()[..., :F - 1], b.window()[..., :F - 1]))
-        o["rewards_equal"] = bool(torch.equal(a.rew, b.rew))
+        o["windows_equal"] = bool(torch.equal(a.window().view(torch.int32), b.window().view(torch.int32)))
+        o["market_equal"] = bool(torch.equal(a.window()[..., :F - 1].contiguous().view(torch.int32),
+                                             b.window()[..., :F - 1].contiguous().view(torch.int32)))
+        o["rewards_equal"] = bool(torch.equal(a.rew.view(torch.int32), b.rew.view(torch.int32)))   # bit patterns (NaN too)
         out[key] = o
         print(key, json.dumps(o), file=sys.stderr, flush=True)
         for e in envs.values():
