@@ -1341,8 +1341,17 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
 // counter come into LDS before the barrier, one row per thread (at most BLOCK rows per
 // workgroup: the plan's rule 4 V BLOCK / (W F) + 2 <= BLOCK). An env window is a whole
 // number of chunks, so a chunk spans at most two rows of one env.
-template <int BLOCK, int V, bool OUT>
+// SHV: the shifted source's LDS reads — 4 (F % 4 == 0: one 16-B read), 2 (F % 4 == 2: two
+// 8-B reads), 1 (dword reads). TWO (the product): the two-level compose of flat_wg_body_patch —
+// every chunk takes the common form (the shifted source, or in place its own weight float once
+// the storage-order ring is full), and only chunks holding a row's last day or its ring slot
+// (a divergent branch) read the rows' bar / w' / slot and compose element by element; TWO =
+// false (tools build): every element composed from its row's LDS values. The same values.
+// POL: the window stream's cache policy (the own-chunk loads and the stores), as the F = 5
+// streams: 0 default, 1 nt (windows past the Infinity Cache).
+template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0>
 __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V;
     constexpr int kFm = 7;                                   // bar floats per staged row (F <= 8)
     __shared__ f4 sh4[CPW + 2];
@@ -1355,7 +1364,7 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
     f4 own[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) own[v] = buf_load4<0>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
     // (no halo buffer in place: nothing is read, the two chunks stay 0)
     const uint32_t nh = blockIdx.x + 1 < gridDim.x && (OUT || p.halo) ? min(2u, qtot - c0 - nblk) : 0u;
     const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : (p.halo ? p.halo + (size_t)blockIdx.x * 8 : p.obs);
@@ -1397,29 +1406,62 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
         const uint32_t j0 = 4u * (q - b * per4);
         const uint32_t row = fdiv(j0, p.div_wf);
         const uint32_t kk = j0 - row * (uint32_t)WF;
-        int t = (int)fdiv(kk, p.div_f);
-        int f = (int)kk - t * F;
-        int r = (int)(b * (uint32_t)N + row - g_lo);                 // the element's row in the workgroup
+        const int t0 = (int)fdiv(kk, p.div_f);
+        const int f0 = (int)kk - t0 * F;
+        const int r0 = (int)(b * (uint32_t)N + row - g_lo);          // the chunk's first row in the workgroup
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        float o[4];
+        const float* src = shf + 4 * j + F;                           // floats 4j+F .. 4j+F+3
+        float sh[4];
+        if constexpr (SHV == 4) {
+            const f4 x = *reinterpret_cast<const f4*>(src);
+            sh[0] = x.x; sh[1] = x.y; sh[2] = x.z; sh[3] = x.w;
+        } else if constexpr (SHV == 2) {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 x0 = *reinterpret_cast<const f2*>(src), x1 = *reinterpret_cast<const f2*>(src + 2);
+            sh[0] = x0.x; sh[1] = x0.y; sh[2] = x1.x; sh[3] = x1.y;
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int slot = sh_sl[r];
-            const float wp = sh_wp[r];
-            const float bf = sh_bar[r * kFm + min(f, kFm - 1)];
-            const float sh = shf[4 * j + e + F];
-            const bool last = t == W - 1;
-            const float wv = slot < 0 ? (last ? wp : sh) : (t == slot ? wp : un[e]);
-            o[e] = f == Fm ? wv : (last ? bf : sh);
-            // the next element: channel, day, row
-            const bool fw = f == Fm;
-            f = fw ? 0 : f + 1;
-            t += fw ? 1 : 0;
-            const bool tw = t == W;
-            t = tw ? 0 : t;
-            r += tw ? 1 : 0;
+            for (int e = 0; e < 4; ++e) sh[e] = src[e];
         }
-        buf_store4<0>(rd, (uint32_t)j * 16u, f4{o[0], o[1], o[2], o[3]});
+        float o[4];
+        bool patch = true;
+        int sl0 = 0;
+        if constexpr (TWO) {
+            sl0 = sh_sl[r0];
+            int f = f0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[e] = sl0 >= 0 && f == Fm ? un[e] : sh[e];
+                f = f == Fm ? 0 : f + 1;
+            }
+            // a last day (every chunk that reaches the row's end holds one) or the ring slot
+            patch = (int)kk + 3 >= WF - F || (sl0 >= 0 && (uint32_t)(sl0 * F + Fm - (int)kk) <= 3u);
+        }
+        if (patch) {
+            const int r1 = min(r0 + 1, BLOCK - 1);
+            if constexpr (!TWO) sl0 = sh_sl[r0];
+            const int sl1 = sh_sl[r1];
+            const float wp0 = sh_wp[r0], wp1 = sh_wp[r1];
+            int t = t0, f = f0;
+            bool nx = false;                                          // past the first row's end
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int slot = nx ? sl1 : sl0;
+                const float wp = nx ? wp1 : wp0;
+                const bool last = t == W - 1;
+                const float bf = last && f < Fm ? sh_bar[(r0 + (nx ? 1 : 0)) * kFm + f] : 0.0f;
+                const float wv = slot < 0 ? (last ? wp : sh[e]) : (t == slot ? wp : un[e]);
+                o[e] = f == Fm ? wv : (last ? bf : sh[e]);
+                // the next element: channel, day, row
+                const bool fw = f == Fm;
+                f = fw ? 0 : f + 1;
+                t += fw ? 1 : 0;
+                const bool tw = t == W;
+                t = tw ? 0 : t;
+                nx = nx || tw;
+            }
+        }
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, f4{o[0], o[1], o[2], o[3]});
     }
 }
 

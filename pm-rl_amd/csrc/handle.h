@@ -262,6 +262,7 @@ bool launch_scalar(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t s
 bool launch_advance(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_one(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_small(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
+bool launch_gen(const pmenv* h, const pmenv_dev::StepParams& p, hipStream_t stream);
 bool launch_fused(const pmenv* h, const pmenv_dev::StepParams& p, int fuse_bit, uint32_t phases, hipStream_t stream);
 bool launch_relay(const pmenv* h, const pmenv_dev::StepParams& p, const pmenv_dev::RelayParams& r, unsigned grid,
                   hipStream_t stream);

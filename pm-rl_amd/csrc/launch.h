@@ -116,15 +116,29 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- the generic stream (F != 5)
+template <int BLOCK, int V, int SHV>
+inline void launch_gen_s(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
+    // nt past the Infinity Cache: the F = 5 streams' rule (flat_ip_pol / flat_pol, pmenv.hip)
+    if (p.obs_out == p.obs) {
+        if (h->flat_ip_pol) advance_gen_kernel<BLOCK, V, false, SHV, true, 1><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+        else advance_gen_kernel<BLOCK, V, false, SHV><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+    } else {
+        if (h->flat_pol) advance_gen_kernel<BLOCK, V, true, SHV, true, 1><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+        else advance_gen_kernel<BLOCK, V, true, SHV><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+    }
+}
 template <int BLOCK, int V>
 inline void launch_gen_g(const pmenv* h, const StepParams& p, hipStream_t stream) {
-    const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
-    if (p.obs_out == p.obs) advance_gen_kernel<BLOCK, V, false><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
-    else advance_gen_kernel<BLOCK, V, true><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+    const int fm4 = h->cfg.features % 4;   // the shifted source's LDS reads: 16 B (F = 4, 8), 8 B (F = 2, 6), dwords
+    if (fm4 == 0) launch_gen_s<BLOCK, V, 4>(h, p, stream);
+    else if (fm4 == 2) launch_gen_s<BLOCK, V, 2>(h, p, stream);
+    else launch_gen_s<BLOCK, V, 1>(h, p, stream);
 }
 inline void launch_gen(const pmenv* h, StepParams p, hipStream_t stream) {
     p.div_units = make_fastdiv(h->per4);
     p.halo = h->halo;                      // in place: the two chunks past each workgroup (the scalar step's copy)
+    if (pmenv_tools::launch_gen(h, p, stream)) return;
     switch (h->gen_block * 10 + h->gen_v) {
     case 2562: launch_gen_g<256, 2>(h, p, stream); break;
     case 5122: launch_gen_g<512, 2>(h, p, stream); break;

@@ -478,10 +478,15 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     {
         const int F = c.features;
         h->gen_block = 256;
-        h->gen_v = 4;
-        const int64_t cpw = (int64_t)h->gen_block * h->gen_v;
+        // 256 x 2 chunks per workgroup, 256 x 4 for F = 8 past the Infinity Cache (A/B with nt
+        // streams, profiles/ab_r05/gen_geom_*_r05x.*: 65,536 / 16,384 x 30 x 50 x 8 in place
+        // 1,201.7 / 310.3 us at 256 x 4 against 1,252.2 / 320.8; 4,096 x 30 x 50 x 8 82.6 vs
+        // 79.8, F = 3 at 65,536 / 16,384 / 4,096 envs 681.6 / 180.2 / 54.4 vs 654.5 / 169.3 /
+        // 48.5, F = 4 at 65,536 786.4 vs 773.2; 512 x 2 lost 10-30 % everywhere)
+        const int64_t cpw = (int64_t)h->gen_block * 4;      // the shape rule at the larger tile
         h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
                     (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= h->gen_block;
+        h->gen_v = F == 8 && win > (256ll << 20) ? 4 : 2;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         h->gen_auto = h->gen_ok && h->small_block && win > (16ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }
@@ -1361,6 +1366,7 @@ __attribute__((weak, noinline)) bool launch_scalar(const pmenv*, const StepParam
 __attribute__((weak, noinline)) bool launch_advance(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_one(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_small(const pmenv*, const StepParams&, hipStream_t) { return false; }
+__attribute__((weak, noinline)) bool launch_gen(const pmenv*, const StepParams&, hipStream_t) { return false; }
 __attribute__((weak, noinline)) bool launch_fused(const pmenv*, const StepParams&, int, uint32_t, hipStream_t) {
     return false;
 }

@@ -56,6 +56,8 @@ struct Tools {
     bool flat_perelem = false;  // PMENV_FLAT_PERELEM: the stream's per-element compose (flat_wg_body)
     int small_abl = -1;         // PMENV_SMALL_ABL: small_stamp_kernel (stamps, + ablation bits), -1 = product
     bool tiny_off = false;      // PMENV_TINY_OFF: step_small_kernel where the product runs step_tiny_kernel
+    bool gen_perelem = false;   // PMENV_GEN_PERELEM: advance_gen_kernel's per-element compose, dword reads
+    bool gen_pol0 = false;      // PMENV_GEN_POL0: advance_gen_kernel with the default cache policy everywhere
     uint32_t small_slot = 0;    // its stamp slot, one per launch
 };
 
@@ -364,6 +366,8 @@ void plan(pmenv* h) {
     }
     t->small_abl = knob_int("PMENV_SMALL_ABL", -1);
     t->tiny_off = knob_int("PMENV_TINY_OFF", 0) != 0;
+    t->gen_perelem = knob_int("PMENV_GEN_PERELEM", 0) != 0;
+    t->gen_pol0 = knob_int("PMENV_GEN_POL0", 0) != 0;
     if (knob_int("PMENV_GEN_OFF", 0)) h->gen_auto = 0;   // AUTO keeps the register step for F != 5
     if (const char* k = knob("PMENV_GEN_GEOM")) {     // advance_gen_kernel's BLOCK x V: 256x4 | 256x2 | 512x2
         int bk = 0, v = 0;
@@ -521,6 +525,24 @@ bool launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
     case 25608: small_stamp<256, 8>(t->small_abl, p, slot, stream); break;
     default: return false;
     }
+    return true;
+}
+
+bool launch_gen(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const unsigned grid = (unsigned)((h->gen_qtot + 1023) / 1024);
+    if (h->gen_block != 256 || h->gen_v != 4) return false;
+    if (tools(h)->gen_pol0) {
+        const int fm4 = h->cfg.features % 4;
+        const bool ip = p.obs_out == p.obs;
+        if (fm4 == 0 && ip) advance_gen_kernel<256, 4, false, 4><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+        else if (fm4 == 0) advance_gen_kernel<256, 4, true, 4><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+        else if (ip) advance_gen_kernel<256, 4, false, 1><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+        else advance_gen_kernel<256, 4, true, 1><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+        return true;
+    }
+    if (!tools(h)->gen_perelem) return false;
+    if (p.obs_out == p.obs) advance_gen_kernel<256, 4, false, 1, false><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+    else advance_gen_kernel<256, 4, true, 1, false><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
     return true;
 }
 

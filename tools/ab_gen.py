@@ -4,6 +4,7 @@ register step (step_small_kernel: the tools build with PMENV_GEN_OFF=1 keeps AUT
 in ONE process, interleaved, per shape: us per step (HIP events over K steps, median of R),
 env-steps/s and the fraction of the 8 TB/s spec for the step's algorithmic bytes
 (tools/bench_shapes.py's count), and whether the two give the same windows and rewards.
+With PMENV_GEN_PERELEM=1 the other leg is advance_gen_kernel's per-element compose (tools).
 
     PMENV_GEN_OFF=1 python tools/ab_gen.py      # prints one JSON object
 """
@@ -76,13 +77,19 @@ class Env:
 
 
 def main():
-    assert os.environ.get("PMENV_GEN_OFF") == "1", "run with PMENV_GEN_OFF=1 (read by the tools build only)"
+    perelem = os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
+    assert perelem or os.environ.get("PMENV_GEN_OFF") == "1", \
+        "run with PMENV_GEN_OFF=1 (against the register step) or PMENV_GEN_PERELEM=1 (against the per-element compose)"
     torch.cuda.set_device(ab.DEV)
     libs = {"gen": ab.load(ab.LIBS["r05"]), "small": ab.load(os.path.join(ROOT, "tools", "libpmenv_ab.so"))}
-    out = {"K": K, "R": R}
+    other = ("advance_gen_kernel, default cache policy (tools)" if os.environ.get("PMENV_GEN_POL0") == "1" else
+             "advance_gen_kernel per-element (tools)" if perelem else "register step (tools)")
+    out = {"K": K, "R": R, "other": other}
     for (B, N, W, F, ip) in SHAPES:
+        if perelem and (B, N, W, F) == (16384, 64, 50, 6):
+            continue
         key = f"{B}x{N}x{W}x{F}{'_ip' if ip else '_db'}"
-        envs = {"gen": Env(libs["gen"], B, N, W, F, ip, True), "small": Env(libs["small"], B, N, W, F, ip, False)}
+        envs = {"gen": Env(libs["gen"], B, N, W, F, ip, True), "small": Env(libs["small"], B, N, W, F, ip, perelem)}
         paths = {n: e.lib.pmenv_step_path(e.h).decode() for n, e in envs.items()}
         res = {n: [] for n in envs}
         for e in envs.values():
