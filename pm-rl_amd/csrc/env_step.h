@@ -1350,14 +1350,17 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
 // POL: the window stream's cache policy (the own-chunk loads and the stores), as the F = 5
 // streams: 0 default, 1 nt (windows past the Infinity Cache).
 template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0>
-__global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot) {
+__global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot, uint32_t rows) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V;
     constexpr int kFm = 7;                                   // bar floats per staged row (F <= 8)
     __shared__ f4 sh4[CPW + 2];
-    __shared__ float sh_bar[BLOCK * kFm];
-    __shared__ float sh_wp[BLOCK];
-    __shared__ int32_t sh_sl[BLOCK];                         // the row's ring slot, or -1 while it shifts
+    // the rows' side data, sized by the plan's bound on rows per workgroup (4 CPW / (W F) + 2:
+    // a dozen at W F = 400) rather than BLOCK — more workgroups per CU, more bytes in flight
+    extern __shared__ float gside[];
+    float* sh_wp = gside;                                    // [rows] w'
+    int32_t* sh_sl = reinterpret_cast<int32_t*>(gside + rows);   // [rows] ring slot, or -1 while it shifts
+    float* sh_bar = gside + 2 * rows;                        // [rows][kFm] bar
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t c0 = blockIdx.x * CPW;
     const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
@@ -1438,7 +1441,7 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
             patch = (int)kk + 3 >= WF - F || (sl0 >= 0 && (uint32_t)(sl0 * F + Fm - (int)kk) <= 3u);
         }
         if (patch) {
-            const int r1 = min(r0 + 1, BLOCK - 1);
+            const int r1 = min(r0 + 1, (int)rows - 1);
             if constexpr (!TWO) sl0 = sh_sl[r0];
             const int sl1 = sh_sl[r1];
             const float wp0 = sh_wp[r0], wp1 = sh_wp[r1];

@@ -116,16 +116,22 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- the generic stream (F != 5)
+// rows of the [B N, W F] window a workgroup of cpw chunks can touch (the plan keeps it <= BLOCK)
+inline uint32_t gen_rows(const pmenv* h, int cpw) {
+    return (uint32_t)(4 * (int64_t)cpw / ((int64_t)h->cfg.window * h->cfg.features) + 2);
+}
 template <int BLOCK, int V, int SHV>
 inline void launch_gen_s(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
+    const uint32_t rows = gen_rows(h, BLOCK * V);
+    const size_t lds = (size_t)rows * (2 + 7) * 4;
     // nt past the Infinity Cache: the F = 5 streams' rule (flat_ip_pol / flat_pol, pmenv.hip)
     if (p.obs_out == p.obs) {
-        if (h->flat_ip_pol) advance_gen_kernel<BLOCK, V, false, SHV, true, 1><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
-        else advance_gen_kernel<BLOCK, V, false, SHV><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+        if (h->flat_ip_pol) advance_gen_kernel<BLOCK, V, false, SHV, true, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else advance_gen_kernel<BLOCK, V, false, SHV><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
     } else {
-        if (h->flat_pol) advance_gen_kernel<BLOCK, V, true, SHV, true, 1><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
-        else advance_gen_kernel<BLOCK, V, true, SHV><<<grid, BLOCK, 0, stream>>>(p, h->gen_qtot);
+        if (h->flat_pol) advance_gen_kernel<BLOCK, V, true, SHV, true, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else advance_gen_kernel<BLOCK, V, true, SHV><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
     }
 }
 template <int BLOCK, int V>

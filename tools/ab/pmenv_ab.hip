@@ -530,19 +530,21 @@ bool launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
 
 bool launch_gen(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const unsigned grid = (unsigned)((h->gen_qtot + 1023) / 1024);
+    const uint32_t rows = gen_rows(h, 1024);
+    const size_t lds = (size_t)rows * 9 * 4;
     if (h->gen_block != 256 || h->gen_v != 4) return false;
     if (tools(h)->gen_pol0) {
         const int fm4 = h->cfg.features % 4;
         const bool ip = p.obs_out == p.obs;
-        if (fm4 == 0 && ip) advance_gen_kernel<256, 4, false, 4><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
-        else if (fm4 == 0) advance_gen_kernel<256, 4, true, 4><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
-        else if (ip) advance_gen_kernel<256, 4, false, 1><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
-        else advance_gen_kernel<256, 4, true, 1><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+        if (fm4 == 0 && ip) advance_gen_kernel<256, 4, false, 4><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+        else if (fm4 == 0) advance_gen_kernel<256, 4, true, 4><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+        else if (ip) advance_gen_kernel<256, 4, false, 1><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+        else advance_gen_kernel<256, 4, true, 1><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
         return true;
     }
     if (!tools(h)->gen_perelem) return false;
-    if (p.obs_out == p.obs) advance_gen_kernel<256, 4, false, 1, false><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
-    else advance_gen_kernel<256, 4, true, 1, false><<<grid, 256, 0, stream>>>(p, h->gen_qtot);
+    if (p.obs_out == p.obs) advance_gen_kernel<256, 4, false, 1, false><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+    else advance_gen_kernel<256, 4, true, 1, false><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
     return true;
 }
 

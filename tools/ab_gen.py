@@ -4,7 +4,8 @@ register step (step_small_kernel: the tools build with PMENV_GEN_OFF=1 keeps AUT
 in ONE process, interleaved, per shape: us per step (HIP events over K steps, median of R),
 env-steps/s and the fraction of the 8 TB/s spec for the step's algorithmic bytes
 (tools/bench_shapes.py's count), and whether the two give the same windows and rewards.
-With PMENV_GEN_PERELEM=1 the other leg is advance_gen_kernel's per-element compose (tools).
+With PMENV_GEN_PERELEM=1 the other leg is advance_gen_kernel's per-element compose (tools);
+with AB_GEN_BASE=<path> another product build (e.g. an earlier commit's), forced alike.
 
     PMENV_GEN_OFF=1 python tools/ab_gen.py      # prints one JSON object
 """
@@ -77,12 +78,15 @@ class Env:
 
 
 def main():
-    perelem = os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
+    base = os.environ.get("AB_GEN_BASE")            # another product build, forced to two launches too
+    perelem = base is not None or os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
     assert perelem or os.environ.get("PMENV_GEN_OFF") == "1", \
         "run with PMENV_GEN_OFF=1 (against the register step) or PMENV_GEN_PERELEM=1 (against the per-element compose)"
     torch.cuda.set_device(ab.DEV)
-    libs = {"gen": ab.load(ab.LIBS["r05"]), "small": ab.load(os.path.join(ROOT, "tools", "libpmenv_ab.so"))}
-    other = ("advance_gen_kernel, default cache policy (tools)" if os.environ.get("PMENV_GEN_POL0") == "1" else
+    libs = {"gen": ab.load(ab.LIBS["r05"]),
+            "small": ab.load(os.path.join(ROOT, base) if base else os.path.join(ROOT, "tools", "libpmenv_ab.so"))}
+    other = (f"{base} (two launches)" if base else
+             "advance_gen_kernel, default cache policy (tools)" if os.environ.get("PMENV_GEN_POL0") == "1" else
              "advance_gen_kernel per-element (tools)" if perelem else "register step (tools)")
     out = {"K": K, "R": R, "other": other}
     for (B, N, W, F, ip) in SHAPES:
