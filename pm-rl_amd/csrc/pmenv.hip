@@ -478,15 +478,16 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     {
         const int F = c.features;
         h->gen_block = 256;
-        // 256 x 2 chunks per workgroup, 256 x 4 for F = 8 past the Infinity Cache (A/B with nt
-        // streams, profiles/ab_r05/gen_geom_*_r05x.*: 65,536 / 16,384 x 30 x 50 x 8 in place
-        // 1,201.7 / 310.3 us at 256 x 4 against 1,252.2 / 320.8; 4,096 x 30 x 50 x 8 82.6 vs
-        // 79.8, F = 3 at 65,536 / 16,384 / 4,096 envs 681.6 / 180.2 / 54.4 vs 654.5 / 169.3 /
-        // 48.5, F = 4 at 65,536 786.4 vs 773.2; 512 x 2 lost 10-30 % everywhere)
+        // 256 x 4 chunks per workgroup for windows past 128 MiB, 256 x 2 below (with the side
+        // data in dynamic LDS, profiles/ab_r05/gen_geom4_dynlds_r05q.*, in place, 256 x 4 / 256 x 2:
+        // F = 3 at 65,536 / 16,384 / 4,096 envs 582.4 / 157.8 / 53.5 against 667.5 / 173.2 /
+        // 49.5 us, F = 4 at 65,536 678.4 / 789.9, F = 8 at 4,096 / 2,048 / 256 77.2 / 47.5 / 15.7
+        // against 81.2 / 46.9 / 14.1, at 65,536 1,105.2 / 1,105.1; 512 x 2 lost 10-30 %
+        // everywhere, gen_geom_*_r05x.*)
         const int64_t cpw = (int64_t)h->gen_block * 4;      // the shape rule at the larger tile
         h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
                     (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= h->gen_block;
-        h->gen_v = F == 8 && win > (256ll << 20) ? 4 : 2;
+        h->gen_v = win > (128ll << 20) ? 4 : 2;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         h->gen_auto = h->gen_ok && h->small_block && win > (16ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }

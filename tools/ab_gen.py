@@ -79,13 +79,15 @@ class Env:
 
 def main():
     base = os.environ.get("AB_GEN_BASE")            # another product build, forced to two launches too
-    perelem = base is not None or os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
+    perelem = (base is not None or os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
+               or os.environ.get("AB_GEN_FORCE") == "1")     # the tools leg forced to two launches (e.g. PMENV_GEN_GEOM)
     assert perelem or os.environ.get("PMENV_GEN_OFF") == "1", \
         "run with PMENV_GEN_OFF=1 (against the register step) or PMENV_GEN_PERELEM=1 (against the per-element compose)"
     torch.cuda.set_device(ab.DEV)
     libs = {"gen": ab.load(ab.LIBS["r05"]),
             "small": ab.load(os.path.join(ROOT, base) if base else os.path.join(ROOT, "tools", "libpmenv_ab.so"))}
     other = (f"{base} (two launches)" if base else
+             f"tools build, PMENV_GEN_GEOM={os.environ.get('PMENV_GEN_GEOM')}" if os.environ.get("AB_GEN_FORCE") == "1" else
              "advance_gen_kernel, default cache policy (tools)" if os.environ.get("PMENV_GEN_POL0") == "1" else
              "advance_gen_kernel per-element (tools)" if perelem else "register step (tools)")
     out = {"K": K, "R": R, "other": other}

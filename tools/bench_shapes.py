@@ -25,7 +25,7 @@ R = int(os.environ.get("SHAPES_R", "5"))
 PEAK = 8.0e12
 # (name, B, N, W, F, in place)
 SHAPES = [("config1_1x5x50x5_ip", 1, 5, 50, 5, True), ("config1_1x5x50x5_db", 1, 5, 50, 5, False),
-          ("base_1x32x32x8_ip", 1, 32, 32, 8, True), ("feat3_4096x30x50x3_ip", 4096, 30, 50, 3, True),
+          ("base_1x32x32x8_ip", 1, 32, 32, 8, True), ("feat3_4096x30x50x3_ip", 4096, 30, 50, 3, True), ("feat3_65536x30x50x3_ip", 65536, 30, 50, 3, True),
           ("feat8_4096x30x50x8_ip", 4096, 30, 50, 8, True), ("feat8_65536x30x50x8_ip", 65536, 30, 50, 8, True),
           ("feat8_65536x30x50x8_db", 65536, 30, 50, 8, False), ("odd5_65536x5x50x5_ip", 65536, 5, 50, 5, True)]
 
