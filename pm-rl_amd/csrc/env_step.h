@@ -87,8 +87,9 @@ __device__ __forceinline__ void gather_inputs(const StepParams& p, int b, Scratc
     }
 }
 
-__device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scratch& s, int32_t k,
-                                               double v_prev) {
+// returns the portfolio value after the step (every lane)
+__device__ __forceinline__ double scalar_compute(const StepParams& p, int b, Scratch& s, int32_t k,
+                                                 double v_prev) {
     const int lane = threadIdx.x & 63;
     const int N = p.N, W = p.W;
 
@@ -210,6 +211,7 @@ __device__ __forceinline__ void scalar_compute(const StepParams& p, int b, Scrat
         s.ints[1] = slot;
         s.ints[2] = k + 1;
     }
+    return value;
 }
 
 // ---------------------------------------------------------------- K1: scalar step
@@ -1826,38 +1828,65 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
     const int tid = threadIdx.x;
     const int N = p.N, W = p.W, F = p.F;
     Scratch s = carve(lds, 0, N, F);
+    // Everything the step reads that does not depend on its own results is issued up front,
+    // none waiting for another: the counter and value as lane values (a load the compiler sees
+    // as uniform is moved to an SGPR at once, and the wait for it would hold the rest back by a
+    // round trip), the window's last closes (host I/O: over PCIe) and the ring rows the channel
+    // is rebuilt from — every slot but the one this step writes (weight_buffer.py:32-44).
+    uint32_t z = 0u;
+    asm volatile("" : "+v"(z));
+    const int32_t k = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.k + b, 4u), z, 0, 0);
+    const double v_prev = buf_load_f64(make_rsrc(p.value + b, 8u), z);
+    const bool out = HOST ? io.chan != nullptr : p.obs != nullptr;
+    const float cl = HOST && out && tid < N ? io.close_in[(size_t)b * N + tid] : 0.0f;
+    constexpr int PF = 4;                          // channel floats per thread prefetched (N W <= 1,024)
+    const int32_t k1 = k + 1;                      // updates since reset, after this step
+    const int slot = ring_slot(k, W), idx = ring_slot(k1, W);
+    const bool full = (int64_t)k1 >= W - 1;
+    const float* ringb = p.ring + (size_t)b * W * N;
+    auto ring_src = [&](int i, int& n) {           // the ring slot feeding channel float i, or -1 (zero padding)
+        n = (int)fdiv((uint32_t)i, p.div_w);
+        const int t = i - n * W;
+        if (!full) return t < W - idx ? -1 : t - (W - idx);
+        return p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
+    };
+    float pv[PF];
+#pragma unroll
+    for (int e = 0; e < PF; ++e) {
+        const int i = tid + kBlock * e;
+        int n = 0;
+        const int rs = out && i < N * W ? ring_src(i, n) : -1;
+        pv[e] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
+    }
     if (tid < 64) {
-        const int32_t k = p.k[b];
-        const double v_prev = p.value[b];
         gather_inputs(p, b, s, k);
-        scalar_compute(p, b, s, k, v_prev);
-        // the lane that wrote the value (scalar_compute's lane 0) hands it out
-        if (HOST && tid == 0) io.value_out[b] = p.value[b];
+        const double value = scalar_compute(p, b, s, k, v_prev);
+        if (HOST && tid == 0) io.value_out[b] = value;          // the value scalar_compute stored
     }
     __syncthreads();
-    if (HOST ? !io.chan : !p.obs) {
+    if (!out) {
         if (HOST) hostio_done(io, b);
         return;
     }
-    const int slot = s.ints[1];
-    const int32_t k1 = s.ints[2];                 // updates since reset, after this step
-    const int idx = ring_slot(k1, W);
-    const bool full = (int64_t)k1 >= W - 1;
-    const float* ringb = p.ring + (size_t)b * W * N;
     float* obs = HOST ? io.chan + (size_t)b * N * W : p.obs + (size_t)b * N * W * F;
     const int fs = HOST ? 1 : F, fo = HOST ? 0 : F - 1;
-    for (int i = tid; i < N * W; i += kBlock) {
-        const int n = (int)fdiv((uint32_t)i, p.div_w);
-        const int t = i - n * W;
-        int rs;  // ring slot feeding position t, or -1 for zero padding (weight_buffer.py:38-44)
-        if (!full) rs = t < W - idx ? -1 : t - (W - idx);
-        else rs = p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
-        float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
-        obs[((size_t)n * W + t) * fs + fo] = v;
+#pragma unroll
+    for (int e = 0; e < PF; ++e) {
+        const int i = tid + kBlock * e;
+        if (i < N * W) {
+            int n;
+            const int rs = ring_src(i, n);
+            obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : pv[e]);
+        }
+    }
+    for (int i = tid + kBlock * PF; i < N * W; i += kBlock) {   // windows past 1,024 channel floats
+        int n;
+        const int rs = ring_src(i, n);
+        obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
     }
     // keep the advance-mode close in step with the caller's window
     for (int n = tid; n < N; n += kBlock)
-        p.last_close[(size_t)b * N + n] = HOST ? io.close_in[(size_t)b * N + n]
+        p.last_close[(size_t)b * N + n] = HOST ? (n == tid ? cl : io.close_in[(size_t)b * N + n])
                                                : obs[((size_t)n * W + (W - 1)) * F + p.close_ch];
     if (HOST) hostio_done(io, b);
 }
