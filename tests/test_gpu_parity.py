@@ -893,6 +893,48 @@ def test_gpu_resident_series_equals_bar_batch(impl):
     assert ea.nonfinite_count() == 1
 
 
+@pytest.mark.parametrize("N,W,F,B,impl,path", [
+    (30, 50, 8, 512, "auto", "advance_gen_kernel"),     # 24.6 MB: AUTO's generic stream
+    (8, 10, 3, 33, "two_launch", "advance_gen_kernel"),
+    (30, 50, 8, 4, "auto", "step_small_kernel"),
+    (5, 50, 5, 9, "auto", "step_tiny_kernel"),          # config 1's env
+    (8, 10, 3, 600, "auto", "step_tiny_kernel"),
+])
+def test_gpu_resident_series_any_F_equals_bar_batch(N, W, F, B, impl, path):
+    """The resident-series data path (env b reads series[day[b]], the day read on the device)
+    through the F != 5 and small-window kernels == stepping with the gathered bar batch, bit for
+    bit, both in place; a day outside the series gives NaN bars and is reported."""
+    from pmenv import TradingEnv, MarketSeries
+    rng = np.random.default_rng(N + W + F)
+    T, S = 3 * W + 40, 2 * W + 3
+    closes = 100 * np.exp(np.cumsum(0.01 * rng.standard_normal((T, N)), axis=0))
+    chans = [closes * np.exp(0.002 * rng.standard_normal((T, N))) for _ in range(F - 2)] + [closes]
+    bars = np.stack(chans, -1).astype(np.float32)                       # [T, N, F - 1], close last
+    m = MarketSeries(bars, device=DEV)
+    start = m.random_starts(B, W, S, generator=torch.Generator().manual_seed(F))
+    obs_a = m.initial_window(start, W)
+    obs_b = obs_a.clone()
+    kw = dict(num_envs=B, num_assets=N, window=W, features=F, close_channel=F - 2, device=DEV, step_impl=impl)
+    ea, eb = TradingEnv(**kw), TradingEnv(**kw)
+    assert path in ea.step_path.split(" | ")[-1], ea.step_path
+    ea.reset(obs_a)
+    eb.reset(obs_b)
+    act = torch.softmax(torch.randn(S, B, N, device=DEV), -1)
+    for t in range(S):
+        day = start + W + t
+        ra, _ = ea.step(act[t], obs_a, series=m, day=day)
+        rb, _ = eb.step(act[t], obs_b, bar=m.bars[day.long()].contiguous())
+        assert torch.equal(ra.view(torch.int32), rb.view(torch.int32)), f"step {t}"
+    assert torch.equal(obs_a.view(torch.int32), obs_b.view(torch.int32)) and torch.equal(ea.value, eb.value)
+    bad = start + W + S                   # the day after the horizon: past the series for the latest starts
+    bad[B // 2] = T + 5
+    ea.step(act[0], obs_a, series=m, day=bad)
+    outside = (bad >= T).cpu().numpy()
+    assert ea.nonfinite_count() == int(outside.sum())
+    nan_rows = torch.isnan(obs_a[:, :, W - 1, :F - 1]).all(-1).all(-1).cpu().numpy()
+    assert np.array_equal(nan_rows, outside)
+
+
 @pytest.mark.parametrize("T,N,W,B,H,S", [
     (200, 30, 12, 33, 40, 64),     # F = 5 vector staging (4 pairs per thread), persistent gather
     (300, 30, 50, 17, 80, 64),     # F = 5, 8 pairs per thread (BASELINE shape)
