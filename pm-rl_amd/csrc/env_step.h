@@ -1698,7 +1698,7 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
 // wave, and no f64 tail after the window's stores. Same values, element by element.
 template <int BLOCK, int E>
 __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
-    static_assert(E % 4 == 0 && E <= 8, "16-B chunks, at most two per thread");
+    static_assert(E % 4 == 0 && E <= 8 && BLOCK >= 256, "16-B chunks, at most two per thread; 2 BLOCK >= 64 x 7 bar floats");
     constexpr int Q = E / 4;                               // chunks per thread
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [NWF + 8] window | [N (F-1)] bar
     __shared__ float sh_wp[64];
@@ -1723,7 +1723,9 @@ __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
     }
     const uint32_t jt = nq * 4u + (uint32_t)tid;            // the block's last NWF % 4 floats
     const float tl = buf_load1(rs_in, jt < NWF ? jt * 4u : kOut);
-    const float bv = buf_load1(rs_bar, (uint32_t)tid < nbar ? (uint32_t)tid * 4u : kOut);
+    // the bar: N (F - 1) <= 64 x 7 floats, two per thread (BLOCK >= 256)
+    const float bv0 = buf_load1(rs_bar, (uint32_t)tid < nbar ? (uint32_t)tid * 4u : kOut);
+    const float bv1 = buf_load1(rs_bar, (uint32_t)(tid + BLOCK) < nbar ? (uint32_t)(tid + BLOCK) * 4u : kOut);
     float* lbar = lds + NWF + 8;
     const int32_t k0 = sin.k;
     ScalarMid mid;
@@ -1741,7 +1743,8 @@ __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
         if (c < nq) reinterpret_cast<f4*>(lds)[c] = ch[q];
     }
     if (jt < NWF + 8u) lds[jt] = jt < NWF ? tl : 0.0f;      // and 8 floats past the block (read only by last days)
-    if ((uint32_t)tid < nbar) lbar[tid] = barg ? bv : __int_as_float(0x7fc00000);
+    if ((uint32_t)tid < nbar) lbar[tid] = barg ? bv0 : __int_as_float(0x7fc00000);
+    if ((uint32_t)(tid + BLOCK) < nbar) lbar[tid + BLOCK] = barg ? bv1 : __int_as_float(0x7fc00000);
     // every load of every wave has returned before any store: the counter the waves past the
     // first read (for the ring slot) is one wave 0 rewrites after the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -542,6 +542,7 @@ def test_gpu_vs_oracle_shapes(N, W, F, B):
     (3, 7, 5, 9, "step_tiny_kernel"),          # 105 floats, most lanes idle
     (7, 10, 3, 6, "step_tiny_kernel"),
     (64, 8, 4, 5, "step_tiny_kernel"),         # 2,048 floats: the tiny step's largest, 64 assets
+    (64, 4, 8, 3, "step_tiny_kernel"),         # 448 bar floats: more than one per thread
     (65, 6, 5, 3, "step_small_kernel"),        # N > 64: the LDS-scratch scalar step
     (30, 50, 12, 3, "step_advance_lds_kernel"),   # 18,000 floats: past the register step
 ])
