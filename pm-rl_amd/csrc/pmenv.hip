@@ -490,6 +490,11 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->gen_v = win > (128ll << 20) ? 4 : 2;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         h->gen_auto = h->gen_ok && h->small_block && win > (16ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
+        // past 16,384 floats per env the LDS fallback is the alternative: the generic stream wins
+        // in place at F = 8 (8,192 x 100 x 50 x 8 461.6 vs 529.3 us, 4,096 x 64 x 50 x 8 159.8 vs
+        // 171.7) and loses or ties elsewhere (2,048 x 128 x 50 x 4 101.0 vs 74.2; 16,384 x 64 x 50
+        // x 6 in place 475.7 vs 485.7, double-buffered 472.9 vs 459.9) — ab_r05/gen_wide_r05w2.*
+        if (h->gen_ok && !h->small_block && F == 8 && win > (16ll << 20)) h->gen_auto = PMENV_FUSE_INPLACE;
     }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {

@@ -568,6 +568,7 @@ def test_gpu_register_step_vs_oracle(N, W, F, B, path, kw, db):
     (11, 4, 7, 5),        # W = 4: most chunks span two rows' days
     (64, 16, 8, 3),
     (65, 16, 4, 2),       # N > 64: the packed scalar step
+    (100, 10, 8, 3),      # N = 100: the packed scalar step, two-envs-per-tile seams
 ])
 @pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
                          ids=["storage", "chrono", "commission"])
@@ -597,6 +598,11 @@ def test_gpu_generic_stream_auto_threshold():
     wide = TradingEnv(num_envs=8, num_assets=30, window=50, features=12, close_channel=10, device=DEV)
     with pytest.raises(ValueError):
         wide.set_step_impl("two_launch")
+    # past the register step's 16,384 floats per env: in place only, F = 8 only
+    w8 = TradingEnv(num_envs=256, num_assets=100, window=50, features=8, close_channel=6, device=DEV)
+    assert w8.step_path == "step_advance_lds_kernel (obs_out) | scalar_step_vec_kernel+advance_gen_kernel (in place)"
+    w6 = TradingEnv(num_envs=512, num_assets=64, window=50, features=6, close_channel=4, device=DEV)
+    assert w6.step_path == "step_advance_lds_kernel"
 
 
 @pytest.mark.parametrize("N,W,F,B,path", [

@@ -31,6 +31,9 @@ SHAPES = [(65536, 30, 50, 8, True), (65536, 30, 50, 8, False), (16384, 30, 50, 8
           (2048, 30, 50, 8, True), (1024, 30, 50, 8, True), (512, 30, 50, 8, True), (256, 30, 50, 8, True),
           (65536, 30, 50, 3, True), (16384, 30, 50, 3, True), (4096, 30, 50, 3, True), (1024, 30, 50, 3, True),
           (65536, 30, 50, 4, True), (16384, 64, 50, 6, True)]
+if os.environ.get("AB_GEN_SHAPES") == "wide":     # windows past the register step's 16,384 floats
+    SHAPES = [(16384, 64, 50, 6, True), (8192, 100, 50, 8, True), (4096, 64, 50, 8, True), (16384, 64, 50, 6, False),
+              (2048, 128, 50, 4, True)]
 
 
 def step_bytes(N, W, F):
