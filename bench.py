@@ -94,8 +94,8 @@ def parse():
     ap.add_argument("--commission", type=float, default=0.0)
     ap.add_argument("--event-every", type=int, default=0,
                     help="timed steps per HIP-event-bracketed kernel sample; 0 (default): every 4th step, every "
-                         "16th when the warm-up steps run under 200 us (an event pair costs the stream ~1.5 us: "
-                         "3.5 %% of a 4,096-env step sampled every 4th step)")
+                         "16th for Infinity-Cache-resident windows, whose steps take tens of us (an event pair costs "
+                         "the stream ~1.5 us: 3.5 %% of a 4,096-env step sampled every 4th step)")
     ap.add_argument("--alt-steps", type=int, default=50,
                     help="extra timed steps of the other window mode (0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -300,7 +300,7 @@ def sha256_file(path):
 
 def spread(us):
     """min / median / max of the sampled kernel times, and which sample was the slowest
-    (sample i brackets timed step EVENT_EVERY * i, or 4 EVENT_EVERY * i for short steps)."""
+    (sample i brackets timed step EVENT_EVERY * i, or 4 EVENT_EVERY * i for cache-resident windows)."""
     return {"min": min(us), "median": statistics.median(us), "max": max(us), "samples": len(us),
             "slowest_sample": max(range(len(us)), key=us.__getitem__)}
 
@@ -413,18 +413,17 @@ def main():
 
     # ---- 2. the timed region
     def timed(steps, warmup, double):
-        torch.cuda.synchronize(dev)
-        tw = time.perf_counter()
         for i in range(warmup):
             one_step(i, double)
         torch.cuda.synchronize(dev)
-        warm_us = (time.perf_counter() - tw) / max(1, warmup) * 1e6
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         # the stream kernel (or the one-launch step) is bracketed by HIP events on every
         # EVENT_EVERY-th step of the timed region (each event pair costs the stream a few us)
-        every = args.event_every if args.event_every > 0 else (EVENT_EVERY if warm_us >= 200.0 else 4 * EVENT_EVERY)
+        # the same on every rank: a function of the shape, not of a measurement
+        every = args.event_every if args.event_every > 0 else (
+            EVENT_EVERY if B * N * W * F * 4 * (2 if double else 1) > L3_BYTES else 4 * EVENT_EVERY)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(0, steps, every)]
         t0 = time.perf_counter()
