@@ -586,6 +586,26 @@ def test_gpu_generic_stream_vs_oracle(N, W, F, B, kw, db):
               impl="two_launch", resets={W // 2 + 1: rng.random(B) < 0.4})
 
 
+@pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
+def test_gpu_generic_stream_auto_at_size(db):
+    """AUTO's generic stream on a window past its 16 MiB threshold (600 x 30 x 50 x 8, the
+    reference loader's F), commission and the differential Sharpe, past the ring's wrap."""
+    from pmenv import TradingEnv
+    kw = {"commission": 0.0025, "reward": "diff_sharpe", "close_channel": 6}
+    e = TradingEnv(num_envs=600, num_assets=30, window=50, features=8, device=DEV, **kw)
+    assert e.step_path.count("advance_gen_kernel") == 2, e.step_path
+    _run_both(kw, B=600, N=30, W=50, T=53, kind="mixed", F=8, seed=608, double_buffer=db)
+
+
+@pytest.mark.parametrize("kw", [{"commission": 0.0025, "reward": "diff_sharpe"}, {"ring": "chrono", "reward": "sharpe_ratio"}],
+                         ids=["commission", "chrono"])
+def test_gpu_tiny_step_many_envs_modes(kw):
+    """step_tiny_kernel with 2,048 envs of config 1's shape in the other reward / ring modes."""
+    from pmenv import TradingEnv
+    assert TradingEnv(num_envs=2048, num_assets=5, window=50, device=DEV, **kw).step_path == "step_tiny_kernel"
+    _run_both(kw, B=2048, N=5, W=50, T=53, kind="mixed", seed=2048)
+
+
 def test_gpu_generic_stream_auto_threshold():
     """AUTO gives F != 5 windows above 16 MiB the generic stream and keeps the register step
     below; F = 5, F > 8 and non-granular windows never take it."""
