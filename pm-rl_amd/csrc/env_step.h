@@ -1853,13 +1853,46 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
         if (!full) return t < W - idx ? -1 : t - (W - idx);
         return p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
     };
+    // HBM-streamed device windows whose env block is 16-B aligned (p.surf_chunked) are
+    // rewritten in whole 16-B chunks (each thread's chunks loaded now, with the ring floats
+    // their weight-channel elements take): the channel alone is every F-th float of the window,
+    // whose dword writes leave every line of it partly written. Cache-resident windows keep the
+    // dword writes (the Infinity Cache merges them; whole chunks move 5x the bytes there)
+    const uint32_t NWF = (uint32_t)(N * W * F), nq = NWF >> 2;
+    const bool chunked = !HOST && out && p.surf_chunked && (NWF & 3u) == 0 && ((uintptr_t)p.obs & 15u) == 0;
+    constexpr int PQ = 8;                          // chunks per thread prefetched (N W F <= 8,192)
+    const auto rs_env = make_rsrc(HOST ? p.obs : p.obs + (size_t)b * NWF, chunked ? NWF * 4u : 0u);
+    f4 ch[PQ];
+    float rv[PQ][2];                               // the ring floats of a chunk's (at most two) weight elements
     float pv[PF];
+    // the chunk's k-th weight-channel element: its float offset in the chunk (>= 4: none) and channel index
+    auto wel = [&](uint32_t q, int kth, int& c, int& i) {
+        const uint32_t j0 = 4u * q;
+        const int f0 = (int)(j0 - fdiv(j0, p.div_f) * (uint32_t)F);
+        c = (F - 1 - f0) + kth * F;
+        i = (int)fdiv(j0 + (uint32_t)c, p.div_f);
+    };
+    if (chunked) {
 #pragma unroll
-    for (int e = 0; e < PF; ++e) {
-        const int i = tid + kBlock * e;
-        int n = 0;
-        const int rs = out && i < N * W ? ring_src(i, n) : -1;
-        pv[e] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
+        for (int e = 0; e < PQ; ++e) {
+            const uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * e);
+            ch[e] = buf_load4<0>(rs_env, q < nq ? q * 16u : 0x80000000u);
+#pragma unroll
+            for (int kth = 0; kth < 2; ++kth) {
+                int c, i, n = 0;
+                wel(q, kth, c, i);
+                const int rs = q < nq && c < 4 ? ring_src(i, n) : -1;
+                rv[e][kth] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < PF; ++e) {
+            const int i = tid + kBlock * e;
+            int n = 0;
+            const int rs = out && i < N * W ? ring_src(i, n) : -1;
+            pv[e] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
+        }
     }
     if (tid < 64) {
         gather_inputs(p, b, s, k);
@@ -1873,8 +1906,44 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
     }
     float* obs = HOST ? io.chan + (size_t)b * N * W : p.obs + (size_t)b * N * W * F;
     const int fs = HOST ? 1 : F, fo = HOST ? 0 : F - 1;
+    if (chunked) {
+        auto patch = [&](uint32_t q, f4& x, const float (&r)[2]) {
 #pragma unroll
-    for (int e = 0; e < PF; ++e) {
+            for (int kth = 0; kth < 2; ++kth) {
+                int c, i, n;
+                wel(q, kth, c, i);
+                if (c < 4) {
+                    const int rs = ring_src(i, n);
+                    const float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : r[kth]);
+                    x.x = c == 0 ? v : x.x;
+                    x.y = c == 1 ? v : x.y;
+                    x.z = c == 2 ? v : x.z;
+                    x.w = c == 3 ? v : x.w;
+                }
+            }
+        };
+#pragma unroll
+        for (int e = 0; e < PQ; ++e) {
+            const uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * e);
+            patch(q, ch[e], rv[e]);
+            buf_store4<0>(rs_env, q < nq ? q * 16u : 0x80000000u, ch[e]);
+        }
+        for (uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * PQ); q < nq; q += kBlock) {   // past 8,192 floats
+            f4 x = buf_load4<0>(rs_env, q * 16u);
+            float r[2];
+#pragma unroll
+            for (int kth = 0; kth < 2; ++kth) {
+                int c, i, n = 0;
+                wel(q, kth, c, i);
+                const int rs = c < 4 ? ring_src(i, n) : -1;
+                r[kth] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
+            }
+            patch(q, x, r);
+            buf_store4<0>(rs_env, q * 16u, x);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < PF && !chunked; ++e) {
         const int i = tid + kBlock * e;
         if (i < N * W) {
             int n;
@@ -1882,7 +1951,7 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
             obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : pv[e]);
         }
     }
-    for (int i = tid + kBlock * PF; i < N * W; i += kBlock) {   // windows past 1,024 channel floats
+    for (int i = tid + kBlock * PF; i < N * W && !chunked; i += kBlock) {   // windows past 1,024 channel floats
         int n;
         const int rs = ring_src(i, n);
         obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);

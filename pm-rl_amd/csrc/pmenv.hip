@@ -315,6 +315,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         // config 1's 1 x 5 x 50 x 5: 4.1 us (step_small_kernel) -> see DESIGN.md §3
         h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64;
     }
+    // surface steps on windows past the Infinity Cache with 16-B granular env blocks rewrite the
+    // channel in whole chunks
+    h->surf_chunk = window_bytes(c) > (256ll << 20) && ((int64_t)c.num_assets * WF) % 4 == 0;
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
@@ -736,6 +739,7 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     if (const int rc = flat1_invalidate(h, stream)) return rc;   // every other path skips the snapshot
     if (!a->bar) {
         if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
+        p.surf_chunked = h->surf_chunk ? 1 : 0;
         step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
         return check_launch(h, "step_surface_kernel");
     }

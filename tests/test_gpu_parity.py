@@ -231,6 +231,24 @@ def test_gpu_vs_oracle_surface_and_advance(mode):
     _run_both({}, B=33, N=30, W=12, T=30, kind="mixed", mode=mode, seed=3)
 
 
+@pytest.mark.parametrize("N,W,F,B", [
+    (30, 50, 5, 40),      # 7,500 floats per env: 16-B chunks, the tail past 8,192 floats not reached
+    (30, 50, 8, 5),       # 12,000 floats: chunks past the prefetched 8,192
+    (64, 16, 8, 3),       # exactly 8,192 floats
+    (7, 6, 4, 9),         # F = 4: one weight float per chunk, at its end
+    (9, 8, 3, 11),        # F = 3: two weight floats in some chunks
+    (5, 50, 5, 7),        # 1,250 floats: not 16-B granular, the dword path
+])
+@pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
+                         ids=["storage", "chrono", "commission"])
+def test_gpu_surface_step_vs_oracle(N, W, F, B, kw):
+    """The reference surface contract with device windows (channel F-1 rebuilt from the ring):
+    16-B-granular env blocks are rewritten in whole chunks, others float by float; past the
+    ring's wrap, against the oracle."""
+    kw = dict(kw, **({} if F == 5 else {"close_channel": F - 2}))
+    _run_both(kw, B=B, N=N, W=W, T=W + 5, kind="mixed", F=F, mode="surface", seed=N * 7 + W + F)
+
+
 @pytest.mark.parametrize("N,W,F", [(30, 50, 5), (129, 50, 5), (5, 50, 5), (7, 6, 3)])
 def test_gpu_double_buffered_advance(N, W, F):
     kw = {} if F == 5 else {"close_channel": F - 2}
