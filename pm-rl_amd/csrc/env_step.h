@@ -1895,9 +1895,20 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
         }
     }
     if (tid < 64) {
-        gather_inputs(p, b, s, k);
-        const double value = scalar_compute(p, b, s, k, v_prev);
-        if (HOST && tid == 0) io.value_out[b] = value;          // the value scalar_compute stored
+        if (N <= 64) {
+            // the register-form scalar step (one asset per lane, DPP reductions, scalar_tail's
+            // state writes), its loads issued inside the branch that consumes them; w' to LDS
+            // for the channel's ring slot
+            const ScalarIn sin = scalar_load<64, true>(p, b, tid, z);
+            const ScalarMid mid = scalar_core<64>(p, b, tid, sin);
+            if (tid < N) s.wp[tid] = mid.wp;
+            scalar_tail<64>(p, b, tid, sin, mid);
+            if (HOST && tid == 0) io.value_out[b] = mid.value;
+        } else {
+            gather_inputs(p, b, s, k);
+            const double value = scalar_compute(p, b, s, k, v_prev);
+            if (HOST && tid == 0) io.value_out[b] = value;      // the value scalar_compute stored
+        }
     }
     __syncthreads();
     if (!out) {
