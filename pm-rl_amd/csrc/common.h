@@ -67,9 +67,6 @@ struct StepParams {
     // first two chunks here (advance_flat_inplace_kernel's halo); null: no copy
     float* halo;
     uint32_t halo_wgs, halo_block, halo_qtot;
-    // surface step: rewrite the channel in whole 16-B chunks of the window (HBM-streamed
-    // windows with 16-B granular env blocks; step_surface_kernel)
-    int32_t surf_chunked;
     // one-launch flat step (step_flat.h): the state snapshot the scalar step reads
     // (parity p: value, counter, get_last(), last close) and the one the env's owner
     // writes for the next step (parity 1 - p); in place, the halo of this step and the

@@ -1853,46 +1853,13 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
         if (!full) return t < W - idx ? -1 : t - (W - idx);
         return p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W;
     };
-    // HBM-streamed device windows whose env block is 16-B aligned (p.surf_chunked) are
-    // rewritten in whole 16-B chunks (each thread's chunks loaded now, with the ring floats
-    // their weight-channel elements take): the channel alone is every F-th float of the window,
-    // whose dword writes leave every line of it partly written. Cache-resident windows keep the
-    // dword writes (the Infinity Cache merges them; whole chunks move 5x the bytes there)
-    const uint32_t NWF = (uint32_t)(N * W * F), nq = NWF >> 2;
-    const bool chunked = !HOST && out && p.surf_chunked && (NWF & 3u) == 0 && ((uintptr_t)p.obs & 15u) == 0;
-    constexpr int PQ = 8;                          // chunks per thread prefetched (N W F <= 8,192)
-    const auto rs_env = make_rsrc(HOST ? p.obs : p.obs + (size_t)b * NWF, chunked ? NWF * 4u : 0u);
-    f4 ch[PQ];
-    float rv[PQ][2];                               // the ring floats of a chunk's (at most two) weight elements
     float pv[PF];
-    // the chunk's k-th weight-channel element: its float offset in the chunk (>= 4: none) and channel index
-    auto wel = [&](uint32_t q, int kth, int& c, int& i) {
-        const uint32_t j0 = 4u * q;
-        const int f0 = (int)(j0 - fdiv(j0, p.div_f) * (uint32_t)F);
-        c = (F - 1 - f0) + kth * F;
-        i = (int)fdiv(j0 + (uint32_t)c, p.div_f);
-    };
-    if (chunked) {
 #pragma unroll
-        for (int e = 0; e < PQ; ++e) {
-            const uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * e);
-            ch[e] = buf_load4<0>(rs_env, q < nq ? q * 16u : 0x80000000u);
-#pragma unroll
-            for (int kth = 0; kth < 2; ++kth) {
-                int c, i, n = 0;
-                wel(q, kth, c, i);
-                const int rs = q < nq && c < 4 ? ring_src(i, n) : -1;
-                rv[e][kth] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < PF; ++e) {
-            const int i = tid + kBlock * e;
-            int n = 0;
-            const int rs = out && i < N * W ? ring_src(i, n) : -1;
-            pv[e] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
-        }
+    for (int e = 0; e < PF; ++e) {
+        const int i = tid + kBlock * e;
+        int n = 0;
+        const int rs = out && i < N * W ? ring_src(i, n) : -1;
+        pv[e] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
     }
     if (tid < 64) {
         if (N <= 64) {
@@ -1917,44 +1884,8 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
     }
     float* obs = HOST ? io.chan + (size_t)b * N * W : p.obs + (size_t)b * N * W * F;
     const int fs = HOST ? 1 : F, fo = HOST ? 0 : F - 1;
-    if (chunked) {
-        auto patch = [&](uint32_t q, f4& x, const float (&r)[2]) {
 #pragma unroll
-            for (int kth = 0; kth < 2; ++kth) {
-                int c, i, n;
-                wel(q, kth, c, i);
-                if (c < 4) {
-                    const int rs = ring_src(i, n);
-                    const float v = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : r[kth]);
-                    x.x = c == 0 ? v : x.x;
-                    x.y = c == 1 ? v : x.y;
-                    x.z = c == 2 ? v : x.z;
-                    x.w = c == 3 ? v : x.w;
-                }
-            }
-        };
-#pragma unroll
-        for (int e = 0; e < PQ; ++e) {
-            const uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * e);
-            patch(q, ch[e], rv[e]);
-            buf_store4<0>(rs_env, q < nq ? q * 16u : 0x80000000u, ch[e]);
-        }
-        for (uint32_t q = (uint32_t)tid + (uint32_t)(kBlock * PQ); q < nq; q += kBlock) {   // past 8,192 floats
-            f4 x = buf_load4<0>(rs_env, q * 16u);
-            float r[2];
-#pragma unroll
-            for (int kth = 0; kth < 2; ++kth) {
-                int c, i, n = 0;
-                wel(q, kth, c, i);
-                const int rs = c < 4 ? ring_src(i, n) : -1;
-                r[kth] = rs >= 0 && rs != slot ? ringb[(size_t)rs * N + n] : 0.0f;
-            }
-            patch(q, x, r);
-            buf_store4<0>(rs_env, q * 16u, x);
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < PF && !chunked; ++e) {
+    for (int e = 0; e < PF; ++e) {
         const int i = tid + kBlock * e;
         if (i < N * W) {
             int n;
@@ -1962,7 +1893,7 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
             obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : pv[e]);
         }
     }
-    for (int i = tid + kBlock * PF; i < N * W && !chunked; i += kBlock) {   // windows past 1,024 channel floats
+    for (int i = tid + kBlock * PF; i < N * W; i += kBlock) {   // windows past 1,024 channel floats
         int n;
         const int rs = ring_src(i, n);
         obs[(size_t)i * fs + fo] = rs < 0 ? 0.0f : (rs == slot ? s.wp[n] : ringb[(size_t)rs * N + n]);
@@ -1979,6 +1910,80 @@ static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams 
 }
 static __global__ __launch_bounds__(kBlock) void step_surface_host_kernel(StepParams p, HostIO io) {
     surface_body<true>(p, io);
+}
+
+// ---------------------------------------------------------------- the surface stream (two launches)
+// The reference surface contract on windows past the Infinity Cache: the scalar step (K1, which
+// also writes this step's ring slot), then this stream over the flat [B, N, W, F] window in
+// 16-B chunks — no shift, so no halo and no LDS: every chunk is loaded, its (at most two)
+// weight-channel floats are replaced by the ring floats they show (weight_buffer.py:32-44,
+// the slot K1 just wrote included), and it is stored whole; the chunk holding a row's close on
+// the last day also writes the advance-mode close (last_close). The per-env workgroup form
+// (step_surface_kernel) waits for its env's scalar step before any store; here the stream
+// streams. POL: the stream's cache policy (1 nt).
+template <int BLOCK, int V, int POL>
+__global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uint32_t qtot) {
+    constexpr int kAux = POL == 1 ? 2 : 0;
+    constexpr int CPW = BLOCK * V;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c0 = blockIdx.x * CPW;
+    const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
+    const auto rs = make_rsrc(p.obs + (size_t)c0 * 4, nblk * 16u);
+    const int N = p.N, W = p.W, F = p.F, Fm = F - 1;
+    const uint32_t WF = (uint32_t)(W * F), per4 = (uint32_t)N * WF >> 2;
+    const int close_pos = (W - 1) * F + p.close_ch;          // the last day's close in a row
+    f4 x[V];
+    float r[V][2];
+#pragma unroll
+    for (int v = 0; v < V; ++v) x[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t q = min(c0 + (uint32_t)(64 * V * wave + 64 * v + lane), qtot - 1u);
+        const uint32_t b = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - b * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const uint32_t kk = j0 - row * WF;
+        const int f0 = (int)(kk - fdiv(kk, p.div_f) * (uint32_t)F);
+        const int32_t k1 = p.k[b];                               // after the scalar step
+        const int idx = ring_slot(k1, W);
+        const bool full = (int64_t)k1 >= W - 1;
+        const float* ringb = p.ring + (size_t)b * W * N;
+#pragma unroll
+        for (int kth = 0; kth < 2; ++kth) {
+            const int c = (Fm - f0) + kth * F;                   // the chunk's kth weight float (>= 4: none)
+            int rsl = -1, rr = (int)row;
+            if (c < 4) {
+                int pos = (int)kk + c;
+                if (pos >= (int)WF) { pos -= (int)WF; ++rr; }
+                const int t = (int)fdiv((uint32_t)pos, p.div_f);   // pos = t F + F - 1
+                rsl = !full ? (t < W - idx ? -1 : t - (W - idx))
+                            : (p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W);
+            }
+            r[v][kth] = rsl >= 0 ? ringb[(size_t)rsl * N + rr] : 0.0f;
+        }
+    }
+    const auto rd = rs;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int j = 64 * V * wave + 64 * v + lane;
+        const uint32_t q = min(c0 + (uint32_t)j, qtot - 1u);
+        const uint32_t b = fdiv(q, p.div_units);
+        const uint32_t j0 = 4u * (q - b * per4);
+        const uint32_t row = fdiv(j0, p.div_wf);
+        const uint32_t kk = j0 - row * WF;
+        const int f0 = (int)(kk - fdiv(kk, p.div_f) * (uint32_t)F);
+        float e[4] = {x[v].x, x[v].y, x[v].z, x[v].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            int pos = (int)kk + c, rr = (int)row;
+            if (pos >= (int)WF) { pos -= (int)WF; ++rr; }
+            if (pos == close_pos && c0 + (uint32_t)j < qtot) p.last_close[(size_t)b * N + rr] = e[c];
+        }
+        const int ca = Fm - f0, cb = ca + F;                       // the weight floats' places (>= 4: none)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) e[c] = c == ca ? r[v][0] : (c == cb ? r[v][1] : e[c]);
+        buf_store4<kAux>(rd, (uint32_t)j * 16u, f4{e[0], e[1], e[2], e[3]});
+    }
 }
 
 // ---------------------------------------------------------------- reset kernel

@@ -35,7 +35,7 @@ struct pmenv {
     // windows of at most 1,024 x 16 floats; 0: the LDS fallback
     int small_block, small_e;
     bool tiny;            // ... of at most 256 x 8 floats and N <= 64: step_tiny_kernel (LDS-staged)
-    bool surf_chunk;      // surface steps rewrite the channel in whole 16-B chunks (StepParams::surf_chunked)
+    bool surf_stream;     // surface steps as two launches: the scalar step, then surface_stream_kernel
     // LDS single-launch fallback geometry
     int rows_per_tile, tile_floats;
     bool vec;

@@ -115,6 +115,16 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
     launch_scalar_kernels(h, p, stream);
 }
 
+// ---------------------------------------------------------------- the surface stream
+inline void launch_surface_stream(const pmenv* h, StepParams p, hipStream_t stream) {
+    const pmenv_cfg& c = h->cfg;
+    const uint32_t per4 = (uint32_t)((int64_t)c.num_assets * c.window * c.features / 4);
+    const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
+    p.div_units = make_fastdiv(per4);
+    const unsigned grid = (qtot + 1023u) / 1024u;
+    surface_stream_kernel<256, 4, 1><<<grid, 256, 0, stream>>>(p, qtot);
+}
+
 // ---------------------------------------------------------------- the generic stream (F != 5)
 // rows of the [B N, W F] window a workgroup of cpw chunks can touch (the plan keeps it <= BLOCK)
 inline uint32_t gen_rows(const pmenv* h, int cpw) {

@@ -315,9 +315,12 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         // config 1's 1 x 5 x 50 x 5: 4.1 us (step_small_kernel) -> see DESIGN.md §3
         h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64;
     }
-    // surface steps on windows past the Infinity Cache with 16-B granular env blocks rewrite the
-    // channel in whole chunks
-    h->surf_chunk = window_bytes(c) > (256ll << 20) && ((int64_t)c.num_assets * WF) % 4 == 0;
+    // surface steps on windows past the Infinity Cache with 16-B granular env blocks: the scalar
+    // step, then surface_stream_kernel (65,536 x 30 x 50 x 5 857 against 939 us on the per-env
+    // kernel's dword writes, 892 with its writes in whole chunks; cache-resident windows keep the
+    // per-env kernel: 4,096 x 30 38.3 against 48.6 in whole chunks — ab_r05/surface_stream_r05s4_*)
+    h->surf_stream = window_bytes(c) > (256ll << 20) && ((int64_t)c.num_assets * WF) % 4 == 0 &&
+                     (int64_t)c.num_envs * ((int64_t)c.num_assets * WF / 4) < (1ll << 31) - 1024;
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
@@ -737,9 +740,21 @@ int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
         return check_launch(h, "step_relay_kernel");
     }
     if (const int rc = flat1_invalidate(h, stream)) return rc;   // every other path skips the snapshot
+    if (!a->bar && h->surf_stream && (((uintptr_t)a->obs) & 15u) == 0) {
+        // past the Infinity Cache: the scalar step, then the surface stream
+        const uint32_t ph = a->phases ? a->phases : (PMENV_PHASE_SCALAR | PMENV_PHASE_ADVANCE);
+        if (ph & PMENV_PHASE_SCALAR) {
+            launch_scalar_kernels(h, p, stream);
+            if (const int rc = check_launch(h, "scalar_step_kernel")) return rc;
+        }
+        if (ph & PMENV_PHASE_ADVANCE) {
+            launch_surface_stream(h, p, stream);
+            return check_launch(h, "surface_stream_kernel");
+        }
+        return PMENV_OK;
+    }
     if (!a->bar) {
         if (a->phases == PMENV_PHASE_ADVANCE) return PMENV_OK;   // single launch: done in the scalar phase
-        p.surf_chunked = h->surf_chunk ? 1 : 0;
         step_surface_kernel<<<B, kBlock, h->lds_surface, stream>>>(p);
         return check_launch(h, "step_surface_kernel");
     }

@@ -366,7 +366,7 @@ void plan(pmenv* h) {
     }
     t->small_abl = knob_int("PMENV_SMALL_ABL", -1);
     t->tiny_off = knob_int("PMENV_TINY_OFF", 0) != 0;
-    if (const char* k = knob("PMENV_SURF_CHUNK")) h->surf_chunk = atoi(k) != 0 && ((int64_t)c.num_assets * c.window * c.features) % 4 == 0;
+    if (const char* k = knob("PMENV_SURF_STREAM")) h->surf_stream = h->surf_stream && atoi(k) != 0;
     t->gen_perelem = knob_int("PMENV_GEN_PERELEM", 0) != 0;
     t->gen_pol0 = knob_int("PMENV_GEN_POL0", 0) != 0;
     if (knob_int("PMENV_GEN_OFF", 0)) h->gen_auto = 0;   // AUTO keeps the register step for F != 5

@@ -11,7 +11,7 @@
 #   bash tools/round_r05_ab.sh gen TAG         # the generic F != 5 stream vs the register step / LDS fallback
 #   bash tools/round_r05_ab.sh gen_geom TAG    # its tile geometries (256 x 4 / 256 x 2 / 512 x 2) and cache policy
 #   bash tools/round_r05_ab.sh gen_prof TAG    # its kernel trace and FETCH_SIZE / WRITE_SIZE at F = 3 / 8
-#   bash tools/round_r05_ab.sh surface TAG     # the surface contract at scale: whole-chunk vs dword channel writes
+#   bash tools/round_r05_ab.sh surface TAG     # the surface contract: the two-launch surface stream vs the per-env kernel
 set -u
 export TMPDIR=/tmp
 CMD=${1:?subcommand}
@@ -97,11 +97,10 @@ gen_prof)
         -- python3 tools/bench_shapes.py $S > ${O}_gen_write.log 2>&1 || exit $? ;;
 surface)
     tests tests/test_gpu_parity.py -k "surface or goldens"
-    for k in 0 1; do      # the tools leg with the chunked rewrite forced off / on
-        SURF_LIBS=pm-rl_amd/pmenv/libpmenv.so,tools/libpmenv_ab.so PMENV_SURF_CHUNK=$k timeout -k 10 300 \
-            python tools/bench_surface.py > ${O}_surf_$k.json 2> ${O}_surf_$k.err || exit $?
-        echo "product vs tools (chunked=$k):"
-        grep -v "^[WE]2" ${O}_surf_$k.err | python3 -c "
+    # the tools leg on the per-env kernel (dword channel writes)
+    SURF_LIBS=pm-rl_amd/pmenv/libpmenv.so,tools/libpmenv_ab.so PMENV_SURF_STREAM=0 timeout -k 10 300 \
+        python tools/bench_surface.py > ${O}_surf.json 2> ${O}_surf.err || exit $?
+    grep -v "^[WE]2" ${O}_surf.err | python3 -c "
 import sys, json
 for l in sys.stdin:
     k, _, j = l.partition(' ')
@@ -109,8 +108,7 @@ for l in sys.stdin:
     except Exception: continue
     legs = [n for n in o if isinstance(o[n], dict)]
     print(k, *[f\"{o[n]['us_per_step']:.1f}\" for n in legs], 'windows', o.get('windows_equal'), 'rewards', o.get('rewards_equal'))
-"
-    done ;;
+" ;;
 *)
     echo "unknown subcommand $CMD"; exit 2 ;;
 esac
