@@ -1350,8 +1350,9 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
 // (a divergent branch) read the rows' bar / w' / slot and compose element by element; TWO =
 // false (tools build): every element composed from its row's LDS values. The same values.
 // POL: the window stream's cache policy (the own-chunk loads and the stores), as the F = 5
-// streams: 0 default, 1 nt (windows past the Infinity Cache).
-template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0>
+// streams: 0 default, 1 nt (windows past the Infinity Cache). ABL (tools build, timing
+// only): 1 no side-data loads, 2 no compose (the shifted source stored), 4 no shifted read.
+template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot, uint32_t rows) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V;
@@ -1382,16 +1383,23 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     const uint32_t ql = c0 + nblk - 1u;
     const uint32_t b_hi = fdiv(ql, p.div_units);
     const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
-    if ((uint32_t)tid <= g_hi - g_lo) {
+    if ((ABL & 1) && (uint32_t)tid <= g_hi - g_lo) {
+#pragma unroll
+        for (int f = 0; f < kFm; ++f) sh_bar[tid * kFm + f] = 0.0f;
+        sh_wp[tid] = 0.0f;
+        sh_sl[tid] = -1;
+    } else if ((uint32_t)tid <= g_hi - g_lo) {
         const uint32_t g = g_lo + (uint32_t)tid;
         const uint32_t b = g / (uint32_t)N, n = g - b * (uint32_t)N;
         const float* barb = env_bar(p, (int)b);                     // null: a day outside the series
-        const auto rb = make_rsrc(barb ? barb + (size_t)n * Fm : p.obs, barb ? (uint32_t)Fm * 4u : 0u);
+        // plain per-lane loads: a buffer resource built from a per-lane base costs a
+        // readfirstlane loop per load, each with its own wait (584 -> 396 us at F = 3, r05ga)
+        const float* rowp = barb + (size_t)n * Fm;
+        float x[kFm];
 #pragma unroll
-        for (int f = 0; f < kFm; ++f) {
-            const float x = buf_load1(rb, f < Fm ? (uint32_t)f * 4u : 0x80000000u);
-            sh_bar[tid * kFm + f] = barb ? x : __int_as_float(0x7fc00000);
-        }
+        for (int f = 0; f < kFm; ++f) x[f] = f < Fm && barb ? rowp[f] : __int_as_float(0x7fc00000);
+#pragma unroll
+        for (int f = 0; f < kFm; ++f) sh_bar[tid * kFm + f] = x[f];
         sh_wp[tid] = p.w_new[g];
         const int32_t kc = p.k[b] - 1;                               // the scalar step counted this step
         const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && kc >= W - 1);
@@ -1417,7 +1425,9 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
         const float* src = shf + 4 * j + F;                           // floats 4j+F .. 4j+F+3
         float sh[4];
-        if constexpr (SHV == 4) {
+        if constexpr ((ABL & 4) != 0) {
+            sh[0] = un[0]; sh[1] = un[1]; sh[2] = un[2]; sh[3] = un[3];
+        } else if constexpr (SHV == 4) {
             const f4 x = *reinterpret_cast<const f4*>(src);
             sh[0] = x.x; sh[1] = x.y; sh[2] = x.z; sh[3] = x.w;
         } else if constexpr (SHV == 2) {
@@ -1441,6 +1451,10 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
             }
             // a last day (every chunk that reaches the row's end holds one) or the ring slot
             patch = (int)kk + 3 >= WF - F || (sl0 >= 0 && (uint32_t)(sl0 * F + Fm - (int)kk) <= 3u);
+        }
+        if constexpr ((ABL & 2) != 0) {
+            o[0] = sh[0]; o[1] = sh[1]; o[2] = sh[2]; o[3] = sh[3];
+            patch = false;
         }
         if (patch) {
             const int r1 = min(r0 + 1, (int)rows - 1);

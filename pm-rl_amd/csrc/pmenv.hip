@@ -476,31 +476,26 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     }
     // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 8 (its halo is the two
     // chunks past a workgroup), 16-B granular env windows, at most BLOCK rows per workgroup.
-    // AUTO gives it the windows above 16 MiB that would take the register step: at 512 /
-    // 1,024 / 4,096 / 65,536 x 30 x 50 x 8 in place 17.3 / 29.3 / 80.0 / 1,272.9 us against
-    // 23.7 / 43.0 / 159.3 / 2,791.4, F = 3 at 1,024 envs 21.2 vs 22.8; at 256 x 30 x 50 x 8
-    // (12 MiB) the register step's one launch wins (13.7 vs 14.8), and past its 16,384 floats
-    // the LDS fallback held (16,384 x 64 x 50 x 6: 485.0 vs 546.6) — profiles/ab_r05/gen_r05t.*
+    // AUTO gives it every window above 2 MiB (16 MiB where step_tiny_kernel would take it),
+    // both modes: against the register step / the LDS fallback, one process, the same bits
+    // (profiles/ab_r05/gen_few_r05gf2.*), 64 / 256 x 30 x 50 x 8 in place 9.2 / 11.2 against
+    // 12.8 / 14.2 us, 128 x 30 x 50 x 3 8.7 vs 9.2, 32 x 64 x 50 x 8 8.6 vs 16.4, 64 x 100 x 50 x 8
+    // 10.9 vs 24.4 (LDS fallback), 2,048 x 128 x 50 x 4 double-buffered 76.8 vs 91.8; ties at 1-2
+    // MiB (128 x 16 x 32 x 8 8.9 / 8.9, 64 x 16 x 32 x 8 9.0 vs 8.8); over tiny windows 1,024 x 5 x
+    // 50 x 8 (8 MiB) 9.9 vs 7.8, 4,096 x 5 x 50 x 8 17.1 / 17.0, 4,096 x 8 x 32 x 6 14.9 vs 16.7
     {
         const int F = c.features;
-        h->gen_block = 256;
-        // 256 x 4 chunks per workgroup for windows past 128 MiB, 256 x 2 below (with the side
-        // data in dynamic LDS, profiles/ab_r05/gen_geom4_dynlds_r05q.*, in place, 256 x 4 / 256 x 2:
-        // F = 3 at 65,536 / 16,384 / 4,096 envs 582.4 / 157.8 / 53.5 against 667.5 / 173.2 /
-        // 49.5 us, F = 4 at 65,536 678.4 / 789.9, F = 8 at 4,096 / 2,048 / 256 77.2 / 47.5 / 15.7
-        // against 81.2 / 46.9 / 14.1, at 65,536 1,105.2 / 1,105.1; 512 x 2 lost 10-30 %
-        // everywhere, gen_geom_*_r05x.*)
-        const int64_t cpw = (int64_t)h->gen_block * 4;      // the shape rule at the larger tile
+        // 512 x 2 chunks per workgroup for windows past 128 MiB, 256 x 2 below (gen_geom_*_r05gg.*,
+        // against 256 x 4: 65,536 x 30 x 50 x 8 in place / double-buffered 1,015.5 / 1,033.2 vs
+        // 1,061.6 / 1,069.0 us, F = 3 / 4 388.8 / 514.9 vs 406.9 / 537.4, 16,384 x 30 x 50 x 8
+        // 254.1 vs 268.3; within 2 % of 256 x 2 at 4,096 envs and below)
+        h->gen_block = win > (128ll << 20) ? 512 : 256;
+        h->gen_v = 2;
+        const int64_t cpw = 1024;                           // the shape rule at the larger tile
         h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
-                    (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= h->gen_block;
-        h->gen_v = win > (128ll << 20) ? 4 : 2;
+                    (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= 256;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
-        h->gen_auto = h->gen_ok && h->small_block && win > (16ll << 20) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
-        // past 16,384 floats per env the LDS fallback is the alternative: the generic stream wins
-        // in place at F = 8 (8,192 x 100 x 50 x 8 461.6 vs 529.3 us, 4,096 x 64 x 50 x 8 159.8 vs
-        // 171.7) and loses or ties elsewhere (2,048 x 128 x 50 x 4 101.0 vs 74.2; 16,384 x 64 x 50
-        // x 6 in place 475.7 vs 485.7, double-buffered 472.9 vs 459.9) — ab_r05/gen_wide_r05w2.*
-        if (h->gen_ok && !h->small_block && F == 8 && win > (16ll << 20)) h->gen_auto = PMENV_FUSE_INPLACE;
+        h->gen_auto = h->gen_ok && win > (h->tiny ? (16ll << 20) : (2ll << 20)) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
     }
     pmenv_tools::plan(h);     // the tools build's PMENV_* knobs (nothing in the product library)
     if (h->streaming) {

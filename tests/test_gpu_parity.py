@@ -618,7 +618,7 @@ def test_gpu_generic_stream_vs_oracle(N, W, F, B, kw, db):
 
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
 def test_gpu_generic_stream_auto_at_size(db):
-    """AUTO's generic stream on a window past its 16 MiB threshold (600 x 30 x 50 x 8, the
+    """AUTO's generic stream on a window past its 2 MiB threshold (600 x 30 x 50 x 8, the
     reference loader's F), commission and the differential Sharpe, past the ring's wrap."""
     from pmenv import TradingEnv
     kw = {"commission": 0.0025, "reward": "diff_sharpe", "close_channel": 6}
@@ -637,28 +637,34 @@ def test_gpu_tiny_step_many_envs_modes(kw):
 
 
 def test_gpu_generic_stream_auto_threshold():
-    """AUTO gives F != 5 windows above 16 MiB the generic stream and keeps the register step
-    below; F = 5, F > 8 and non-granular windows never take it."""
+    """AUTO gives F != 5 windows above 2 MiB the generic stream (16 MiB over the tiny step's
+    windows; past the register step's 16,384 floats too, both modes) and keeps the one-launch
+    steps below; F = 5, F > 8 and non-granular windows never take it."""
     from pmenv import TradingEnv
-    big = TradingEnv(num_envs=512, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    big = TradingEnv(num_envs=48, num_assets=30, window=50, features=8, close_channel=6, device=DEV)   # 2.3 MB
     assert big.step_path.count("advance_gen_kernel") == 2, big.step_path
-    small = TradingEnv(num_envs=256, num_assets=30, window=50, features=8, close_channel=6, device=DEV)
+    small = TradingEnv(num_envs=40, num_assets=30, window=50, features=8, close_channel=6, device=DEV)  # 1.9 MB
     assert small.step_path == "step_small_kernel"
     assert "advance_gen_kernel" not in TradingEnv(num_envs=4096, num_assets=30, window=50, device=DEV).step_path
+    # tiny windows (<= 2,048 floats): 16 MiB
+    tiny = TradingEnv(num_envs=2048, num_assets=5, window=50, features=8, close_channel=6, device=DEV)  # 16.4 MB
+    assert tiny.step_path == "step_tiny_kernel"
+    tiny_big = TradingEnv(num_envs=2100, num_assets=5, window=50, features=8, close_channel=6, device=DEV)
+    assert tiny_big.step_path.count("advance_gen_kernel") == 2, tiny_big.step_path
     wide = TradingEnv(num_envs=8, num_assets=30, window=50, features=12, close_channel=10, device=DEV)
     with pytest.raises(ValueError):
         wide.set_step_impl("two_launch")
-    # past the register step's 16,384 floats per env: in place only, F = 8 only
-    w8 = TradingEnv(num_envs=256, num_assets=100, window=50, features=8, close_channel=6, device=DEV)
-    assert w8.step_path == "step_advance_lds_kernel (obs_out) | scalar_step_vec_kernel+advance_gen_kernel (in place)"
-    w6 = TradingEnv(num_envs=512, num_assets=64, window=50, features=6, close_channel=4, device=DEV)
+    # past the register step's 16,384 floats per env: the LDS fallback below 2 MiB
+    w8 = TradingEnv(num_envs=16, num_assets=100, window=50, features=8, close_channel=6, device=DEV)   # 2.6 MB
+    assert w8.step_path.count("advance_gen_kernel") == 2, w8.step_path
+    w6 = TradingEnv(num_envs=8, num_assets=64, window=50, features=6, close_channel=4, device=DEV)     # 0.6 MB
     assert w6.step_path == "step_advance_lds_kernel"
 
 
 @pytest.mark.parametrize("N,W,F,B,path", [
     (5, 50, 5, 4096, "step_tiny_kernel"),      # config 1's env, 4,096 of them (odd envs 8-B aligned)
-    (8, 50, 8, 1024, "step_small_kernel"),     # 3,200 floats: 256 x 16
-    (30, 50, 8, 96, "step_small_kernel"),      # 12,000 floats: 1,024 x 16
+    (9, 50, 7, 1024, "step_small_kernel"),     # 3,150 floats (8-B granular: AUTO keeps the register step)
+    (30, 49, 7, 96, "step_small_kernel"),      # 10,290 floats: 1,024 x 16
     (7, 10, 3, 2048, "step_tiny_kernel"),
 ])
 def test_gpu_register_step_many_envs(N, W, F, B, path):

@@ -58,6 +58,7 @@ struct Tools {
     bool tiny_off = false;      // PMENV_TINY_OFF: step_small_kernel where the product runs step_tiny_kernel
     bool gen_perelem = false;   // PMENV_GEN_PERELEM: advance_gen_kernel's per-element compose, dword reads
     bool gen_pol0 = false;      // PMENV_GEN_POL0: advance_gen_kernel with the default cache policy everywhere
+    int gen_abl = 0;            // PMENV_GEN_ABL: advance_gen_kernel's timing-only ablations (in place, nt)
     uint32_t small_slot = 0;    // its stamp slot, one per launch
 };
 
@@ -369,11 +370,12 @@ void plan(pmenv* h) {
     if (const char* k = knob("PMENV_SURF_STREAM")) h->surf_stream = h->surf_stream && atoi(k) != 0;
     t->gen_perelem = knob_int("PMENV_GEN_PERELEM", 0) != 0;
     t->gen_pol0 = knob_int("PMENV_GEN_POL0", 0) != 0;
+    t->gen_abl = knob_int("PMENV_GEN_ABL", 0);
     if (knob_int("PMENV_GEN_OFF", 0)) h->gen_auto = 0;   // AUTO keeps the register step for F != 5
-    if (const char* k = knob("PMENV_GEN_GEOM")) {     // advance_gen_kernel's BLOCK x V: 256x4 | 256x2 | 512x2
+    if (const char* k = knob("PMENV_GEN_GEOM")) {     // advance_gen_kernel's BLOCK x V: 256x4 | 256x2 | 512x2 | 512x4 | 1024x2
         int bk = 0, v = 0;
-        if (h->gen_ok && sscanf(k, "%dx%d", &bk, &v) == 2 && (bk * 10 + v == 2564 || bk * 10 + v == 2562 ||
-                                                               bk * 10 + v == 5122)) {
+        const int g = sscanf(k, "%dx%d", &bk, &v) == 2 ? bk * 10 + v : 0;
+        if (h->gen_ok && (g == 2564 || g == 2562 || g == 5122 || g == 5124 || g == 10242)) {
             h->gen_block = bk;
             h->gen_v = v;
         }
@@ -529,24 +531,51 @@ bool launch_small(const pmenv* h, const StepParams& p, hipStream_t stream) {
     return true;
 }
 
-bool launch_gen(const pmenv* h, const StepParams& p, hipStream_t stream) {
-    const unsigned grid = (unsigned)((h->gen_qtot + 1023) / 1024);
-    const uint32_t rows = gen_rows(h, 1024);
+// the generic stream's tools variants at the product's tile (256 x 4 as in round 5's first
+// form, or 512 x 2 past 128 MiB)
+template <int BLOCK, int V>
+bool launch_gen_t(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
+    const uint32_t rows = gen_rows(h, BLOCK * V);
     const size_t lds = (size_t)rows * 9 * 4;
-    if (h->gen_block != 256 || h->gen_v != 4) return false;
+    const int fm4 = h->cfg.features % 4;
+    const bool ip = p.obs_out == p.obs;
     if (tools(h)->gen_pol0) {
-        const int fm4 = h->cfg.features % 4;
-        const bool ip = p.obs_out == p.obs;
-        if (fm4 == 0 && ip) advance_gen_kernel<256, 4, false, 4><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
-        else if (fm4 == 0) advance_gen_kernel<256, 4, true, 4><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
-        else if (ip) advance_gen_kernel<256, 4, false, 1><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
-        else advance_gen_kernel<256, 4, true, 1><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+        if (fm4 == 0 && ip) advance_gen_kernel<BLOCK, V, false, 4><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else if (fm4 == 0) advance_gen_kernel<BLOCK, V, true, 4><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else if (ip) advance_gen_kernel<BLOCK, V, false, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else advance_gen_kernel<BLOCK, V, true, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        return true;
+    }
+    if (const int a = tools(h)->gen_abl; a > 0 && ip) {
+#define GEN_ABL(A)                                                                                       \
+    case A:                                                                                              \
+        if (fm4 == 0) advance_gen_kernel<BLOCK, V, false, 4, true, 1, A><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows); \
+        else advance_gen_kernel<BLOCK, V, false, 1, true, 1, A><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);      \
+        break;
+        switch (a) { GEN_ABL(1) GEN_ABL(2) GEN_ABL(3) GEN_ABL(6) GEN_ABL(7) default: return false; }
+#undef GEN_ABL
         return true;
     }
     if (!tools(h)->gen_perelem) return false;
-    if (p.obs_out == p.obs) advance_gen_kernel<256, 4, false, 1, false><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
-    else advance_gen_kernel<256, 4, true, 1, false><<<grid, 256, lds, stream>>>(p, h->gen_qtot, rows);
+    if (ip) advance_gen_kernel<BLOCK, V, false, 1, false><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+    else advance_gen_kernel<BLOCK, V, true, 1, false><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
     return true;
+}
+
+bool launch_gen(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    if (h->gen_block == 256 && h->gen_v == 4) return launch_gen_t<256, 4>(h, p, stream);
+    if (h->gen_block == 512 && h->gen_v == 2) return launch_gen_t<512, 2>(h, p, stream);
+    // tiles the product does not instantiate (PMENV_GEN_GEOM=512x4 | 1024x2)
+    if (h->gen_block == 512 && h->gen_v == 4) {
+        if (!launch_gen_t<512, 4>(h, p, stream)) launch_gen_g<512, 4>(h, p, stream);
+        return true;
+    }
+    if (h->gen_block == 1024 && h->gen_v == 2) {
+        if (!launch_gen_t<1024, 2>(h, p, stream)) launch_gen_g<1024, 2>(h, p, stream);
+        return true;
+    }
+    return false;
 }
 
 bool launch_advance(const pmenv* h, const StepParams& p, hipStream_t stream) {

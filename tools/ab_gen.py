@@ -34,6 +34,19 @@ SHAPES = [(65536, 30, 50, 8, True), (65536, 30, 50, 8, False), (16384, 30, 50, 8
 if os.environ.get("AB_GEN_SHAPES") == "wide":     # windows past the register step's 16,384 floats
     SHAPES = [(16384, 64, 50, 6, True), (8192, 100, 50, 8, True), (4096, 64, 50, 8, True), (16384, 64, 50, 6, False),
               (2048, 128, 50, 4, True)]
+elif os.environ.get("AB_GEN_SHAPES") == "few":    # around AUTO's threshold against the register step
+    SHAPES = [(64, 30, 50, 8, True), (128, 30, 50, 8, True), (256, 30, 50, 8, True), (128, 30, 50, 3, True),
+              (256, 30, 50, 3, True), (512, 30, 50, 3, True), (256, 30, 50, 4, True), (256, 30, 50, 6, True),
+              (256, 30, 50, 8, False), (512, 30, 50, 3, False), (32, 64, 50, 8, True), (128, 16, 32, 8, True),
+              (64, 30, 50, 3, True), (96, 30, 50, 4, True), (64, 16, 32, 8, True),
+              # windows of <= 2,048 floats (step_tiny_kernel's)
+              (1024, 5, 50, 8, True), (4096, 5, 50, 8, True), (16384, 5, 50, 8, True), (4096, 8, 32, 6, True),
+              (16384, 8, 32, 6, False), (4096, 10, 50, 4, True), (65536, 5, 50, 8, True),
+              # past the register step's 16,384 floats (the LDS fallback's)
+              (64, 100, 50, 8, True), (64, 100, 50, 8, False), (128, 64, 50, 6, True), (128, 64, 50, 6, False),
+              (256, 128, 50, 4, True), (8192, 100, 50, 8, False), (2048, 128, 50, 4, False)]
+elif os.environ.get("AB_GEN_SHAPES") == "big":    # in place past 128 MiB (the 256 x 4 nt tiles; PMENV_GEN_ABL legs)
+    SHAPES = [(65536, 30, 50, 3, True), (65536, 30, 50, 4, True), (65536, 30, 50, 8, True)]
 
 
 def step_bytes(N, W, F):
@@ -83,7 +96,7 @@ class Env:
 def main():
     base = os.environ.get("AB_GEN_BASE")            # another product build, forced to two launches too
     perelem = (base is not None or os.environ.get("PMENV_GEN_PERELEM") == "1" or os.environ.get("PMENV_GEN_POL0") == "1"
-               or os.environ.get("AB_GEN_FORCE") == "1")     # the tools leg forced to two launches (e.g. PMENV_GEN_GEOM)
+               or os.environ.get("AB_GEN_FORCE") == "1" or os.environ.get("PMENV_GEN_ABL") is not None)     # the tools leg forced to two launches (e.g. PMENV_GEN_GEOM)
     assert perelem or os.environ.get("PMENV_GEN_OFF") == "1", \
         "run with PMENV_GEN_OFF=1 (against the register step) or PMENV_GEN_PERELEM=1 (against the per-element compose)"
     torch.cuda.set_device(ab.DEV)
@@ -91,6 +104,8 @@ def main():
             "small": ab.load(os.path.join(ROOT, base) if base else os.path.join(ROOT, "tools", "libpmenv_ab.so"))}
     other = (f"{base} (two launches)" if base else
              f"tools build, PMENV_GEN_GEOM={os.environ.get('PMENV_GEN_GEOM')}" if os.environ.get("AB_GEN_FORCE") == "1" else
+             f"advance_gen_kernel ablation PMENV_GEN_ABL={os.environ.get('PMENV_GEN_ABL')} (tools, timing only)"
+             if os.environ.get("PMENV_GEN_ABL") is not None else
              "advance_gen_kernel, default cache policy (tools)" if os.environ.get("PMENV_GEN_POL0") == "1" else
              "advance_gen_kernel per-element (tools)" if perelem else "register step (tools)")
     out = {"K": K, "R": R, "other": other}

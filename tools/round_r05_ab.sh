@@ -11,6 +11,8 @@
 #   bash tools/round_r05_ab.sh gen TAG         # the generic F != 5 stream vs the register step / LDS fallback
 #   bash tools/round_r05_ab.sh gen_geom TAG    # its tile geometries (256 x 4 / 256 x 2 / 512 x 2) and cache policy
 #   bash tools/round_r05_ab.sh gen_prof TAG    # its kernel trace and FETCH_SIZE / WRITE_SIZE at F = 3 / 8
+#   bash tools/round_r05_ab.sh gen_few TAG     # the generic stream vs the register step around AUTO's threshold
+#   bash tools/round_r05_ab.sh gen_abl TAG     # its timing-only ablations (no side data / compose / shifted read)
 #   bash tools/round_r05_ab.sh surface TAG     # the surface contract: the two-launch surface stream vs the per-env kernel
 set -u
 export TMPDIR=/tmp
@@ -79,13 +81,22 @@ gen)
     AB_GEN_SHAPES=wide PMENV_GEN_OFF=1 timeout -k 10 300 python tools/ab_gen.py > ${O}_gen_wide.json 2> ${O}_gen_wide.err || exit $?
     summ ${O}_gen_wide.err ;;
 gen_geom)
-    for g in 256x4 256x2 512x2; do
+    for g in ${GEOMS:-256x4 256x2 512x2}; do
         PMENV_GEN_GEOM=$g AB_GEN_FORCE=1 AB_R=3 timeout -k 10 300 python tools/ab_gen.py > ${O}_geom_$g.json \
             2> ${O}_geom_$g.err || exit $?
         echo "tools leg at $g:"; summ ${O}_geom_$g.err
     done
     PMENV_GEN_POL0=1 AB_R=3 timeout -k 10 300 python tools/ab_gen.py > ${O}_pol.json 2> ${O}_pol.err || exit $?
     echo "tools leg with the default cache policy:"; summ ${O}_pol.err ;;
+gen_abl)    # timing-only ablations of the generic stream at 65,536 x 30 x 50 x {3, 4, 8} in place
+    for a in 1 2 3 6 7; do
+        PMENV_GEN_ABL=$a AB_GEN_SHAPES=big AB_R=3 timeout -k 10 300 python tools/ab_gen.py > ${O}_abl$a.json \
+            2> ${O}_abl$a.err || exit $?
+        echo "ablation $a:"; summ ${O}_abl$a.err
+    done ;;
+gen_few)    # the generic stream against the register step around AUTO's threshold
+    AB_GEN_SHAPES=few PMENV_GEN_OFF=1 timeout -k 10 300 python tools/ab_gen.py > ${O}_few.json 2> ${O}_few.err || exit $?
+    summ ${O}_few.err ;;
 gen_prof)
     S="feat3_65536x30x50x3_ip feat8_65536x30x50x8_ip"
     SHAPES_K=50 SHAPES_R=3 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_gen_prof -o run --output-format csv \
