@@ -1939,6 +1939,10 @@ template <int BLOCK, int V, int POL>
 __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uint32_t qtot) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V;
+    // the workgroup's rows' ring columns, [row][slot]: the ring is [B][W][N] (slot-major), so a
+    // row's days are N floats apart and a chunk-per-lane gather touches a line per lane — staged
+    // instead slot by slot, the rows of a slot adjacent (launch_surface_stream sizes it)
+    extern __shared__ float sring[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t c0 = blockIdx.x * CPW;
     const uint32_t nblk = min((uint32_t)CPW, qtot - c0);
@@ -1947,9 +1951,22 @@ __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uin
     const uint32_t WF = (uint32_t)(W * F), per4 = (uint32_t)N * WF >> 2;
     const int close_pos = (W - 1) * F + p.close_ch;          // the last day's close in a row
     f4 x[V];
-    float r[V][2];
 #pragma unroll
     for (int v = 0; v < V; ++v) x[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t b_lo = fdiv(c0, p.div_units);
+    const uint32_t g_lo = b_lo * (uint32_t)N + fdiv(4u * (c0 - b_lo * per4), p.div_wf);
+    const uint32_t ql = c0 + nblk - 1u;
+    const uint32_t b_hi = fdiv(ql, p.div_units);
+    const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
+    const uint32_t nrows = g_hi - g_lo + 1u;
+    for (uint32_t i = (uint32_t)tid; i < nrows * (uint32_t)W; i += BLOCK) {
+        const uint32_t sl = i / nrows, r = i - sl * nrows;
+        const uint32_t g = g_lo + r, b = g / (uint32_t)N, n = g - b * (uint32_t)N;
+        sring[r * (uint32_t)W + sl] = p.ring[((size_t)b * W + sl) * N + n];
+    }
+    __syncthreads();
+    float r[V][2];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = min(c0 + (uint32_t)(64 * V * wave + 64 * v + lane), qtot - 1u);
@@ -1961,11 +1978,11 @@ __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uin
         const int32_t k1 = p.k[b];                               // after the scalar step
         const int idx = ring_slot(k1, W);
         const bool full = (int64_t)k1 >= W - 1;
-        const float* ringb = p.ring + (size_t)b * W * N;
+        const uint32_t r0 = b * (uint32_t)N + row - g_lo;        // the chunk's row in the workgroup
 #pragma unroll
         for (int kth = 0; kth < 2; ++kth) {
             const int c = (Fm - f0) + kth * F;                   // the chunk's kth weight float (>= 4: none)
-            int rsl = -1, rr = (int)row;
+            int rsl = -1, rr = (int)r0;
             if (c < 4) {
                 int pos = (int)kk + c;
                 if (pos >= (int)WF) { pos -= (int)WF; ++rr; }
@@ -1973,7 +1990,7 @@ __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uin
                 rsl = !full ? (t < W - idx ? -1 : t - (W - idx))
                             : (p.ring_mode == PMENV_RING_STORAGE ? t : (idx + t) % W);
             }
-            r[v][kth] = rsl >= 0 ? ringb[(size_t)rsl * N + rr] : 0.0f;
+            r[v][kth] = rsl >= 0 ? sring[rr * W + rsl] : 0.0f;
         }
     }
     const auto rd = rs;

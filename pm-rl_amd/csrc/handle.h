@@ -36,6 +36,7 @@ struct pmenv {
     int small_block, small_e;
     bool tiny;            // ... of at most 256 x 8 floats and N <= 64: step_tiny_kernel (LDS-staged)
     bool surf_stream;     // surface steps as two launches: the scalar step, then surface_stream_kernel
+    size_t surf_lds;      // its workgroup's rows' ring columns (rows x W floats)
     // LDS single-launch fallback geometry
     int rows_per_tile, tile_floats;
     bool vec;

@@ -122,7 +122,7 @@ inline void launch_surface_stream(const pmenv* h, StepParams p, hipStream_t stre
     const uint32_t qtot = (uint32_t)((int64_t)c.num_envs * per4);
     p.div_units = make_fastdiv(per4);
     const unsigned grid = (qtot + 1023u) / 1024u;
-    surface_stream_kernel<256, 4, 1><<<grid, 256, 0, stream>>>(p, qtot);
+    surface_stream_kernel<256, 4, 1><<<grid, 256, h->surf_lds, stream>>>(p, qtot);
 }
 
 // ---------------------------------------------------------------- the generic stream (F != 5)

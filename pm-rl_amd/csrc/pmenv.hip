@@ -316,11 +316,15 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64;
     }
     // surface steps on windows past the Infinity Cache with 16-B granular env blocks: the scalar
-    // step, then surface_stream_kernel (65,536 x 30 x 50 x 5 857 against 939 us on the per-env
-    // kernel's dword writes, 892 with its writes in whole chunks; cache-resident windows keep the
-    // per-env kernel: 4,096 x 30 38.3 against 48.6 in whole chunks — ab_r05/surface_stream_r05s4_*)
+    // step, then surface_stream_kernel (65,536 x 30 x 50 x 5 723 us with the ring columns staged
+    // in LDS, against 939 on the per-env kernel's dword writes, 892 with its writes in whole
+    // chunks; cache-resident windows keep the per-env kernel: 4,096 x 30 38.3 against 48.6 in
+    // whole chunks — ab_r05/surface_stream_r05s4_*, surface_ringlds_r05sr.*); the staged
+    // columns (rows x W floats) within 64 KiB
+    h->surf_lds = (size_t)(4 * 1024 / WF + 2) * c.window * 4;
     h->surf_stream = window_bytes(c) > (256ll << 20) && ((int64_t)c.num_assets * WF) % 4 == 0 &&
-                     (int64_t)c.num_envs * ((int64_t)c.num_assets * WF / 4) < (1ll << 31) - 1024;
+                     (int64_t)c.num_envs * ((int64_t)c.num_assets * WF / 4) < (1ll << 31) - 1024 &&
+                     h->surf_lds <= (64u << 10);
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);

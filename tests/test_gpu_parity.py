@@ -252,11 +252,12 @@ def test_gpu_surface_step_vs_oracle(N, W, F, B, kw):
 @pytest.mark.parametrize("N,W,F,B,T,kw", [
     (30, 50, 5, 9000, 53, {}),                                      # 270 MB: past the Infinity Cache
     (16, 12, 8, 44000, 15, {"ring": "chrono", "commission": 0.0025}),
+    (4, 5, 4, 850000, 8, {"ring": "chrono"}),                      # 206 rows of 51 envs per workgroup
 ])
 def test_gpu_surface_stream_vs_oracle(N, W, F, B, T, kw):
     """The surface contract on windows past the Infinity Cache: the scalar step, then
     surface_stream_kernel (the window's 16-B chunks with their weight floats replaced from the
-    ring), past the ring's wrap, against the oracle."""
+    ring columns staged in LDS), past the ring's wrap, against the oracle."""
     kw = dict(kw, **({} if F == 5 else {"close_channel": F - 2}))
     _run_both(kw, B=B, N=N, W=W, T=T, kind="simplex", F=F, mode="surface", seed=B + F)
 

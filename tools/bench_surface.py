@@ -25,6 +25,8 @@ DEV = torch.device("cuda:0")
 K = int(os.environ.get("SURF_K", "50"))
 R = int(os.environ.get("SURF_R", "5"))
 SHAPES = [(1, 5, 50, 5), (4096, 30, 50, 5), (16384, 30, 50, 5), (65536, 30, 50, 5), (16384, 30, 50, 8)]
+if os.environ.get("SURF_SHAPES"):                  # e.g. SURF_SHAPES=65536x30x50x5 (profiling passes)
+    SHAPES = [tuple(int(x) for x in s.split("x")) for s in os.environ["SURF_SHAPES"].split(",")]
 
 
 def load(path):

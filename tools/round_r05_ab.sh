@@ -14,6 +14,7 @@
 #   bash tools/round_r05_ab.sh gen_few TAG     # the generic stream vs the register step around AUTO's threshold
 #   bash tools/round_r05_ab.sh gen_abl TAG     # its timing-only ablations (no side data / compose / shifted read)
 #   bash tools/round_r05_ab.sh surface TAG     # the surface contract: the two-launch surface stream vs the per-env kernel
+#   bash tools/round_r05_ab.sh surface_prev TAG  # the surface contract against another product build (SURF_PREV)
 set -u
 export TMPDIR=/tmp
 CMD=${1:?subcommand}
@@ -110,6 +111,28 @@ surface)
     tests tests/test_gpu_parity.py -k "surface or goldens"
     # the tools leg on the per-env kernel (dword channel writes)
     SURF_LIBS=pm-rl_amd/pmenv/libpmenv.so,tools/libpmenv_ab.so PMENV_SURF_STREAM=0 timeout -k 10 300 \
+        python tools/bench_surface.py > ${O}_surf.json 2> ${O}_surf.err || exit $?
+    grep -v "^[WE]2" ${O}_surf.err | python3 -c "
+import sys, json
+for l in sys.stdin:
+    k, _, j = l.partition(' ')
+    try: o = json.loads(j)
+    except Exception: continue
+    legs = [n for n in o if isinstance(o[n], dict)]
+    print(k, *[f\"{o[n]['us_per_step']:.1f}\" for n in legs], 'windows', o.get('windows_equal'), 'rewards', o.get('rewards_equal'))
+" ;;
+surface_prof)   # the surface stream's kernel trace and FETCH_SIZE / WRITE_SIZE at 65,536 x 30 x 50 x 5
+    export SURF_SHAPES=65536x30x50x5
+    SURF_K=20 SURF_R=3 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_surf_prof -o run --output-format csv \
+        -- python3 tools/bench_surface.py > ${O}_surf_prof.log 2>&1 || exit $?
+    grep "surface\|scalar_step" ${O}_surf_prof/run_kernel_stats.csv | cut -c1-170
+    SURF_K=5 SURF_R=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d ${O}_surf_fetch -o run --output-format csv \
+        -- python3 tools/bench_surface.py > ${O}_surf_fetch.log 2>&1 || exit $?
+    SURF_K=5 SURF_R=1 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d ${O}_surf_write -o run --output-format csv \
+        -- python3 tools/bench_surface.py > ${O}_surf_write.log 2>&1 || exit $? ;;
+surface_prev)   # the surface contract against another product build (SURF_PREV, e.g. the last commit's)
+    tests tests/test_gpu_parity.py -k "surface or goldens"
+    SURF_LIBS=pm-rl_amd/pmenv/libpmenv.so,${SURF_PREV:-tools/libpmenv_prev.so} timeout -k 10 300 \
         python tools/bench_surface.py > ${O}_surf.json 2> ${O}_surf.err || exit $?
     grep -v "^[WE]2" ${O}_surf.err | python3 -c "
 import sys, json
