@@ -226,8 +226,8 @@ const char* pmenv_step_path(const pmenv* h);
  * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
  * kernel followed by the window stream (F = 5, 16-B granular env windows; or the generic
  * stream advance_gen_kernel for 2 <= F <= 8, F != 5, 16-B granular env windows with
- * W F >= 17, which AUTO also takes for such windows above 16 MiB of at most 16,384 floats
- * per env, and in place for F = 8 above 16 MiB at any env size); FLAT forces
+ * W F >= 17, which AUTO also takes for such windows above 2 MiB in both modes, 16 MiB
+ * where the env window is at most 2,048 floats with N <= 64); FLAT forces
  * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:
  * F = 5, W >= 2, env windows of >= 148 16-B chunks, N <= 64 — or, as step_flat_vec_kernel,
  * 64 < N <= 512 with W >= 14). Returns PMENV_ERR_ARG

@@ -1,5 +1,5 @@
 """A/B of the F != 5 step: the two-launch generic stream (scalar step + advance_gen_kernel,
-the product's AUTO above 16 MiB, or forced with PMENV_STEP_PATH_TWO_LAUNCH) against the
+the product's AUTO above 2 MiB, or forced with PMENV_STEP_PATH_TWO_LAUNCH) against the
 register step (step_small_kernel: the tools build with PMENV_GEN_OFF=1 keeps AUTO there),
 in ONE process, interleaved, per shape: us per step (HIP events over K steps, median of R),
 env-steps/s and the fraction of the 8 TB/s spec for the step's algorithmic bytes
@@ -45,7 +45,7 @@ elif os.environ.get("AB_GEN_SHAPES") == "few":    # around AUTO's threshold agai
               # past the register step's 16,384 floats (the LDS fallback's)
               (64, 100, 50, 8, True), (64, 100, 50, 8, False), (128, 64, 50, 6, True), (128, 64, 50, 6, False),
               (256, 128, 50, 4, True), (8192, 100, 50, 8, False), (2048, 128, 50, 4, False)]
-elif os.environ.get("AB_GEN_SHAPES") == "big":    # in place past 128 MiB (the 256 x 4 nt tiles; PMENV_GEN_ABL legs)
+elif os.environ.get("AB_GEN_SHAPES") == "big":    # in place past 128 MiB (the nt tiles; PMENV_GEN_ABL legs)
     SHAPES = [(65536, 30, 50, 3, True), (65536, 30, 50, 4, True), (65536, 30, 50, 8, True)]
 
 
