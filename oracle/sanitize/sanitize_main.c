@@ -360,6 +360,56 @@ static void emulate_gen(int B, int N, int W, int F, int BLOCK, int CPW, int shif
     free(mem); free(ref); free(bar); free(wp); free(stored); free(halo); free(order); free(lds);
 }
 
+/* ------------------------------------------------------------ 2c. the surface stream's ring columns */
+/* env_step.h surface_stream_kernel: a workgroup of CPW chunks stages its rows' ring columns
+ * (ring [B][W][N], slot-major) in LDS as [row][slot], rows g_lo .. g_hi; checked: the staged
+ * floats within launch_surface_stream's size ((4 CPW / (W F) + 2) W), every weight float's row
+ * (the chunk's row, or the next one when the chunk crosses a row's end) inside the staged rows,
+ * and the staged float it reads equal to the ring's (row, slot) — for every slot. */
+static void emulate_surf(int B, int N, int W, int F, int CPW) {
+    const int Fm = F - 1, WF = W * F;
+    const int64_t per = (int64_t)N * WF;
+    if (per % 4) return;
+    const int64_t per4 = per / 4, qtot = per4 * B;
+    float* ring = malloc(sizeof(float) * (size_t)B * W * N);
+    for (int64_t i = 0; i < (int64_t)B * W * N; ++i) ring[i] = (float)nrand();
+    const int64_t cap = (int64_t)(4 * CPW / WF + 2) * W;
+    float* sring = malloc(sizeof(float) * (size_t)cap);
+    for (int64_t c0 = 0; c0 < qtot; c0 += CPW) {
+        const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
+        const int64_t b_lo = c0 / per4, ql = c0 + nblk - 1, b_hi = ql / per4;
+        const int64_t g_lo = b_lo * N + (4 * (c0 - b_lo * per4)) / WF;
+        const int64_t g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
+        const int64_t nrows = g_hi - g_lo + 1;
+        CHECK(nrows * W <= cap, "surf: %lld staged floats past %lld", (long long)(nrows * W), (long long)cap);
+        if (nrows * W > cap) break;
+        for (int64_t i = 0; i < nrows * W; ++i) {
+            const int64_t sl = i / nrows, r = i - sl * nrows, g = g_lo + r, b = g / N, n = g - b * N;
+            sring[r * W + sl] = ring[(b * W + sl) * N + n];
+        }
+        for (int64_t q = c0; q < c0 + nblk; ++q) {
+            const int64_t b = q / per4, j0 = 4 * (q - b * per4), row = j0 / WF, kk = j0 - row * WF;
+            const int f0 = (int)(kk % F);
+            for (int kth = 0; kth < 2; ++kth) {
+                const int c = (Fm - f0) + kth * F;
+                if (c >= 4) continue;
+                int64_t pos = kk + c, rr = b * N + row - g_lo;
+                if (pos >= WF) { pos -= WF; ++rr; }
+                CHECK((pos % F) == Fm, "surf: weight float at channel %lld", (long long)(pos % F));
+                CHECK(rr >= 0 && rr < nrows, "surf: row %lld outside the %lld staged", (long long)rr, (long long)nrows);
+                const int64_t g = g_lo + rr, gb = g / N, gn = g - gb * N;
+                CHECK(gb == b, "surf: a chunk's weight float in another env");
+                for (int sl = 0; sl < W; ++sl)
+                    if (memcmp(&sring[rr * W + sl], &ring[(gb * W + sl) * N + gn], 4)) {
+                        CHECK(0, "surf: staged (row %lld, slot %d) differs (B%d N%d W%d F%d)", (long long)rr, sl, B, N, W, F);
+                        break;
+                    }
+            }
+        }
+    }
+    free(ring); free(sring);
+}
+
 /* ------------------------------------------------------------ 3. the flat one-launch step */
 /* step_flat.h over T consecutive steps: tiles of CPW chunks in a random order each step,
  * every store visible at once. A tile reads only its own chunks from the window (checked:
@@ -1047,8 +1097,9 @@ int main(void) {
             for (int cpw = 0; cpw < 2; ++cpw)
                 emulate(shapes[i][0], shapes[i][1], shapes[i][2], cpw ? 1024 : 96, mode == 0,
                         mode ? (int)(urand() * shapes[i][2]) : 0);
-    /* the generic stream (F != 5): the product's 256 x 4 tiles and 512 x 2, and small ones
-     * (64 threads x 1) that put many envs and rows in one tile, both weight-channel modes */
+    /* the generic stream (F != 5): the product's 512 x 2 and 256 x 2 tiles (and 256 x 4, the
+     * tools build's), and small ones (64 threads x 1) that put many envs and rows in one tile,
+     * both weight-channel modes */
     const int gshp[][4] = {{4, 30, 50, 8}, {11, 8, 10, 3}, {9, 5, 12, 2}, {13, 9, 8, 4}, {7, 3, 20, 6},
                            {5, 11, 4, 7}, {3, 64, 16, 8}, {2, 65, 16, 4}, {40, 2, 10, 6}};
     for (size_t i = 0; i < sizeof gshp / sizeof gshp[0]; ++i)
@@ -1057,8 +1108,17 @@ int main(void) {
             const int sl = mode ? (int)(urand() * W) : 0;
             if (4 * 1024 / (W * F) + 2 <= 256) emulate_gen(B, N, W, F, 256, 1024, mode == 0, sl);
             if (4 * 1024 / (W * F) + 2 <= 512) emulate_gen(B, N, W, F, 512, 1024, mode == 0, sl);
+            if (4 * 512 / (W * F) + 2 <= 256) emulate_gen(B, N, W, F, 256, 512, mode == 0, sl);
             if (4 * 64 / (W * F) + 2 <= 64) emulate_gen(B, N, W, F, 64, 64, mode == 0, sl);
         }
+    /* the surface stream's staged ring columns: rows of 20 .. 400 floats, tiles spanning
+     * many envs, the product's 1,024-chunk tiles and small ones */
+    const int sshp[][4] = {{9, 30, 50, 5}, {51, 4, 5, 4}, {13, 16, 12, 8}, {7, 5, 50, 8}, {300, 4, 5, 4},
+                           {5, 30, 50, 3}, {2, 64, 50, 6}};
+    for (size_t i = 0; i < sizeof sshp / sizeof sshp[0]; ++i) {
+        emulate_surf(sshp[i][0], sshp[i][1], sshp[i][2], sshp[i][3], 1024);
+        emulate_surf(sshp[i][0], sshp[i][1], sshp[i][2], sshp[i][3], 64);
+    }
     /* the flat one-launch step: the product's 1,024-chunk tiles (256 x 4 and 512 x 2) and
      * small tiles that put several tiles in one env and several envs in one tile, both ring
      * orders, through the wrap and a re-prime */
