@@ -164,9 +164,12 @@ typedef struct pmenv_step_args {
                               one launch of the two-launch advance path (the advance
                               phase must follow the scalar phase of the same step;
                               used to time the streaming kernel on its own). Where the
-                              step is one launch (step_flat_kernel, step_env_kernel)
-                              the scalar phase runs all of it, the advance phase
-                              nothing                                                 */
+                              step is one launch (step_flat_kernel, step_env_kernel,
+                              step_relay_kernel, the per-env surface step) the scalar
+                              phase runs all of it, the advance phase nothing; the
+                              surface step past the Infinity Cache is two launches (the
+                              scalar step, then surface_stream_kernel rewriting channel
+                              F-1), so its scalar phase alone leaves that channel stale */
 } pmenv_step_args;
 
 #define PMENV_PHASE_SCALAR 1u
@@ -225,7 +228,7 @@ const char* pmenv_step_path(const pmenv* h);
  * mode; ONE_LAUNCH forces step_env_kernel (one workgroup per env: F = 5, W >= 2,
  * N <= 64, the env window within 64 KiB of LDS); TWO_LAUNCH forces the scalar-step
  * kernel followed by the window stream (F = 5, 16-B granular env windows; or the generic
- * stream advance_gen_kernel for 2 <= F <= 8, F != 5, 16-B granular env windows with
+ * stream advance_gen_kernel for 2 <= F <= 16, F != 5, 16-B granular env windows with
  * W F >= 17, which AUTO also takes for such windows above 2 MiB in both modes, 16 MiB
  * where the env window is at most 2,048 floats with N <= 64); FLAT forces
  * step_flat_kernel (the whole step in one launch over fixed 16 KiB tiles of the window:

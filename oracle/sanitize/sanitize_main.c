@@ -18,7 +18,7 @@
  *      - the one-launch step (step_env.h): a workgroup owns one env; its slots are the
  *        env's 1 KiB-aligned 64-chunk blocks, lanes outside the env read 0 and store
  *        nothing. Reads outside the env are checked never to feed a kept position.
- *    - the generic stream for F != 5 (env_step.h advance_gen_kernel): the same workgroup
+ *    - the generic stream for F != 5, F <= 16 (env_step.h advance_gen_kernel): the same workgroup
  *      and halo, the shift by F floats, the element walk over rows and the staged rows.
  * 3. Emulates the flat one-launch step (step_flat.h) over consecutive steps: tiles in a
  *    random order, the halo and the state snapshot by parity, one owner per env (below).
@@ -276,8 +276,9 @@ static void emulate(int B, int N, int W, int CPW, int shift_w, int slot) {
 
 /* ------------------------------------------------------------ 2b. the generic stream (F != 5) */
 /* env_step.h advance_gen_kernel in place: workgroups of CPW chunks in a random order, every
- * store visible at once; the two chunks past a workgroup from the halo (copied before any
- * store), the shift by F floats read from the staged image (checked: never past it), the
+ * store visible at once; the HC chunks past a workgroup (two for F <= 8, four up to F = 16)
+ * from the halo, copied before any store as the scalar step does (halo_src: two-chunk items,
+ * item i of boundary i >> hs), the shift by F floats read from the staged image (checked: never past it), the
  * workgroup's rows g_lo .. g_hi staged one per thread (checked: at most BLOCK rows, and the
  * element walk's row index inside them), and each element's (day, channel, row) from the
  * chunk's first element plus the kernel's increments. Exact against the out-of-place advance. */
@@ -304,25 +305,27 @@ static void emulate_gen(int B, int N, int W, int F, int BLOCK, int CPW, int shif
                 ref[j] = v;
             }
     const int64_t nwg = (qtot + CPW - 1) / CPW;
-    float* halo = malloc(sizeof(float) * 8 * (size_t)nwg);
-    for (int64_t i = 0; i + 1 < nwg; ++i)                /* the scalar step's halo copy, before any store */
+    const int hs = F > 8 ? 1 : 0, HC = 2 << hs;
+    float* halo = malloc(sizeof(float) * 4 * HC * (size_t)nwg);
+    for (int64_t i = 0; i < (nwg - 1) << hs; ++i)       /* the scalar step's halo copy, before any store */
         for (int h = 0; h < 2; ++h) {
-            const int64_t q = (i + 1) * CPW + h;
+            const int64_t q = ((i >> hs) + 1) * CPW + 2 * (i & ((1 << hs) - 1)) + h;
+            CHECK(i * 8 + h * 4 + 3 < 4 * HC * nwg, "gen: halo item %lld past the buffer", (long long)i);
             for (int e = 0; e < 4; ++e) halo[i * 8 + h * 4 + e] = q < qtot ? mem[q * 4 + e] : 0.0f;
         }
     int* order = malloc(sizeof(int) * (size_t)nwg);
     shuffle(order, (int)nwg);
-    float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
+    float* lds = malloc(sizeof(float) * 4 * (CPW + HC));
     for (int o = 0; o < nwg; ++o) {
         const int64_t wg = order[o], c0 = wg * CPW;
         const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
-        for (int64_t q = 0; q < CPW + 2; ++q) {
+        for (int64_t q = 0; q < CPW + HC; ++q) {
             for (int e = 0; e < 4; ++e) lds[q * 4 + e] = 0.0f;
             if (q < nblk) {
                 CHECK(!stored[c0 + q], "gen: chunk %lld read after a store", (long long)(c0 + q));
                 for (int e = 0; e < 4; ++e) lds[q * 4 + e] = mem[(c0 + q) * 4 + e];
             } else if (q >= CPW && wg + 1 < nwg) {
-                for (int e = 0; e < 4; ++e) lds[q * 4 + e] = halo[wg * 8 + (q - CPW) * 4 + e];
+                for (int e = 0; e < 4; ++e) lds[q * 4 + e] = halo[wg * 4 * HC + (q - CPW) * 4 + e];
             }
         }
         const int64_t b_lo = c0 / per4, ql = c0 + nblk - 1, b_hi = ql / per4;
@@ -336,7 +339,7 @@ static void emulate_gen(int B, int N, int W, int F, int BLOCK, int CPW, int shif
             int64_t r = b * N + row - g_lo;
             for (int e = 0; e < 4; ++e) {
                 CHECK(r >= 0 && r <= g_hi - g_lo, "gen: row %lld outside the staged rows", (long long)r);
-                CHECK(q * 4 + e + F < 4 * (CPW + 2), "gen: shifted read past the image");
+                CHECK(q * 4 + e + F < 4 * (CPW + HC), "gen: shifted read past the image");
                 const int64_t g = g_lo + r;
                 const float sh = lds[q * 4 + e + F], un = lds[q * 4 + e];
                 const int last = t == W - 1;
@@ -547,15 +550,21 @@ static void emulate_flat1(int B, int N, int W, int CPW, int T, int storage) {
 /* step_relay.h: blocks [0, scal) are scalar blocks (EPB envs each), the rest tiles of CPW =
  * BLOCK x V chunks. A scalar block writes each env's w' as {epoch, w'} words, the counter's
  * next-step copy (kp parity 1 - q) and the canonical state. A tile stages one row per thread
- * (g_lo .. g_hi), the rows' w' from the words (it waits until they carry this step's epoch)
- * and their counter from kp parity q; in place, the two chunks past it from the halo of
- * parity q, and it writes its first two output chunks into the halo of parity 1 - q.
- * Dispatch models (a waiting tile holds its slot; a finished workgroup frees one):
- *   0  blockIdx order, 1 to 64 workgroups resident — the hardware's order, which the kernel
- *      requires (include/pmenv.h); no step may deadlock;
- *   1  a random order with every workgroup resident; no step may deadlock;
- *   2  a random order with ONE resident (negative control): returns 1 on the first
- *      deadlock, which shows the requirement is real and the detection works. */
+ * (g_lo .. g_hi), the rows' w' from the words and their counter from kp parity q; in place, the
+ * two chunks past it from the halo of parity q, and it writes its first two output chunks into
+ * the halo of parity 1 - q. A tile whose words are still missing after `spin` polls DEFERS: it
+ * stores nothing, appends itself to the step's list, re-checks once (and runs under its claim if
+ * every word arrived) and exits; every scalar block, after its units, runs each listed tile whose
+ * words have all arrived, under the tile's claim. Events are sequentially consistent here — the
+ * order the kernel builds with completion waits around the list (step_relay.h's head).
+ * Dispatch models (a polling tile holds its slot; a finished or deferred workgroup frees one):
+ *   0  blockIdx order, 1 to 64 workgroups resident (the hardware's order);
+ *   1  a random order with every workgroup resident;
+ *   2  a random order with ONE resident;
+ *   3  tiles first (the tools build's PMENV_RELAY_TILES_FIRST), 1 to 4 resident.
+ * Every tile must run exactly once per step, every env be stepped once, in every model. spin < 0
+ * removes the deferral (round 5's kernel): under model 2 it returns 1 on the first deadlock — the
+ * negative control that shows the detection works. */
 typedef struct { uint64_t* w; int32_t* kp[2]; float* halo[2]; uint32_t epoch; int par, kp_ok; const float* obs; } relay_st;
 
 static void relay_prime(relay_st* r, const float* obs, int B, const int32_t* k, int64_t ntiles, int64_t CPW,
@@ -570,7 +579,105 @@ static void relay_prime(relay_st* r, const float* obs, int B, const int32_t* k, 
         for (int b = 0; b < B; ++b) r->kp[r->par][b] = k[b];
 }
 
-static int emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, int storage, int dbuf, int model) {
+/* one step's context for the tile runs */
+typedef struct {
+    relay_st* r;
+    int B, N, W, BLOCK, storage, dbuf, q;
+    int64_t per4, qtot, CPW, ntiles, nhal;
+    const float* in; float* out; const float* bar;
+    const double* v0; const int32_t* k0;
+    uint8_t* stored; uint8_t* halo_w[2]; uint8_t* ran;
+    float* lds; float* s_wp; int32_t* s_kc;
+} relay_ctx;
+
+static void relay_rows(const relay_ctx* c, int64_t tile, int64_t* g_lo, int64_t* g_hi) {
+    const int WF = c->W * 5;
+    const int64_t c0 = tile * c->CPW, nb = c->qtot - c0 < c->CPW ? c->qtot - c0 : c->CPW;
+    const int64_t b_lo = c0 / c->per4, ql = c0 + nb - 1, b_hi = ql / c->per4;
+    *g_lo = b_lo * c->N + 4 * (c0 - b_lo * c->per4) / WF;
+    *g_hi = b_hi * c->N + (4 * (ql - b_hi * c->per4) + 3) / WF;
+}
+
+static int relay_ready(const relay_ctx* c, int64_t tile) {
+    int64_t g_lo, g_hi;
+    relay_rows(c, tile, &g_lo, &g_hi);
+    for (int64_t g = g_lo; g <= g_hi; ++g)
+        if ((uint32_t)(c->r->w[g] >> 32) != c->r->epoch) return 0;
+    return 1;
+}
+
+static void relay_run_tile(relay_ctx* c, int64_t tile) {
+    relay_st* r = c->r;
+    const int N = c->N, W = c->W, F = 5, WF = W * F, q = c->q;
+    CHECK(!c->ran[tile]++, "relay: tile %lld ran twice", (long long)tile);
+    const int64_t c0 = tile * c->CPW, CPW = c->CPW, qtot = c->qtot, per4 = c->per4;
+    const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
+    const int64_t nh = tile + 1 < c->ntiles ? (qtot - c0 - nblk < 2 ? qtot - c0 - nblk : 2) : 0;
+    for (int64_t j = 0; j < CPW + 2; ++j) {
+        for (int e = 0; e < 4; ++e) c->lds[j * 4 + e] = 0.0f;
+        if (j < nblk) {
+            CHECK(c->dbuf || !c->stored[c0 + j], "relay: chunk %lld read after a store", (long long)(c0 + j));
+            for (int e = 0; e < 4; ++e) c->lds[j * 4 + e] = c->in[(c0 + j) * 4 + e];
+        } else if (j >= CPW && j - CPW < nh) {
+            if (c->dbuf) {
+                for (int e = 0; e < 4; ++e) c->lds[j * 4 + e] = c->in[(c0 + nblk + j - CPW) * 4 + e];
+            } else {
+                CHECK(!c->halo_w[q][tile], "relay: halo %lld read after this step wrote it", (long long)tile);
+                CHECK(tile * 8 + (j - CPW) * 4 + 3 < c->nhal, "relay: halo index past its buffer");
+                for (int e = 0; e < 4; ++e) c->lds[j * 4 + e] = r->halo[q][tile * 8 + (j - CPW) * 4 + e];
+            }
+        }
+    }
+    int64_t g_lo, g_hi;
+    relay_rows(c, tile, &g_lo, &g_hi);
+    CHECK(g_hi - g_lo < c->BLOCK, "relay: tile %lld stages %lld rows > %d threads", (long long)tile,
+          (long long)(g_hi - g_lo + 1), c->BLOCK);
+    for (int64_t g = g_lo; g <= g_hi && g - g_lo < c->BLOCK; ++g) {
+        const int64_t b = g / N;
+        CHECK(g < (int64_t)c->B * N, "relay: row %lld past the batch", (long long)g);
+        CHECK((uint32_t)(r->w[g] >> 32) == r->epoch, "relay: tile %lld ran before row %lld's word", (long long)tile,
+              (long long)g);
+        c->s_kc[g - g_lo] = r->kp[q][b];
+        c->s_wp[g - g_lo] = flat1_wp(c->v0[b], c->k0[b], b, (int)(g - b * N));   /* what the word carries */
+    }
+    for (int64_t j = 0; j < nblk; ++j) {
+        const int64_t gq = c0 + j, bq = gq / per4, j0 = 4 * (gq - bq * per4), row = j0 / WF;
+        const int kk = (int)(j0 - row * WF);
+        const int64_t li = bq * N + row - g_lo;
+        CHECK(li >= 0 && li <= g_hi - g_lo, "relay: chunk %lld row index %lld", (long long)gq, (long long)li);
+        const int32_t kc = c->s_kc[li];
+        CHECK(kc == c->k0[bq], "relay: env %lld counter copy %d != %d", (long long)bq, kc, c->k0[bq]);
+        const int shift_w = !(c->storage && kc >= W - 1), slot = (int)((1 + (int64_t)kc) % W);
+        for (int e = 0; e < 4; ++e) {
+            const int pos = kk + e;
+            const int64_t jg = gq * 4 + e, rg = jg / WF;
+            const int f = (int)((jg - rg * WF) % F), td = (int)((jg - rg * WF) / F);
+            const float un = c->lds[j * 4 + e], sh = c->lds[j * 4 + e + 5];
+            float v;
+            if (pos >= WF) v = sh;                                   /* the next row's positions 0..2 */
+            else if (f == F - 1) v = shift_w ? (td == W - 1 ? c->s_wp[li] : sh) : (td == slot ? c->s_wp[li] : un);
+            else v = td == W - 1 ? c->bar[rg * 4 + f] : sh;
+            c->out[jg] = v;
+            if (!c->dbuf && tile > 0 && j < 2) {
+                CHECK((tile - 1) * 8 + j * 4 + e < c->nhal, "relay: halo_out index past its buffer");
+                r->halo[1 - q][(tile - 1) * 8 + j * 4 + e] = v;
+            }
+        }
+        c->stored[gq] = 1;
+    }
+    if (!c->dbuf && tile > 0) c->halo_w[1 - q][tile - 1] = 1;
+}
+
+/* a deferred tile's run (relay_tile<ADOPT>): all words arrived and the claim won */
+static void relay_adopt_one(relay_ctx* c, uint32_t* done, int64_t tile) {
+    if (!relay_ready(c, tile)) return;
+    if (done[tile] == c->r->epoch) return;                  /* the claim: ran elsewhere */
+    done[tile] = c->r->epoch;
+    relay_run_tile(c, tile);
+}
+
+static int emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, int storage, int dbuf, int model,
+                         int spin) {
     const int F = 5, WF = W * F;
     const int64_t per = (int64_t)N * WF, tot = per * B;
     if (per % 4 || W < 2) return 0;
@@ -594,16 +701,22 @@ static int emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, i
     r.halo[0] = malloc(sizeof(float) * nhal); r.halo[1] = malloc(sizeof(float) * nhal);
     const int grid = scal + (int)ntiles;
     r.epoch = 0xFFFFFFFDu; r.par = 0; r.kp_ok = 0; r.obs = NULL;
-    int deadlocked = 0;
+    int deadlocked = 0, deferred = 0;
+    uint32_t* done = calloc((size_t)ntiles, sizeof(uint32_t));
+    int64_t* list = malloc(sizeof(int64_t) * (size_t)ntiles);
     uint8_t* stored = calloc((size_t)qtot, 1);
     uint8_t* halo_w[2] = {calloc((size_t)ntiles, 1), calloc((size_t)ntiles, 1)};   /* written this step, per parity */
+    uint8_t* ran = calloc((size_t)ntiles, 1);
     uint8_t* scal_owner = calloc((size_t)B, 1);
-    int* runnable = malloc(sizeof(int) * (size_t)(scal + ntiles));
-    int* order = malloc(sizeof(int) * (size_t)(scal + ntiles));
-    int* res_idx = malloc(sizeof(int) * (size_t)(scal + ntiles));      /* resident workgroups */
-    float* lds = malloc(sizeof(float) * 4 * (CPW + 2));
-    float* s_wp = malloc(sizeof(float) * BLOCK);
-    int32_t* s_kc = malloc(sizeof(int32_t) * BLOCK);
+    int* polls = malloc(sizeof(int) * (size_t)grid);
+    int* order = malloc(sizeof(int) * (size_t)grid);
+    int* res_idx = malloc(sizeof(int) * (size_t)grid);  /* resident workgroups */
+    relay_ctx c;
+    c.r = &r; c.B = B; c.N = N; c.W = W; c.BLOCK = BLOCK; c.storage = storage; c.dbuf = dbuf;
+    c.per4 = per4; c.qtot = qtot; c.CPW = CPW; c.ntiles = ntiles; c.nhal = nhal; c.bar = bar; c.v0 = v0; c.k0 = k0;
+    c.stored = stored; c.halo_w[0] = halo_w[0]; c.halo_w[1] = halo_w[1]; c.ran = ran;
+    c.lds = malloc(sizeof(float) * 4 * (CPW + 2)); c.s_wp = malloc(sizeof(float) * BLOCK);
+    c.s_kc = malloc(sizeof(int32_t) * BLOCK);
     int cur = 0;
     for (int64_t i = 0; i < tot; ++i) buf[0][i] = ref[i] = (float)nrand();
     for (int b = 0; b < B; ++b) { value[b] = 25000.0 + b; k[b] = (int32_t)(urand() * 2 * W); }
@@ -631,121 +744,88 @@ static int emulate_relay(int B, int N, int W, int BLOCK, int V, int KL, int T, i
             for (int b = 0; b < B; ++b) { value[b] = value[b] * 1.0001 + 1.0; k[b] += 1; }
             r.obs = NULL; r.kp_ok = 0;
         } else {
-            /* launch_relay: prime, next epoch (the words restart at 0 on the wrap) */
+            /* launch_relay: prime, next epoch (the words, list and claims restart at 0 on the wrap) */
             relay_prime(&r, in, B, k, ntiles, CPW, qtot, !dbuf && r.obs != in);
-            if (++r.epoch == 0) { memset(r.w, 0, sizeof(uint64_t) * (size_t)B * N); r.epoch = 1; }
+            if (++r.epoch == 0) {
+                memset(r.w, 0, sizeof(uint64_t) * (size_t)B * N);
+                memset(done, 0, sizeof(uint32_t) * (size_t)ntiles);
+                r.epoch = 1;
+            }
             const int q = r.par;
+            c.q = q; c.in = in; c.out = out;
+            int nlist = 0;
             if (model == 0) for (int i = 0; i < grid; ++i) order[i] = i;
+            else if (model == 3) for (int i = 0; i < grid; ++i) order[i] = (i + scal) % grid;   /* blockIdx + rot */
             else shuffle(order, grid);
-            const int resident = model == 0 ? 1 + (int)(urand() * (t % 3 == 0 ? 4 : 64)) : model == 1 ? grid : 1;
+            const int resident = model == 0 ? 1 + (int)(urand() * (t % 3 == 0 ? 4 : 64))
+                               : model == 1 ? grid : model == 2 ? 1 : 1 + (int)(urand() * 4);
             int next = 0, live = 0;
             memset(stored, 0, (size_t)qtot); memset(halo_w[0], 0, (size_t)ntiles); memset(halo_w[1], 0, (size_t)ntiles);
-            memset(scal_owner, 0, (size_t)B);
-            for (int left = grid; left > 0; --left) {
+            memset(scal_owner, 0, (size_t)B); memset(ran, 0, (size_t)ntiles);
+            for (int i = 0; i < grid; ++i) polls[i] = 0;
+            for (int left = grid; left > 0;) {
                 while (live < resident && next < grid) res_idx[live++] = order[next++];
-                int nr = 0;
-                for (int s2 = 0; s2 < live; ++s2) {
+                /* a workgroup that can move: a scalar block, or a tile (it runs, polls or defers); without
+                 * the deferral (spin < 0) a tile whose words are missing cannot */
+                int s2 = (int)(urand() * live), moved = 0;
+                for (int tries = 0; tries < live && !moved; ++tries) {
+                    if (tries) s2 = (s2 + 1) % live;
                     const int i = res_idx[s2];
-                    if (i >= scal) {                    /* a tile waits for its rows' words */
-                        const int64_t c0 = (int64_t)(i - scal) * CPW, nb = qtot - c0 < CPW ? qtot - c0 : CPW;
-                        const int64_t b_lo = c0 / per4, g_lo = b_lo * N + 4 * (c0 - b_lo * per4) / WF;
-                        const int64_t ql = c0 + nb - 1, b_hi = ql / per4, g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
-                        int ready = 1;
-                        for (int64_t g = g_lo; g <= g_hi && ready; ++g) ready = (uint32_t)(r.w[g] >> 32) == r.epoch;
-                        if (!ready) continue;
-                    }
-                    runnable[nr++] = s2;
-                }
-                if (!nr && model == 2) { deadlocked = 1; break; }
-                CHECK(nr > 0, "relay: deadlock, %d resident workgroups all wait (B%d N%d W%d model %d)", live, B, N, W,
-                      model);
-                if (!nr) break;
-                const int slot_r = runnable[(int)(urand() * nr)];
-                const int i = res_idx[slot_r];
-                res_idx[slot_r] = res_idx[--live];
-                if (i < scal) {                         /* relay_scalar */
-                    for (int j = 0; j < EPB; ++j) {
-                        const int b = i * EPB + j;
-                        if (b >= B) continue;
-                        CHECK(!scal_owner[b]++, "relay: env %d stepped twice", b);
-                        for (int n = 0; n < N; ++n)
-                            r.w[(size_t)b * N + n] = ((uint64_t)r.epoch << 32) | 0u;   /* the tag; w' below */
-                        r.kp[1 - q][b] = k[b] + 1;                     /* parity 1 - q: no tile reads it */
-                        value[b] = value[b] * 1.0001 + 1.0;                            /* scalar_tail */
-                        k[b] += 1;
-                    }
-                    continue;
-                }
-                const int64_t tile = i - scal, c0 = tile * CPW;
-                const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
-                const int64_t nh = tile + 1 < ntiles ? (qtot - c0 - nblk < 2 ? qtot - c0 - nblk : 2) : 0;
-                for (int64_t j = 0; j < CPW + 2; ++j) {
-                    for (int e = 0; e < 4; ++e) lds[j * 4 + e] = 0.0f;
-                    if (j < nblk) {
-                        CHECK(dbuf || !stored[c0 + j], "relay: chunk %lld read after a store", (long long)(c0 + j));
-                        for (int e = 0; e < 4; ++e) lds[j * 4 + e] = in[(c0 + j) * 4 + e];
-                    } else if (j >= CPW && j - CPW < nh) {
-                        if (dbuf) {
-                            for (int e = 0; e < 4; ++e) lds[j * 4 + e] = in[(c0 + nblk + j - CPW) * 4 + e];
-                        } else {
-                            CHECK(!halo_w[q][tile], "relay: halo %lld read after this step wrote it", (long long)tile);
-                            CHECK(tile * 8 + (j - CPW) * 4 + 3 < nhal, "relay: halo index past its buffer");
-                            for (int e = 0; e < 4; ++e) lds[j * 4 + e] = r.halo[q][tile * 8 + (j - CPW) * 4 + e];
+                    if (i < scal) {                     /* relay_scalar, then relay_adopt */
+                        for (int j = 0; j < EPB; ++j) {
+                            const int b = i * EPB + j;
+                            if (b >= B) continue;
+                            CHECK(!scal_owner[b]++, "relay: env %d stepped twice", b);
+                            for (int n = 0; n < N; ++n) r.w[(size_t)b * N + n] = ((uint64_t)r.epoch << 32) | 0u;
+                            r.kp[1 - q][b] = k[b] + 1;          /* parity 1 - q: no tile reads it */
+                            value[b] = value[b] * 1.0001 + 1.0; /* scalar_tail */
+                            k[b] += 1;
+                        }
+                        for (int e = 0; e < nlist; ++e) relay_adopt_one(&c, done, list[e]);
+                    } else {
+                        const int64_t tile = i - scal;
+                        if (polls[i] <= spin && relay_ready(&c, tile)) {
+                            relay_run_tile(&c, tile);
+                        } else if (spin < 0) {
+                            continue;                   /* waits without bound */
+                        } else if (polls[i]++ <= spin) {
+                            moved = 1;                  /* a poll (the last one gives up): the tile stays */
+                            break;
+                        } else {                        /* relay_defer, a later event: append, re-check once, exit */
+                            CHECK(nlist < ntiles, "relay: deferral list past its %lld entries", (long long)ntiles);
+                            list[nlist++] = tile;
+                            ++deferred;
+                            relay_adopt_one(&c, done, tile);
                         }
                     }
+                    res_idx[s2] = res_idx[--live]; --left;
+                    moved = 1;
                 }
-                const int64_t b_lo = c0 / per4, g_lo = b_lo * N + 4 * (c0 - b_lo * per4) / WF;
-                const int64_t ql = c0 + nblk - 1, b_hi = ql / per4, g_hi = b_hi * N + (4 * (ql - b_hi * per4) + 3) / WF;
-                CHECK(g_hi - g_lo < BLOCK, "relay: tile %lld stages %lld rows > %d threads", (long long)tile,
-                      (long long)(g_hi - g_lo + 1), BLOCK);
-                for (int64_t g = g_lo; g <= g_hi && g - g_lo < BLOCK; ++g) {
-                    const int64_t b = g / N;
-                    CHECK(g < (int64_t)B * N, "relay: row %lld past the batch", (long long)g);
-                    s_kc[g - g_lo] = r.kp[q][b];
-                    s_wp[g - g_lo] = flat1_wp(v0[b], k0[b], b, (int)(g - b * N));   /* what the word carries */
-                }
-                for (int64_t j = 0; j < nblk; ++j) {
-                    const int64_t gq = c0 + j, bq = gq / per4, j0 = 4 * (gq - bq * per4), row = j0 / WF;
-                    const int kk = (int)(j0 - row * WF);
-                    const int64_t li = bq * N + row - g_lo;
-                    CHECK(li >= 0 && li <= g_hi - g_lo, "relay: chunk %lld row index %lld", (long long)gq, (long long)li);
-                    const int32_t kc = s_kc[li];
-                    CHECK(kc == k0[bq], "relay: env %lld counter copy %d != %d", (long long)bq, kc, k0[bq]);
-                    const int shift_w = !(storage && kc >= W - 1), slot = (int)((1 + (int64_t)kc) % W);
-                    for (int e = 0; e < 4; ++e) {
-                        const int pos = kk + e;
-                        const int64_t jg = gq * 4 + e, rg = jg / WF;
-                        const int f = (int)((jg - rg * WF) % F), td = (int)((jg - rg * WF) / F);
-                        const float un = lds[j * 4 + e], sh = lds[j * 4 + e + 5];
-                        float v;
-                        if (pos >= WF) v = sh;                                   /* the next row's positions 0..2 */
-                        else if (f == F - 1) v = shift_w ? (td == W - 1 ? s_wp[li] : sh) : (td == slot ? s_wp[li] : un);
-                        else v = td == W - 1 ? bar[rg * 4 + f] : sh;
-                        out[jg] = v;
-                        if (!dbuf && tile > 0 && j < 2) {
-                            CHECK((tile - 1) * 8 + j * 4 + e < nhal, "relay: halo_out index past its buffer");
-                            r.halo[1 - q][(tile - 1) * 8 + j * 4 + e] = v;
-                        }
-                    }
-                    stored[gq] = 1;
-                }
-                if (!dbuf && tile > 0) halo_w[1 - q][tile - 1] = 1;
+                if (!moved && spin < 0 && model == 2) { deadlocked = 1; break; }
+                CHECK(moved, "relay: deadlock, %d resident workgroups all wait (B%d N%d W%d model %d spin %d)", live, B,
+                      N, W, model, spin);
+                if (!moved) break;
             }
             if (deadlocked) break;
             for (int b = 0; b < B; ++b) CHECK(scal_owner[b] == 1, "relay: env %d stepped %d times", b, scal_owner[b]);
+            for (int64_t i = 0; i < ntiles; ++i) CHECK(ran[i] == 1, "relay: tile %lld ran %d times (model %d)", (long long)i,
+                                                       ran[i], model);
             r.par = 1 - q; r.kp_ok = 1; r.obs = dbuf ? NULL : out;
         }
         float* sw = ref; ref = nxt; nxt = sw;
         for (int64_t i = 0; i < tot; ++i)
             if (memcmp(&out[i], &ref[i], 4)) {
-                CHECK(0, "relay: step %d float %lld differs (B%d N%d W%d %dx%d db%d)", t, (long long)i, B, N, W, BLOCK, V, dbuf);
+                CHECK(0, "relay: step %d float %lld differs (B%d N%d W%d %dx%d db%d model %d)", t, (long long)i, B, N, W,
+                      BLOCK, V, dbuf, model);
                 break;
             }
         if (dbuf) cur = 1 - cur;
     }
     free(buf[0]); free(buf[1]); free(ref); free(nxt); free(bar); free(wp); free(value); free(k); free(k0); free(v0);
-    free(r.w); free(r.kp[0]); free(r.kp[1]); free(r.halo[0]); free(r.halo[1]); free(stored); free(halo_w[0]); free(halo_w[1]);
-    free(scal_owner); free(runnable); free(order); free(res_idx); free(lds); free(s_wp); free(s_kc);
+    free(r.w); free(r.kp[0]); free(r.kp[1]); free(r.halo[0]); free(r.halo[1]); free(stored); free(halo_w[0]);
+    free(halo_w[1]); free(ran); free(done); free(list); free(scal_owner); free(polls); free(order); free(res_idx);
+    free(c.lds); free(c.s_wp); free(c.s_kc);
+    if (model >= 2 && spin >= 0) CHECK(deferred > 0, "relay: model %d never exercised the deferral", model);
     return deadlocked;
 }
 
@@ -1101,7 +1181,10 @@ int main(void) {
      * tools build's), and small ones (64 threads x 1) that put many envs and rows in one tile,
      * both weight-channel modes */
     const int gshp[][4] = {{4, 30, 50, 8}, {11, 8, 10, 3}, {9, 5, 12, 2}, {13, 9, 8, 4}, {7, 3, 20, 6},
-                           {5, 11, 4, 7}, {3, 64, 16, 8}, {2, 65, 16, 4}, {40, 2, 10, 6}};
+                           {5, 11, 4, 7}, {3, 64, 16, 8}, {2, 65, 16, 4}, {40, 2, 10, 6},
+                           /* past F = 8: the four-chunk halo */
+                           {3, 30, 50, 12}, {5, 7, 10, 16}, {9, 5, 4, 9}, {11, 3, 6, 10}, {4, 13, 3, 13},
+                           {6, 9, 2, 14}, {3, 20, 8, 11}, {2, 16, 32, 15}};
     for (size_t i = 0; i < sizeof gshp / sizeof gshp[0]; ++i)
         for (int mode = 0; mode < 2; ++mode) {
             const int B = gshp[i][0], N = gshp[i][1], W = gshp[i][2], F = gshp[i][3];
@@ -1131,23 +1214,23 @@ int main(void) {
     /* the relayed step: the product's 256 x 2 and 512 x 2 tiles, small tiles that put many
      * rows and envs in one tile, the register (32 / 64 lanes) and packed (8 / 16 lanes)
      * scalar forms' blocks, W = 2 (every day a last day), both ring orders, in place and
-     * double-buffered */
+     * double-buffered; every dispatch model, the fallback after 0 to 3 polls */
     const int rshapes[][4] = {{37, 30, 50, 32}, {301, 8, 12, 8}, {97, 16, 20, 16}, {9, 64, 47, 64}, {400, 30, 2, 32},
-                              {13, 5, 48, 8}, {3, 1, 600, 8}};
+                              {13, 5, 48, 8}, {3, 1, 600, 8}, {61, 24, 3, 32}};
+    const int bks[3] = {256, 512, 64};
     for (size_t i = 0; i < sizeof rshapes / sizeof rshapes[0]; ++i)
         for (int storage = 0; storage < 2; ++storage)
             for (int db = 0; db < 2; ++db)
-                for (int model = 0; model < 2; ++model) {     /* blockIdx order, limited residency; any order, all resident */
-                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 256, 2, rshapes[i][3], 12, storage, db, model);
-                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 512, 2, rshapes[i][3], 12, storage, db, model);
-                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 64, 2, rshapes[i][3], 12, storage, db, model);
-                }
-    /* negative control: a non-monotone dispatch order with one workgroup resident deadlocks the
-     * blockIdx-role kernel (a tile dispatched before its scalar block waits forever) — the
-     * requirement include/pmenv.h states is real, and the detection above sees it */
+                for (int model = 0; model < 4; ++model)
+                    for (int bk = 0; bk < 3; ++bk)
+                        emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], bks[bk], 2, rshapes[i][3], 12, storage,
+                                      db, model, (int)(urand() * 4));
+    /* negative control: without the fallback (round 5's kernel), a non-monotone dispatch order with
+     * one workgroup resident deadlocks (a tile dispatched before its scalar block waits forever) —
+     * the detection above sees a deadlock when there is one */
     int dl = 0;
-    for (int rep = 0; rep < 8 && !dl; ++rep) dl = emulate_relay(37, 30, 50, 64, 2, 32, 3, 1, 0, 2);
-    CHECK(dl, "relay: no deadlock under a non-monotone order with one resident workgroup (negative control)");
+    for (int rep = 0; rep < 8 && !dl; ++rep) dl = emulate_relay(37, 30, 50, 64, 2, 32, 3, 1, 0, 2, -1);
+    CHECK(dl, "relay: no deadlock without the fallback under a non-monotone order, one resident (negative control)");
     /* the look-back GAE: the product's rule and both chunk lengths, ragged B and T, one chunk */
     const int gshapes[][2] = {{700, 67}, {513, 3}, {1000, 130}, {600, 64}, {130, 5}};
     for (size_t i = 0; i < sizeof gshapes / sizeof gshapes[0]; ++i) {

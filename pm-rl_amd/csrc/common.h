@@ -10,6 +10,10 @@
 namespace pmenv_dev {
 
 constexpr int kWideMaxAssets = 512;   // the widest env the packed scalar step and the wide flat step take
+// polls of a missing relay word before a tile defers (step_relay.h): each is an s_sleep plus an
+// agent-scope load round trip (~1 us under the stream), so ~1 ms — two orders of magnitude above
+// the scalar blocks' whole run, reached only when they were not dispatched ahead of the tile
+constexpr uint32_t kRelaySpin = 1024;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));   // dword-aligned 16-B access
@@ -67,6 +71,8 @@ struct StepParams {
     // first two chunks here (advance_flat_inplace_kernel's halo); null: no copy
     float* halo;
     uint32_t halo_wgs, halo_block, halo_qtot;
+    uint32_t halo_hs;      // log2 of the two-chunk items per workgroup boundary: 0 (two chunks,
+                           // every F <= 8 stream), 1 (four: the generic stream past F = 8)
     // one-launch flat step (step_flat.h): the state snapshot the scalar step reads
     // (parity p: value, counter, get_last(), last close) and the one the env's owner
     // writes for the next step (parity 1 - p); in place, the halo of this step and the

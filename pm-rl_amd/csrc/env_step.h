@@ -597,6 +597,11 @@ struct HaloRegs {
     bool d0, d1;
 };
 
+// halo item i (two chunks): boundary i >> halo_hs, chunks 2 (i & (2^hs - 1)) + {0, 1} past it
+__device__ __forceinline__ uint32_t halo_src(const StepParams& p, uint32_t i) {
+    return ((i >> p.halo_hs) + 1u) * p.halo_block + 2u * (i & ((1u << p.halo_hs) - 1u));
+}
+
 __device__ __forceinline__ HaloRegs halo_load(const StepParams& p) {
     HaloRegs h;
     const uint32_t nthr = gridDim.x * blockDim.x, gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -607,7 +612,7 @@ __device__ __forceinline__ HaloRegs halo_load(const StepParams& p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const bool d = t ? h.d1 : h.d0;
-        const uint32_t q = (gid + t * nthr + 1) * p.halo_block;
+        const uint32_t q = halo_src(p, gid + t * nthr);
         h.v[2 * t] = d && q < p.halo_qtot ? src[q] : z;
         h.v[2 * t + 1] = d && q + 1 < p.halo_qtot ? src[q + 1] : z;
     }
@@ -622,7 +627,7 @@ __device__ __forceinline__ void halo_store(const StepParams& p, const HaloRegs& 
     if (h.d1) { dst[2 * (gid + nthr)] = h.v[2]; dst[2 * (gid + nthr) + 1] = h.v[3]; }
     const f4* src = reinterpret_cast<const f4*>(p.obs);
     for (uint32_t i = gid + 2 * nthr; i < p.halo_wgs; i += nthr) {
-        const uint32_t q = (i + 1) * p.halo_block;
+        const uint32_t q = halo_src(p, i);
         dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
         dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1323,7 +1328,7 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
     const f4* src = reinterpret_cast<const f4*>(p.obs);
     f4* dst = reinterpret_cast<f4*>(p.halo);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.halo_wgs; i += nthr) {
-        const uint32_t q = (i + 1) * p.halo_block;
+        const uint32_t q = halo_src(p, i);
         dst[2 * i] = q < p.halo_qtot ? src[q] : f4{0.f, 0.f, 0.f, 0.f};
         dst[2 * i + 1] = q + 1 < p.halo_qtot ? src[q + 1] : f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1331,9 +1336,11 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
 
 // ---------------------------------------------------------------- K2 for F != 5: the generic stream
 // The two-launch step's window stream for the channel counts the F = 5 streams do not take
-// (2 <= F <= 8, F != 5; 16-B granular env windows): flat_wg_body_patch's workgroup layout —
-// BLOCK x V chunks of the flat [B, N, W, F] tensor staged in LDS, the two chunks past the
-// workgroup read from `halo` in place (copied by the scalar step of the same step) or from
+// (2 <= F <= 16, F != 5; 16-B granular env windows): flat_wg_body_patch's workgroup layout —
+// BLOCK x V chunks of the flat [B, N, W, F] tensor staged in LDS, the HC chunks past the
+// workgroup that a shift by F floats reads (two for F <= 8, four up to 16: FMAX — the
+// reference loader's width grows past 8 with every indicator of config/base.py:30-44,
+// data/data_loader.py:48) read from `halo` in place (copied by the scalar step of the same step) or from
 // obs double-buffered — with the shift by F floats read from LDS dword-wise and every
 // element composed from its own (day, channel) (weight_buffer.py:32-44, instrument.py:339-356):
 //   market f < F-1:  t < W-1 ? in[n, t+1, f] : bar[n, f]
@@ -1352,12 +1359,14 @@ __device__ __forceinline__ void copy_halo(const StepParams& p) {
 // POL: the window stream's cache policy (the own-chunk loads and the stores), as the F = 5
 // streams: 0 default, 1 nt (windows past the Infinity Cache). ABL (tools build, timing
 // only): 1 no side-data loads, 2 no compose (the shifted source stored), 4 no shifted read.
-template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0, int ABL = 0>
+template <int BLOCK, int V, bool OUT, int SHV = 1, bool TWO = true, int POL = 0, int ABL = 0, int FMAX = 8>
 __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32_t qtot, uint32_t rows) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V;
-    constexpr int kFm = 7;                                   // bar floats per staged row (F <= 8)
-    __shared__ f4 sh4[CPW + 2];
+    constexpr int kFm = FMAX - 1;                            // bar floats per staged row (F <= FMAX)
+    constexpr int HC = FMAX > 8 ? 4 : 2;                     // chunks past the workgroup the shift reads
+    static_assert(FMAX == 8 || FMAX == 16, "F <= 8: two chunks past a workgroup; F <= 16: four");
+    __shared__ f4 sh4[CPW + HC];
     // the rows' side data, sized by the plan's bound on rows per workgroup (4 CPW / (W F) + 2:
     // a dozen at W F = 400) rather than BLOCK — more workgroups per CU, more bytes in flight
     extern __shared__ float gside[];
@@ -1371,10 +1380,10 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     f4 own[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, (uint32_t)(64 * V * wave + 64 * v + lane) * 16u);
-    // (no halo buffer in place: nothing is read, the two chunks stay 0)
-    const uint32_t nh = blockIdx.x + 1 < gridDim.x && (OUT || p.halo) ? min(2u, qtot - c0 - nblk) : 0u;
-    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : (p.halo ? p.halo + (size_t)blockIdx.x * 8 : p.obs);
-    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < 2 ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
+    // (no halo buffer in place: nothing is read, the HC chunks stay 0)
+    const uint32_t nh = blockIdx.x + 1 < gridDim.x && (OUT || p.halo) ? min((uint32_t)HC, qtot - c0 - nblk) : 0u;
+    const float* hsrc = OUT ? p.obs + (size_t)(c0 + nblk) * 4 : (p.halo ? p.halo + (size_t)blockIdx.x * 4 * HC : p.obs);
+    const f4 hal = buf_load4<0>(make_rsrc(hsrc, nh * 16u), tid < HC ? (uint32_t)tid * 16u : 0xFFFFFFF0u);
     __builtin_amdgcn_sched_barrier(0);
     const int N = p.N, W = p.W, F = p.F, Fm = F - 1, WF = W * F;
     const uint32_t per4 = (uint32_t)(N * WF) >> 2;
@@ -1407,7 +1416,7 @@ __global__ __launch_bounds__(BLOCK) void advance_gen_kernel(StepParams p, uint32
     }
 #pragma unroll
     for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
-    if (tid < 2) sh4[CPW + tid] = hal;
+    if (tid < HC) sh4[CPW + tid] = hal;
     __syncthreads();
     const float* shf = reinterpret_cast<const float*>(sh4);
     const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
@@ -1712,7 +1721,7 @@ __global__ __launch_bounds__(BLOCK) void step_small_kernel(StepParams p) {
 // wave, and no f64 tail after the window's stores. Same values, element by element.
 template <int BLOCK, int E>
 __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
-    static_assert(E % 4 == 0 && E <= 8 && BLOCK >= 256, "16-B chunks, at most two per thread; 2 BLOCK >= 64 x 7 bar floats");
+    static_assert(E % 4 == 0 && E <= 8 && BLOCK >= 256, "16-B chunks, at most two per thread");
     constexpr int Q = E / 4;                               // chunks per thread
     extern __shared__ __attribute__((aligned(16))) float lds[];   // [NWF + 8] window | [N (F-1)] bar
     __shared__ float sh_wp[64];
@@ -1737,7 +1746,7 @@ __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
     }
     const uint32_t jt = nq * 4u + (uint32_t)tid;            // the block's last NWF % 4 floats
     const float tl = buf_load1(rs_in, jt < NWF ? jt * 4u : kOut);
-    // the bar: N (F - 1) <= 64 x 7 floats, two per thread (BLOCK >= 256)
+    // the bar: N (F - 1) <= 2 BLOCK floats (the plan: pmenv.hip), two per thread
     const float bv0 = buf_load1(rs_bar, (uint32_t)tid < nbar ? (uint32_t)tid * 4u : kOut);
     const float bv1 = buf_load1(rs_bar, (uint32_t)(tid + BLOCK) < nbar ? (uint32_t)(tid + BLOCK) * 4u : kOut);
     float* lbar = lds + NWF + 8;

@@ -97,10 +97,12 @@ struct pmenv {
     int relay_block, relay_v; // the tiles' geometry: relay_block threads x relay_v 16-B chunks
     int relay_epb;        // envs per scalar block (relay_block / 64 waves x 64 / relay_kl envs)
     uint32_t relay_tiles, relay_scal;
-    void* relay_mem;      // control words | relay words | counter copy x 2 | halo x 2 (allocated when
+    void* relay_mem;      // control words | relay words, deferral list, tile claims | counter copy x 2 | halo x 2 (allocated when
                           // AUTO gives the shape the relay step or pmenv_set_step_path asks for it)
     uint32_t* relay_seq;  // device-sequenced words {D, E, V, C, EC, pad, HOBS lo, HOBS hi} (step_relay.h)
     uint64_t* relay_w;    // [B * N] {epoch, w'}
+    uint64_t* relay_list; // the deferral list: [0] {epoch, count}, [1 .. relay_tiles] {epoch, tile}
+    uint32_t* relay_done; // [relay_tiles] the epoch in which each deferred tile last ran
     int32_t* relay_kp;    // [2][B] the counter copies, per parity
     float* relay_halo;    // in place: [2][relay_halo_stride] floats
     uint32_t relay_halo_stride;
@@ -175,6 +177,12 @@ inline pmenv_dev::StepParams base_params(const pmenv* h) {
 }
 
 inline bool aligned4(const void* ptr) { return ((uintptr_t)ptr & 3u) == 0; }
+
+// the relay step's deferral list ({epoch, count} + one entry per tile) and tile claims, 16-B padded
+inline size_t relay_list_bytes(const pmenv* h) {
+    const size_t tiles = h->relay_tiles;
+    return ((tiles + 1) * 8 + 15) / 16 * 16 + (tiles * 4 + 15) / 16 * 16;
+}
 
 inline int check_launch(pmenv* h, const char* what) {
     hipError_t e = hipGetLastError();

@@ -107,7 +107,8 @@ inline void launch_scalar(const pmenv* h, StepParams p, hipStream_t stream) {
         p.halo_qtot = h->flat_qtot;
     } else if (p.obs_out == p.obs && (h->gen & PMENV_FUSE_INPLACE)) {   // the generic stream's halo
         p.halo = h->halo;
-        p.halo_wgs = h->halo_wgs;
+        p.halo_hs = h->cfg.features > 8 ? 1u : 0u;   // four chunks per workgroup past F = 8
+        p.halo_wgs = h->halo_wgs << p.halo_hs;
         p.halo_block = (uint32_t)(h->gen_block * h->gen_v);
         p.halo_qtot = h->gen_qtot;
     }
@@ -130,30 +131,39 @@ inline void launch_surface_stream(const pmenv* h, StepParams p, hipStream_t stre
 inline uint32_t gen_rows(const pmenv* h, int cpw) {
     return (uint32_t)(4 * (int64_t)cpw / ((int64_t)h->cfg.window * h->cfg.features) + 2);
 }
-template <int BLOCK, int V, int SHV>
+template <int BLOCK, int V, int SHV, int FMAX>
 inline void launch_gen_s(const pmenv* h, const StepParams& p, hipStream_t stream) {
     const unsigned grid = (unsigned)((h->gen_qtot + BLOCK * V - 1) / (BLOCK * V));
     const uint32_t rows = gen_rows(h, BLOCK * V);
-    const size_t lds = (size_t)rows * (2 + 7) * 4;
+    const size_t lds = (size_t)rows * (2 + (FMAX - 1)) * 4;
     // nt past the Infinity Cache: the F = 5 streams' rule (flat_ip_pol / flat_pol, pmenv.hip)
     if (p.obs_out == p.obs) {
-        if (h->flat_ip_pol) advance_gen_kernel<BLOCK, V, false, SHV, true, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
-        else advance_gen_kernel<BLOCK, V, false, SHV><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        if (h->flat_ip_pol)
+            advance_gen_kernel<BLOCK, V, false, SHV, true, 1, 0, FMAX><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else
+            advance_gen_kernel<BLOCK, V, false, SHV, true, 0, 0, FMAX><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
     } else {
-        if (h->flat_pol) advance_gen_kernel<BLOCK, V, true, SHV, true, 1><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
-        else advance_gen_kernel<BLOCK, V, true, SHV><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        if (h->flat_pol)
+            advance_gen_kernel<BLOCK, V, true, SHV, true, 1, 0, FMAX><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
+        else
+            advance_gen_kernel<BLOCK, V, true, SHV, true, 0, 0, FMAX><<<grid, BLOCK, lds, stream>>>(p, h->gen_qtot, rows);
     }
+}
+template <int BLOCK, int V, int FMAX>
+inline void launch_gen_f(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    const int fm4 = h->cfg.features % 4;   // the shifted source's LDS reads: 16 B (F % 4 = 0), 8 B (F % 4 = 2), dwords
+    if (fm4 == 0) launch_gen_s<BLOCK, V, 4, FMAX>(h, p, stream);
+    else if (fm4 == 2) launch_gen_s<BLOCK, V, 2, FMAX>(h, p, stream);
+    else launch_gen_s<BLOCK, V, 1, FMAX>(h, p, stream);
 }
 template <int BLOCK, int V>
 inline void launch_gen_g(const pmenv* h, const StepParams& p, hipStream_t stream) {
-    const int fm4 = h->cfg.features % 4;   // the shifted source's LDS reads: 16 B (F = 4, 8), 8 B (F = 2, 6), dwords
-    if (fm4 == 0) launch_gen_s<BLOCK, V, 4>(h, p, stream);
-    else if (fm4 == 2) launch_gen_s<BLOCK, V, 2>(h, p, stream);
-    else launch_gen_s<BLOCK, V, 1>(h, p, stream);
+    if (h->cfg.features > 8) launch_gen_f<BLOCK, V, 16>(h, p, stream);
+    else launch_gen_f<BLOCK, V, 8>(h, p, stream);
 }
 inline void launch_gen(const pmenv* h, StepParams p, hipStream_t stream) {
     p.div_units = make_fastdiv(h->per4);
-    p.halo = h->halo;                      // in place: the two chunks past each workgroup (the scalar step's copy)
+    p.halo = h->halo;                      // in place: the chunks past each workgroup (the scalar step's copy)
     if (pmenv_tools::launch_gen(h, p, stream)) return;
     switch (h->gen_block * 10 + h->gen_v) {
     case 2562: launch_gen_g<256, 2>(h, p, stream); break;
@@ -297,29 +307,29 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- one launch, relayed (step_relay.h)
-template <int BLOCK, int POL, bool OUT, bool SEQ>
+template <int BLOCK, int POL, bool OUT, bool SEQ, bool ANY = false>
 inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
                            hipStream_t stream) {
     const uint32_t q = h->flat_qtot;
     switch (h->relay_kl * 100 + h->relay_ka) {
-    case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 3200: step_relay_kernel<BLOCK, 2, POL, OUT, 32, 0, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4, 1, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
-    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8, SEQ><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 3200: step_relay_kernel<BLOCK, 2, POL, OUT, 32, 0, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6400: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 0, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6402: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 2, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    case 6404: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 4, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
+    default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     }
 }
-template <int BLOCK, int POL>
+template <int BLOCK, int POL, bool ANY = false>
 inline void launch_relay_b(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, bool out,
                            bool seq, hipStream_t stream) {
     if (out) {
-        if (seq) launch_relay_g<BLOCK, POL, true, true>(h, p, r, grid, stream);
-        else launch_relay_g<BLOCK, POL, true, false>(h, p, r, grid, stream);
+        if (seq) launch_relay_g<BLOCK, POL, true, true, ANY>(h, p, r, grid, stream);
+        else launch_relay_g<BLOCK, POL, true, false, ANY>(h, p, r, grid, stream);
     } else {
-        if (seq) launch_relay_g<BLOCK, POL, false, true>(h, p, r, grid, stream);
-        else launch_relay_g<BLOCK, POL, false, false>(h, p, r, grid, stream);
+        if (seq) launch_relay_g<BLOCK, POL, false, true, ANY>(h, p, r, grid, stream);
+        else launch_relay_g<BLOCK, POL, false, false, ANY>(h, p, r, grid, stream);
     }
 }
 
@@ -332,8 +342,8 @@ inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     const bool dseq = h->relay_dseq;
     p.per4 = h->per4;
     p.div_units = make_fastdiv(h->per4);
-    if (!dseq && ++h->relay_epoch == 0) {           // the words restart at 0 when the counter wraps
-        const size_t words = (size_t)h->cfg.num_envs * h->cfg.num_assets * 8;
+    if (!dseq && ++h->relay_epoch == 0) {           // the words, list and claims restart at 0 when the counter wraps
+        const size_t words = (size_t)((char*)h->relay_list - (char*)h->relay_w) + relay_list_bytes(h);
         if (hipMemsetAsync(h->relay_w, 0, words, stream) != hipSuccess) return PMENV_ERR_HIP;
         h->relay_epoch = 1;
     }
@@ -348,6 +358,11 @@ inline int launch_relay(pmenv* h, StepParams p, hipStream_t stream) {
     r.halo_out = h->relay_halo + (size_t)(1 - q) * h->relay_halo_stride;
     r.seq = dseq ? h->relay_seq : nullptr;
     r.w = h->relay_w;
+    r.list = h->relay_list;
+    r.done = h->relay_done;
+    r.spin = pmenv_dev::kRelaySpin;
+    r.rot = 0;
+    r.grid = h->relay_tiles + h->relay_scal;
     r.kp = h->relay_kp;
     r.halo = h->relay_halo;
     r.B = (uint32_t)h->cfg.num_envs;

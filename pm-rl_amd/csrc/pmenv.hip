@@ -129,14 +129,16 @@ int flat1_invalidate(pmenv* h, hipStream_t stream, int what = kInvalSnap | kInva
     return PMENV_OK;
 }
 
-// The relay step's memory (zeroed: the device-sequenced words, no relay word of any epoch), allocated
-// when AUTO gives the shape the relay step or pmenv_set_step_path asks for it — not on a step.
+// The relay step's memory (zeroed: the device-sequenced words, no relay word, deferral list or tile
+// claim of any epoch), allocated when AUTO gives the shape the relay step or pmenv_set_step_path asks
+// for it — not on a step. The deferral list and claims (step_relay.h) follow the relay words, so
+// one memset clears all three when the eager epoch wraps.
 int relay_alloc(pmenv* h) {
     if (h->relay_mem || !h->relay_ok) return PMENV_OK;
     const pmenv_cfg& c = h->cfg;
     const uint64_t B = (uint64_t)c.num_envs, BN = B * (uint64_t)c.num_assets;
     auto up16 = [](size_t x) { return (x + 15) / 16 * 16; };
-    const size_t ctl_b = 64, words_b = up16(BN * 8), kp_b = up16(B * 4);
+    const size_t ctl_b = 64, words_b = up16(BN * 8) + relay_list_bytes(h), kp_b = up16(B * 4);
     const size_t hal = up16((size_t)h->relay_tiles * 32);
     const size_t bytes = ctl_b + words_b + 2 * kp_b + 2 * hal;
     DeviceGuard g(h->device);
@@ -156,6 +158,8 @@ int relay_alloc(pmenv* h) {
     h->relay_mem = m;
     h->relay_seq = (uint32_t*)b;
     h->relay_w = (uint64_t*)(b + ctl_b);
+    h->relay_list = (uint64_t*)(b + ctl_b + up16(BN * 8));
+    h->relay_done = (uint32_t*)(b + ctl_b + up16(BN * 8) + up16(((size_t)h->relay_tiles + 1) * 8));
     h->relay_kp = (int32_t*)(b + ctl_b + words_b);
     h->relay_halo = (float*)(b + ctl_b + words_b + 2 * kp_b);
     h->relay_halo_stride = (uint32_t)(hal / 4);
@@ -313,7 +317,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->small_block = nwf <= 256 * 16 ? 256 : nwf <= 512 * 16 ? 512 : nwf <= 1024 * 16 ? 1024 : 0;
         h->small_e = nwf <= 256 * 8 ? 8 : 16;
         // config 1's 1 x 5 x 50 x 5: 4.1 us (step_small_kernel) -> see DESIGN.md §3
-        h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64;
+        // (step_tiny_kernel stages the day's bar two floats per thread: N (F - 1) <= 2 x 256)
+        h->tiny = h->small_block == 256 && h->small_e == 8 && c.num_assets <= 64 &&
+                  (int64_t)c.num_assets * (c.features - 1) <= 2 * 256;
     }
     // surface steps on windows past the Infinity Cache with 16-B granular env blocks: the scalar
     // step, then surface_stream_kernel (65,536 x 30 x 50 x 5 723 us with the ring columns staged
@@ -478,8 +484,9 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->one_auto &= ~h->relay_auto;
         h->flat1_auto &= ~h->relay_auto;
     }
-    // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 8 (its halo is the two
-    // chunks past a workgroup), 16-B granular env windows, at most BLOCK rows per workgroup.
+    // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 16 (its halo is the two
+    // chunks past a workgroup, four past F = 8), 16-B granular env windows, at most BLOCK rows
+    // per workgroup.
     // AUTO gives it every window above 2 MiB (16 MiB where step_tiny_kernel would take it),
     // both modes: against the register step / the LDS fallback, one process, the same bits
     // (profiles/ab_r05/gen_few_r05gf2.*), 64 / 256 x 30 x 50 x 8 in place 9.2 / 11.2 against
@@ -496,7 +503,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         h->gen_block = win > (128ll << 20) ? 512 : 256;
         h->gen_v = 2;
         const int64_t cpw = 1024;                           // the shape rule at the larger tile
-        h->gen_ok = F != 5 && F >= 2 && F <= 8 && per % 4 == 0 &&
+        h->gen_ok = F != 5 && F >= 2 && F <= 16 && per % 4 == 0 &&
                     (int64_t)c.num_envs * (per / 4) < (1ll << 31) - 1024 && 4 * cpw / WF + 2 <= 256;
         h->gen_qtot = h->gen_ok ? (uint32_t)((int64_t)c.num_envs * (per / 4)) : 0u;
         h->gen_auto = h->gen_ok && win > (h->tiny ? (16ll << 20) : (2ll << 20)) ? (PMENV_FUSE_DB | PMENV_FUSE_INPLACE) : 0;
@@ -550,7 +557,8 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         const uint32_t qtot = h->flat_inplace ? h->flat_qtot : h->gen_qtot;
         const uint32_t wgs = (qtot + cpw - 1) / cpw;
         h->halo_wgs = wgs > 0 ? wgs - 1 : 0;
-        hipError_t ae = hipMalloc(&h->halo, (size_t)(h->halo_wgs + 1) * 32);
+        const size_t per_wg = !h->flat_inplace && c.features > 8 ? 64 : 32;   // four chunks past F = 8
+        hipError_t ae = hipMalloc(&h->halo, (size_t)(h->halo_wgs + 1) * per_wg);
         if (ae != hipSuccess) {
             set_err(h, "hipMalloc(halo) failed: %s", hipGetErrorString(ae));
             h->halo = nullptr;
@@ -608,6 +616,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         {(const void*)step_advance_lds_kernel<true>, h->lds_tile},
         {(const void*)step_advance_lds_kernel<false>, h->lds_tile},
         {(const void*)step_surface_kernel, h->lds_surface},
+        {(const void*)step_surface_host_kernel, h->lds_surface},
         {(const void*)step_small_kernel<64, 32, false>, h->lds_surface},
         {(const void*)step_small_kernel<256, 8, false>, h->lds_surface},
         {(const void*)step_small_kernel<256, 16, false>, h->lds_surface},
@@ -909,6 +918,10 @@ int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* o
     if (!h) return PMENV_ERR_ARG;
     if (!action || !prices) { set_err(h, "host step: action and prices are required"); return PMENV_ERR_ARG; }
     DeviceGuard g(h->device);
+    if (capturing(stream)) {          // the host waits on the kernel's words: nothing runs under capture
+        set_err(h, "pmenv_step_host is not graph-capturable (the stream is being captured)");
+        return PMENV_ERR_ARG;
+    }
     if (const int rc = hio_ensure(h)) return rc;
     const pmenv_cfg& c = h->cfg;
     const size_t B = (size_t)c.num_envs, BN = B * (size_t)c.num_assets;
@@ -941,6 +954,10 @@ int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* o
 int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
+    if (capturing(stream)) {
+        set_err(h, "pmenv_reset_host is not graph-capturable (the stream is being captured)");
+        return PMENV_ERR_ARG;
+    }
     if (const int rc = hio_ensure(h)) return rc;
     if (obs) hio_gather_closes(h, obs);
     if (const int rc = flat1_invalidate(h, stream)) return rc;

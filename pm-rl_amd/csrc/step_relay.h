@@ -18,19 +18,24 @@
 //     tries). Each word validates itself, so no flag and no ordering between words is needed
 //     (the pattern rocPRIM's look-back scan state uses on gfx942 / gfx950: atomic loads /
 //     stores that bypass the non-coherent L2).
-// A tile only ever waits for scalar blocks, which come before every tile in dispatch order
-// and never wait, so every wait ends. That is a property of the hardware, not a HIP guarantee:
-// the command processor dispatches a grid's workgroups in blockIdx order (round-robin over the
-// XCDs, in order within each), and the product relies on it here (include/pmenv.h states it as
-// a requirement of the relay step). The alternative that does not — an ordered ticket, one
-// agent-scope fetch-add per workgroup on one counter (rocPRIM's ordered block id) — measured
-// 4.7x slower: the ~15,900 same-address atomics of a 4,096 x 30 step serialise at ~10 ns each
-// (194.9 against 41.0 us in place, 383.0 against 80.4 at 8,192 x 30; profiles/ab_r05/). Scalar
-// blocks placed only `lead` tiles ahead of their first consumer measured slower at every lead
-// tried: 4,096 x 30 in place 41.2 us at 8,192 tiles against 40.7 with every scalar block first,
-// 8,192 x 30 80.4 at 16,384 against 78.6, 16-27 % slower at a 1,024-tile lead
-// (profiles/ab_r04/relay_lead2_r04t.err, relay_lead_r04l.err, relay_r04r.err): the first tiles
-// wait for a scalar block either way, and the ones that come later find their w' relayed.
+// Forward progress does not rest on dispatch order. A tile polls its rows' words at most `spin`
+// times; if one is still missing it DEFERS: it stores nothing, appends its index to the step's
+// deferral list ({epoch, count} word + entries), re-checks its words once and exits. A deferred
+// tile is run exactly once — under its own claim word {epoch} — by itself on that re-check if every
+// word has arrived by then, or else by a scalar block: after its units, every scalar block reads
+// the list and runs each listed tile whose words have all arrived. No workgroup ever waits without
+// bound, so every scalar block is eventually dispatched, and a listed tile is never missed: the
+// tile's append and re-check and each scalar block's word stores and list read are ordered by
+// completion waits (a store-buffering pair), so either the re-check sees the last of its words or
+// that word's scalar block sees the entry. The same tile code runs in either case (the same bits).
+// In the hardware's dispatch order (blockIdx order, round-robin over the XCDs) the scalar blocks
+// come first and no tile defers; the normal path's cost is the bounded poll, one LDS vote, and
+// one list read per scalar block. (The first fallback built — tiles running the missing
+// scalar-step units themselves under per-unit claims — put the scalar step into the tile's path:
+// 106 SGPRs, 7 waves per SIMD, +4 % at 4,096 x 30 and +10 % at 8,192 x 30; profiles/r06/. An
+// ordered ticket, one agent-scope fetch-add per workgroup on one counter — rocPRIM's ordered block
+// id — ran 4.7x slower: the ~15,900 same-address atomics of a 4,096 x 30 step serialise at ~10 ns
+// each, 194.9 against 41.0 us; profiles/ab_r05/ticket_r05b.*.)
 //
 // Epoch and parity: eager steps take them from the host (launch arguments). A handle seen under
 // stream capture sequences its relay steps on the device instead (graph replays must not
@@ -58,6 +63,11 @@ struct RelayParams {
     uint32_t scal;           // scalar blocks (the first `scal` blocks of the grid)
     uint32_t epoch;          // eager: this step's tag (never 0: the words start zeroed)
     uint64_t* w;             // [B * N] {epoch, w' bits}
+    uint64_t* list;          // the deferral list: [0] {epoch, count}, [1 + i] {epoch, tile}
+    uint32_t* done;          // [tiles] the epoch of the step in which a deferred tile last ran
+    uint32_t spin;           // tools build (ANY): polls of a missing word before a tile defers
+    uint32_t rot;            // tools build (ANY): blockIdx rotated by `rot` (tiles first: no order)
+    uint32_t grid;           // the launch's workgroups
     // eager: this step's copies (parity p: the counter before the step and, in place, its input
     // chunks past each tile; parity 1 - p: the same for the next step, written by this one)
     const int32_t* kp_in;
@@ -76,11 +86,67 @@ struct RelayParams {
 };
 enum { kSeqD = 0, kSeqE = 1, kSeqV = 2, kSeqC = 3, kSeqEC = 4, kSeqHobs = 6 };
 
+// this step's epoch and parity copies: eager from the launch arguments, device-sequenced from the
+// words relay_prime_kernel published (C, EC: nothing writes them during the launch)
+struct RelayCtx {
+    uint32_t epoch;
+    const int32_t* kp_in;
+    int32_t* kp_out;
+    const float* halo_in;
+    float* halo_out;
+};
+template <bool SEQ>
+__device__ __forceinline__ RelayCtx relay_ctx(const RelayParams& r) {
+    RelayCtx c{r.epoch, r.kp_in, r.kp_out, r.halo_in, r.halo_out};
+    if constexpr (SEQ) {
+        const uint32_t par = __builtin_amdgcn_readfirstlane(r.seq[kSeqC]);
+        c.epoch = __builtin_amdgcn_readfirstlane(r.seq[kSeqEC]);
+        c.kp_in = r.kp + (size_t)par * r.B;
+        c.kp_out = r.kp + (size_t)(par ^ 1u) * r.B;
+        c.halo_in = r.halo + (size_t)par * r.halo_stride;
+        c.halo_out = r.halo + (size_t)(par ^ 1u) * r.halo_stride;
+    }
+    return c;
+}
+
+// step_relay_kernel's arguments read afresh from the kernel-argument segment, through a pointer
+// the compiler cannot see through: the deferral paths (relay_defer, relay_adopt) run a second
+// copy of the tile's code after the first attempt or the scalar step, and the compiler hoists
+// every argument load to the kernel's entry — values held from there through the first code
+// would push the kernel past the SGPR budget of its occupancy (81 SGPRs without the deferral
+// paths, 106 with them on the hoisted arguments: 7 waves per SIMD instead of 8)
+struct KArgs {
+    StepParams p;
+    RelayParams r;
+    uint32_t qtot;
+};
+__device__ __forceinline__ KArgs kargs() {
+    typedef __attribute__((address_space(4))) const uint32_t KWord;
+    KWord* ka = (KWord*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    uint32_t w[sizeof(KArgs) / 4];
+#pragma unroll
+    for (size_t i = 0; i < sizeof(KArgs) / 4; ++i) w[i] = ka[i];
+    KArgs k;
+    __builtin_memcpy(&k, w, sizeof(KArgs));                   // not a punned store: well-defined
+    return k;
+}
+
 __device__ __forceinline__ void relay_put(uint64_t* w, uint32_t epoch, uint32_t bits) {
     __hip_atomic_store(w, ((uint64_t)epoch << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t relay_get(const uint64_t* w) {
     return __hip_atomic_load(const_cast<uint64_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A scalar wave's read of the deferral list's count, once its relay words have completed (the
+// store-buffering pair with relay_defer: step_relay.h's head)
+__device__ __forceinline__ uint32_t relay_list_read(const RelayParams& r, uint32_t epoch) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t lw = relay_get(r.list);
+    return (uint32_t)(lw >> 32) == epoch ? (uint32_t)lw : 0u;
 }
 
 // The scalar role: the two-launch path's scalar step for envs [s * EPB, (s + 1) * EPB).
@@ -89,19 +155,22 @@ __device__ __forceinline__ uint64_t relay_get(const uint64_t* w) {
 // through the relay words; the counter of the next step goes to kp_out (read after this
 // launch has ended).
 template <int BLOCK, int KL, int KA>
-__device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayParams& r, int s, uint32_t epoch,
-                                             int32_t* kp_out) {
+__device__ __forceinline__ uint32_t relay_scalar(const StepParams& p, const RelayParams& r, int s, uint32_t epoch,
+                                                 int32_t* kp_out) {
     constexpr int EPW = 64 / KL, EPB = (BLOCK / 64) * EPW;
     const int lane = threadIdx.x & 63;
     const int b = s * EPB + (int)(threadIdx.x >> 6) * EPW + lane / KL;
     const int j = lane % KL;
     const int N = p.N;
     const bool env_ok = b < p.B;
+    // after the words: the wave's list read (relay_list_read), its round trip under the tail's stores
+    uint32_t listed;
     if constexpr (KA == 0) {
         const ScalarIn in = scalar_load<KL>(p, b, lane);
         const ScalarMid m = scalar_core<KL>(p, b, lane, in);
         if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, epoch, __float_as_uint(m.wp));
         if (env_ok && j == 0) kp_out[b] = m.k + 1;
+        listed = relay_list_read(r, epoch);
         scalar_tail<KL>(p, b, lane, in, m);
     } else {
         const VecIn<KA> in = vec_load<KL, KA, true>(p, b, lane);
@@ -112,8 +181,10 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
             if (env_ok && n < N) relay_put(r.w + (size_t)b * N + n, epoch, __float_as_uint(m.wp[e]));
         }
         if (env_ok && j == 0) kp_out[b] = in.k + 1;
+        listed = relay_list_read(r, epoch);
         vec_tail<KL, KA, true>(p, b, lane, in, m);
     }
+    return listed;
 }
 
 // The tile role: flat_wg_body_patch's stream of tile t, its rows' bar and counter (kp_in)
@@ -122,10 +193,16 @@ __device__ __forceinline__ void relay_scalar(const StepParams& p, const RelayPar
 // after, ran 1.1-1.4x slower: the deferred 16-B chunks leave partly written lines between the
 // two store waves — profiles/ab_r04/relay_split_r04s.err.)
 // OUT: double-buffered (the chunks past the tile read straight from obs).
-template <int BLOCK, int V, int POL, bool OUT>
-__device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t t,
+// ADOPT = false: the tile's own attempt, which polls `spin` times at most and returns false — having
+// stored nothing — when a wave still misses a word; ADOPT = true: a deferred tile's run (by itself
+// after the re-check, or by a scalar block), which polls once, returns false if a word is missing,
+// and else runs only under the tile's claim (one run per step: in place, a second run would shift
+// the window twice).
+template <int BLOCK, int V, int POL, bool OUT, bool ADOPT>
+__device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t spin, uint32_t t,
                                            uint32_t epoch, const int32_t* kp_in, const float* halo_in,
-                                           float* halo_out, f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc) {
+                                           float* halo_out, f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc,
+                                           int32_t* sh_ok) {
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -158,16 +235,17 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
     uint64_t ww = 0;
     if (barb) xb = *reinterpret_cast<const f4*>(barb + (size_t)n * 4);
     kc = kp_in[b];
-    // w': relayed by the scalar blocks placed before this tile
+    // w': relayed by the scalar blocks, polled `spin` times at most (ADOPT: once)
     ww = relay_get(r.w + g);
     bool ready = !mine || (uint32_t)(ww >> 32) == epoch;
-    while (!__all(ready)) {
+    for (uint32_t polls = 0; !ADOPT && !__all(ready) && polls < spin; ++polls) {
         __builtin_amdgcn_s_sleep(2);
         if (!ready) {
             ww = relay_get(r.w + g);
             ready = (uint32_t)(ww >> 32) == epoch;
         }
     }
+    const bool wave_ok = __all(ready);                              // the whole wave, before any branch
     if (mine) {
         sh_bar[tid] = xb;
         sh_wp[tid] = __uint_as_float((uint32_t)ww);
@@ -176,9 +254,21 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
 #pragma unroll
     for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
     if (tid < 2) sh4[CPW + tid] = hal;
+    if (lane == 0) sh_ok[wave] = wave_ok ? 1 : 0;
     __syncthreads();
+    if constexpr (ADOPT) {                                          // polled once; then the tile's claim
+        bool tile_ok = true;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) tile_ok = tile_ok && sh_ok[w] != 0;
+        if (!tile_ok) return false;                                 // the whole workgroup: nothing stored
+        if (tid == 0)
+            sh_ok[BLOCK / 64] = __hip_atomic_exchange(r.done + t, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;
+        __syncthreads();
+        if (!sh_ok[BLOCK / 64]) return true;                        // ran elsewhere
+    }
     const auto rd = OUT ? make_rsrc(p.obs_out + (size_t)c0 * 4, nblk * 16u) : rs;
     const bool first_out = !OUT && t > 0;                           // feeds the previous tile's halo
+    bool ok = true;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const int j = 64 * V * wave + 64 * v + lane;
@@ -191,52 +281,121 @@ __device__ __forceinline__ void relay_tile(const StepParams& p, const RelayParam
         const f4 n1 = sh4[j + 1], n2 = sh4[j + 2];
         const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
         const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        const f4 o = compose2(p, kk, sh_kc[i], un, sh, [&](f4& x, float& xwp) {
+        f4 o = compose2(p, kk, sh_kc[i], un, sh, [&](f4& x, float& xwp) {
             x = sh_bar[i];
             xwp = sh_wp[i];
         });
-        buf_store4<kAux>(rd, (uint32_t)j * 16u, o);                 // past the end: dropped
-        if (first_out && j < 2) reinterpret_cast<f4*>(halo_out)[2 * (t - 1) + j] = o;
+        if (!ADOPT && v == 0) {
+            // the first attempt's vote: no branch on it ahead of the compose (that would put one more
+            // LDS round trip on every tile's path), only the stores' offsets — a tile that gives up
+            // drops its stores (out-of-range buffer offsets) and returns false
+            int32_t okv = 1;
+#pragma unroll
+            for (int w = 0; w < BLOCK / 64; ++w) okv &= sh_ok[w];
+            ok = __builtin_amdgcn_readfirstlane(okv) != 0;
+        }
+        buf_store4<kAux>(rd, ok ? (uint32_t)j * 16u : 0x80000000u, o);  // past the end: dropped
+        if (ok && first_out && j < 2) reinterpret_cast<f4*>(halo_out)[2 * (t - 1) + j] = o;
     }
+    return ok;
+}
+
+// A scalar block, after its units: every tile on the step's deferral list (as far as any of its
+// waves read it, each after its own relay words completed: relay_list_read) whose words have all
+// arrived, run under its claim. With the deferring tile's append-then-re-check, no listed tile is
+// missed (step_relay.h's head). The normal case — an empty list — costs one LDS vote.
+template <int BLOCK, int V, int POL, bool OUT, bool SEQ>
+__device__ __forceinline__ void relay_adopt(f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc, int32_t* sh_ok,
+                                            uint32_t listed) {
+    constexpr int kB = BLOCK / 64 + 1;                              // sh_ok's broadcast slot (the tile's: below)
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh_ok[wave] = (int32_t)__builtin_amdgcn_readfirstlane(listed);
+    __syncthreads();
+    uint32_t n = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) n = max(n, (uint32_t)sh_ok[w]);
+    if (n == 0) return;
+    const KArgs ka = kargs();
+    const RelayCtx c = relay_ctx<SEQ>(ka.r);
+    for (uint32_t i = 0; i < n; ++i) {
+        __syncthreads();                                            // sh_ok / the tile's LDS are free
+        if (threadIdx.x == 0) {
+            const uint64_t e = relay_get(ka.r.list + 1 + i);        // its tile may not have stored it yet
+            int32_t t = (uint32_t)(e >> 32) == c.epoch ? (int32_t)(uint32_t)e : -1;
+            if (t >= 0 && __hip_atomic_load(ka.r.done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c.epoch)
+                t = -1;                                             // ran already
+            sh_ok[kB] = t;
+        }
+        __syncthreads();
+        const int32_t t = __builtin_amdgcn_readfirstlane(sh_ok[kB]);
+        if (t >= 0)
+            (void)relay_tile<BLOCK, V, POL, OUT, true>(ka.p, ka.r, ka.qtot, 0u, (uint32_t)t, c.epoch, c.kp_in, c.halo_in,
+                                                       c.halo_out, sh4, sh_bar, sh_wp, sh_kc, sh_ok);
+    }
+}
+
+// A tile that gave up: append it to the deferral list, wait for that store, re-check once (and run
+// under its claim if every word has arrived), exit
+template <int BLOCK, int V, int POL, bool OUT, bool SEQ>
+__device__ __forceinline__ void relay_defer(uint32_t t, f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc,
+                                            int32_t* sh_ok) {
+    const KArgs ka = kargs();
+    const RelayCtx c = relay_ctx<SEQ>(ka.r);
+    if (threadIdx.x == 0) {
+        uint64_t lw = relay_get(ka.r.list), nw;
+        do {                                                        // {epoch, count}: a stale epoch restarts it
+            nw = (uint32_t)(lw >> 32) == c.epoch ? lw + 1 : ((uint64_t)c.epoch << 32) | 1u;
+        } while (!__hip_atomic_compare_exchange_strong(ka.r.list, &lw, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+        const uint32_t slot = (uint32_t)(lw >> 32) == c.epoch ? (uint32_t)lw : 0u;
+        relay_put(ka.r.list + 1 + slot, c.epoch, t);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);                              // the entry is stored before the re-check
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    __syncthreads();
+    (void)relay_tile<BLOCK, V, POL, OUT, true>(ka.p, ka.r, ka.qtot, 0u, t, c.epoch, c.kp_in, c.halo_in, c.halo_out, sh4,
+                                               sh_bar, sh_wp, sh_kc, sh_ok);
 }
 
 // BLOCK x V tiles (the flat stream's 256 x 2 / 512 x 2), POL the window stream's cache
 // policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar), OCC the waves
 // per SIMD the kernel is held to (the 8-assets-per-lane form would otherwise take 84 VGPRs
 // and cut the tiles to 5 waves per SIMD)
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1, bool SEQ = false>
+// ANY (tools build only): the dispatch order and the polls before a tile defers from the launch
+// arguments (r.rot, r.spin), to force the deferral paths; the product takes blockIdx order and
+// kRelaySpin
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1, bool SEQ = false, bool ANY = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void step_relay_kernel(
     StepParams p, RelayParams r, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
     __shared__ f4 sh_bar[BLOCK];
     __shared__ float sh_wp[BLOCK];
     __shared__ int32_t sh_kc[BLOCK];
-    uint32_t epoch = r.epoch;
-    const int32_t* kp_in = r.kp_in;
-    int32_t* kp_out = r.kp_out;
-    const float* halo_in = r.halo_in;
-    float* halo_out = r.halo_out;
+    __shared__ int32_t sh_ok[BLOCK / 64 + 2];   // the waves' votes | the claim | a broadcast
+    const RelayCtx c = relay_ctx<SEQ>(r);
     if constexpr (SEQ) {                         // relay_prime_kernel published C and EC
-        const uint32_t par = __builtin_amdgcn_readfirstlane(r.seq[kSeqC]);
-        epoch = __builtin_amdgcn_readfirstlane(r.seq[kSeqEC]);
-        kp_in = r.kp + (size_t)par * r.B;
-        kp_out = r.kp + (size_t)(par ^ 1u) * r.B;
-        halo_in = r.halo + (size_t)par * r.halo_stride;
-        halo_out = r.halo + (size_t)(par ^ 1u) * r.halo_stride;
         if (blockIdx.x == 0 && threadIdx.x == 0) {   // what the next step finds
             const uint64_t hobs = OUT ? 0ull : (uint64_t)(uintptr_t)r.obs;
-            r.seq[kSeqD] = par ^ 1u;
-            r.seq[kSeqE] = epoch;
+            r.seq[kSeqD] = (uint32_t)((c.kp_in - r.kp) / r.B) ^ 1u;
+            r.seq[kSeqE] = c.epoch;
             r.seq[kSeqV] = 1u;
             r.seq[kSeqHobs] = (uint32_t)hobs;
             r.seq[kSeqHobs + 1] = (uint32_t)(hobs >> 32);
         }
     }
-    if (blockIdx.x < r.scal)
-        relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x, epoch, kp_out);
-    else
-        relay_tile<BLOCK, V, POL, OUT>(p, r, qtot, blockIdx.x - r.scal, epoch, kp_in, halo_in, halo_out, sh4, sh_bar,
-                                       sh_wp, sh_kc);
+    uint32_t bid = blockIdx.x;
+    if constexpr (ANY) {
+        bid += r.rot;
+        if (bid >= r.grid) bid -= r.grid;
+    }
+    if (bid < r.scal) {
+        const uint32_t listed = relay_scalar<BLOCK, KL, KA>(p, r, (int)bid, c.epoch, c.kp_out);
+        relay_adopt<BLOCK, V, POL, OUT, SEQ>(sh4, sh_bar, sh_wp, sh_kc, sh_ok, listed);
+    } else if (!relay_tile<BLOCK, V, POL, OUT, false>(p, r, qtot, ANY ? r.spin : kRelaySpin, bid - r.scal, c.epoch, c.kp_in, c.halo_in, c.halo_out,
+                                                      sh4, sh_bar, sh_wp, sh_kc, sh_ok)) {
+        relay_defer<BLOCK, V, POL, OUT, SEQ>(bid - r.scal, sh4, sh_bar, sh_wp, sh_kc, sh_ok);
+    }
 }
 
 // The relay step's copies of parity D (eager: r.par; device-sequenced: the word D): kp[D] <- the

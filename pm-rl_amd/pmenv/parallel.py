@@ -71,9 +71,12 @@ def allreduce_grads(params, loss_sum, count, group=None):
     if not ps:
         raise ValueError("allreduce_grads needs the replicated parameters")
     dev = ps[0].device
-    parts = [(p.grad.detach().reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=p.device))
-             .to(device=dev, dtype=torch.float64) for p in ps]
-    has = torch.tensor([1.0 if p.grad is not None else 0.0 for p in ps], dtype=torch.float64, device=dev)
+    # only trainable parameters count: a frozen one's local .grad neither rides in the bucket nor
+    # gets a flag, and it is cleared on every rank alike (no rank keeps an un-averaged gradient)
+    live = [p.requires_grad and p.grad is not None for p in ps]
+    parts = [(p.grad.detach().reshape(-1) if ok else torch.zeros(p.numel(), device=p.device))
+             .to(device=dev, dtype=torch.float64) for p, ok in zip(ps, live)]
+    has = torch.tensor([1.0 if ok else 0.0 for ok in live], dtype=torch.float64, device=dev)
     extra = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64).reshape(()).to(dev),
                          torch.tensor(float(count), dtype=torch.float64, device=dev)])
     bucket = torch.cat(parts + [has, extra])
@@ -84,7 +87,9 @@ def allreduce_grads(params, loss_sum, count, group=None):
     off = 0
     for p, f in zip(ps, flags):
         k = p.numel()
-        if f > 0 and p.requires_grad:
+        if not p.requires_grad:
+            p.grad = None
+        elif f > 0:
             g = (bucket[off:off + k] / n).reshape(p.shape).to(device=p.device, dtype=p.dtype)
             if p.grad is None:
                 p.grad = g

@@ -88,8 +88,8 @@ def test_gpu_every_step_path_matches_reference_goldens(name, impl):
     N, W, F = m["N"], m["W"], m["F"]
     # the shape rules of pmenv_set_step_path (include/pmenv.h)
     granular = F == 5 and (N * W * F) % 4 == 0
-    # F != 5: the generic stream (2 <= F <= 8, 16-B granular, the workgroup's rows fit)
-    generic = F != 5 and 2 <= F <= 8 and (N * W * F) % 4 == 0 and 4 * 1024 // (W * F) + 2 <= 256
+    # F != 5: the generic stream (2 <= F <= 16, 16-B granular, the workgroup's rows fit)
+    generic = F != 5 and 2 <= F <= 16 and (N * W * F) % 4 == 0 and 4 * 1024 // (W * F) + 2 <= 256
     misfit = {"two_launch": not (granular or generic),
               "one_launch": not (granular and W >= 2 and N <= 64 and N * W * F * 4 <= 64 * 1024),
               "flat": not (granular and W >= 2 and N <= 64 and N * W * F // 4 >= 148),
@@ -574,6 +574,9 @@ def test_gpu_vs_oracle_shapes(N, W, F, B):
     (7, 10, 3, 6, "step_tiny_kernel"),
     (64, 8, 4, 5, "step_tiny_kernel"),         # 2,048 floats: the tiny step's largest, 64 assets
     (64, 4, 8, 3, "step_tiny_kernel"),         # 448 bar floats: more than one per thread
+    (64, 3, 9, 2, "step_tiny_kernel"),         # 512 bar floats: two per thread, every thread
+    (60, 3, 10, 3, "step_small_kernel"),       # 540 bar floats: past the tiny step's staging
+    (40, 3, 16, 2, "step_small_kernel"),       # 600 bar floats, F = 16
     (65, 6, 5, 3, "step_small_kernel"),        # N > 64: the LDS-scratch scalar step
     (30, 50, 12, 3, "step_advance_lds_kernel"),   # 18,000 floats: past the register step
 ])
@@ -600,6 +603,12 @@ def test_gpu_register_step_vs_oracle(N, W, F, B, path, kw, db):
     (64, 16, 8, 3),
     (65, 16, 4, 2),       # N > 64: the packed scalar step
     (100, 10, 8, 3),      # N = 100: the packed scalar step, two-envs-per-tile seams
+    (30, 50, 12, 4),      # F = 12 (config/base.py's indicators): four halo chunks, 16-B shifted reads
+    (8, 10, 16, 11),      # F = 16: the widest, a shift of four whole chunks
+    (9, 8, 9, 13),        # F = 9: dword shifted reads past the two-chunk halo
+    (11, 4, 10, 5),       # F = 10, W = 4: 8-B shifted reads, chunks across rows
+    (3, 20, 13, 7),
+    (65, 16, 14, 2),      # N > 64 with F = 14
 ])
 @pytest.mark.parametrize("kw", [{}, {"ring": "chrono"}, {"commission": 0.0025, "reward": "diff_sharpe"}],
                          ids=["storage", "chrono", "commission"])
@@ -617,15 +626,17 @@ def test_gpu_generic_stream_vs_oracle(N, W, F, B, kw, db):
               impl="two_launch", resets={W // 2 + 1: rng.random(B) < 0.4})
 
 
+@pytest.mark.parametrize("F", [8, 12, 16])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
-def test_gpu_generic_stream_auto_at_size(db):
-    """AUTO's generic stream on a window past its 2 MiB threshold (600 x 30 x 50 x 8, the
-    reference loader's F), commission and the differential Sharpe, past the ring's wrap."""
+def test_gpu_generic_stream_auto_at_size(db, F):
+    """AUTO's generic stream on a window past its 2 MiB threshold (600 x 30 x 50 x F: the
+    reference loader's F = 8, and its width with config/base.py's indicators on), commission
+    and the differential Sharpe, past the ring's wrap."""
     from pmenv import TradingEnv
-    kw = {"commission": 0.0025, "reward": "diff_sharpe", "close_channel": 6}
-    e = TradingEnv(num_envs=600, num_assets=30, window=50, features=8, device=DEV, **kw)
+    kw = {"commission": 0.0025, "reward": "diff_sharpe", "close_channel": F - 2}
+    e = TradingEnv(num_envs=600, num_assets=30, window=50, features=F, device=DEV, **kw)
     assert e.step_path.count("advance_gen_kernel") == 2, e.step_path
-    _run_both(kw, B=600, N=30, W=50, T=53, kind="mixed", F=8, seed=608, double_buffer=db)
+    _run_both(kw, B=600, N=30, W=50, T=53, kind="mixed", F=F, seed=600 + F, double_buffer=db)
 
 
 @pytest.mark.parametrize("kw", [{"commission": 0.0025, "reward": "diff_sharpe"}, {"ring": "chrono", "reward": "sharpe_ratio"}],
@@ -653,8 +664,11 @@ def test_gpu_generic_stream_auto_threshold():
     tiny_big = TradingEnv(num_envs=2100, num_assets=5, window=50, features=8, close_channel=6, device=DEV)
     assert tiny_big.step_path.count("advance_gen_kernel") == 2, tiny_big.step_path
     wide = TradingEnv(num_envs=8, num_assets=30, window=50, features=12, close_channel=10, device=DEV)
+    wide.set_step_impl("two_launch")                                  # F <= 16 streams (four halo chunks)
+    assert wide.step_path.count("advance_gen_kernel") == 2, wide.step_path
+    wider = TradingEnv(num_envs=8, num_assets=30, window=50, features=17, close_channel=15, device=DEV)
     with pytest.raises(ValueError):
-        wide.set_step_impl("two_launch")
+        wider.set_step_impl("two_launch")
     # past the register step's 16,384 floats per env: the LDS fallback below 2 MiB
     w8 = TradingEnv(num_envs=16, num_assets=100, window=50, features=8, close_channel=6, device=DEV)   # 2.6 MB
     assert w8.step_path.count("advance_gen_kernel") == 2, w8.step_path

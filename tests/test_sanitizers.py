@@ -6,9 +6,13 @@ HIP path's in-place schedules, built with AddressSanitizer + UndefinedBehaviorSa
     chunk another one has already stored, and the in-place result equals an out-of-place
     advance;
   * the relayed step (step_relay.h) — scalar blocks and tiles interleaved at random, a tile
-    runnable only once its rows' relay words carry the step's epoch, through the epoch's
-    wrap, caller edits, a state write and a step of another path; every staged row fits the
-    tile's threads and every LDS / halo / counter index its buffer;
+    runnable only once its rows' relay words carry the step's epoch or, past its polls, giving
+    up and running its rows' scalar-step units under their claims, through the epoch's wrap,
+    caller edits, a state write and a step of another path, in blockIdx order, any order, one
+    resident workgroup and tiles first — no deadlock, every env stepped once from its pre-step
+    state, the product's bits; every staged row fits the tile's threads and every LDS / halo /
+    counter index its buffer; without the fallback, one resident in a non-monotone order must
+    deadlock (the detection's negative control);
   * the one-pass look-back GAE — workgroups publishing and composing in a random order under
     the flag waits, on an exact-size workspace holding garbage or the previous call's flags;
   * an address audit of the halo copy for every scalar-step grid and of the tools build's

@@ -602,113 +602,8 @@ __global__ __launch_bounds__(64 * NW) void gae_lookback2_kernel(const float* r, 
 }
 
 
-// ---------------------------------------------------------------- env-aligned relay tiles (round 5 A/B, PMENV_RELAY_ENV)
-// The same relay with one tile per ENV (step_env_kernel's geometry: the env's 1 KiB-aligned
-// 64-chunk blocks over the workgroup's waves, V chunks per lane) instead of fixed 8 KiB
-// tiles of the flat window: a tile owns its env's whole window, so the in-place advance needs
-// no halo and no tile ever reads a chunk another one stores — every load of the env lands
-// before any of its stores (one barrier). Wave 0 stages the env's bar rows and waits for the
-// env's relayed w' (one word per asset) and reads the counter copy; the scalar step itself
-// runs in the scalar blocks before every tile, as in step_relay_kernel. For cache-resident
-// windows this is the pattern the Infinity Cache favours: an in-place shift one workgroup per
-// env ran 34.6 us at 4,096 x 30 x 50 x 5 against 40.0 for a flat read+write copy of the same
-// bytes (tools/membench.hip, profiles/ab_r05/). Measured against the product's relay (the same
-// bits): 3-6 % slower at 2,048 - 6,144 x 30, 1.8 % faster at 8,192 x 30, 20 % slower at
-// N = 8 / 16 (profiles/ab_r05/relay_env_r05g.err) — not kept.
-template <int BLOCK, int V, int POL, bool OUT>
-__device__ __forceinline__ void relay_env_tile(const StepParams& p, const RelayParams& r, uint32_t per4, int b,
-                                               uint32_t epoch, const int32_t* kp_in) {
-    constexpr int kAux = POL == 1 ? 2 : 0;
-    constexpr int F = 5;
-    extern __shared__ __attribute__((aligned(16))) f4 sh4[];        // [64 * V * waves + 2] window image
-    __shared__ f4 sh_bar[64];
-    __shared__ float sh_wp[64];
-    __shared__ int32_t sh_k;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int N = p.N, WF = p.W * F;
-    const uint64_t e0 = (uint64_t)b * per4;
-    const uint32_t a = (uint32_t)(e0 & 63u);
-    const auto rs = make_rsrc(p.obs + e0 * 4, per4 * 16u);
-    // the window stream first (offsets relative to the env: negative ones wrap out of range)
-    f4 own[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) own[v] = buf_load4<kAux>(rs, ((uint32_t)(64 * V * wave + 64 * v + lane) - a) * 16u);
-    __builtin_amdgcn_sched_barrier(0);
-    if (wave == 0) {                              // the env's side data: bar rows, w' (relayed), counter
-        const float* barb = env_bar(p, b);
-        const uint32_t nb = (uint32_t)N * 16u;
-        const f4 xb = buf_load4<0>(make_rsrc(barb ? barb : p.bar, barb ? nb : 0u), (uint32_t)lane * 16u);
-        const int32_t kc = kp_in[b];
-        const bool mine = lane < N;
-        const uint64_t* wq = r.w + (size_t)b * N + (mine ? lane : 0);
-        uint64_t ww = relay_get(wq);
-        bool ready = !mine || (uint32_t)(ww >> 32) == epoch;
-        while (!__all(ready)) {
-            __builtin_amdgcn_s_sleep(2);
-            if (!ready) {
-                ww = relay_get(wq);
-                ready = (uint32_t)(ww >> 32) == epoch;
-            }
-        }
-        sh_wp[lane] = __uint_as_float((uint32_t)ww);
-        sh_bar[lane] = barb ? xb : f4{NAN, NAN, NAN, NAN};            // day outside the series: NaN bar
-        if (lane == 0) sh_k = kc;
-    }
-#pragma unroll
-    for (int v = 0; v < V; ++v) sh4[64 * V * wave + 64 * v + lane] = own[v];
-    __syncthreads();
-    // compose and store (step_env_body's): only the chunks holding a row's last day or (ring
-    // full, storage order) its weight slot read the env's bar / w' from LDS
-    const int32_t k = sh_k;
-    const bool shift_w = !(p.ring_mode == PMENV_RING_STORAGE && k >= p.W - 1);
-    const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)p.W) * F + (F - 1));
-    const auto rd = OUT ? make_rsrc(p.obs_out + e0 * 4, per4 * 16u) : rs;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-        const uint32_t slot = (uint32_t)(64 * V * wave + 64 * v + lane);
-        const uint32_t c = slot - a;                                         // env-local chunk (wraps if < 0)
-        const uint32_t j0 = 4u * min(c, per4 - 1u);                          // lanes outside the env: any row
-        const uint32_t row = fdiv(j0, p.div_wf);
-        FlatSide sd;
-        sd.kk = (int)(j0 - row * (uint32_t)WF);
-        sd.bar_nan = false;
-        const bool need = sd.kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - sd.kk) <= 3u);
-        sd.xb = f4{0.f, 0.f, 0.f, 0.f};
-        sd.xwp = 0.f;
-        if (need) {
-            sd.xb = sh_bar[row];
-            sd.xwp = sh_wp[row];
-        }
-        sd.k = k;
-        const f4 n1 = sh4[slot + 1], n2 = sh4[slot + 2];
-        const float sh[4] = {n1.y, n1.z, n1.w, n2.x};
-        const float un[4] = {own[v].x, own[v].y, own[v].z, own[v].w};
-        buf_store4<kAux>(rd, c * 16u, flat_compose(p, sd, un, sh));          // outside the env: dropped
-    }
-}
-
-// blocks [0, scal): scalar blocks (EPB envs each); block scal + b: env b's tile
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, bool SEQ = false>
-__global__ __launch_bounds__(BLOCK) void step_relay_env_kernel(StepParams p, RelayParams r, uint32_t per4) {
-    uint32_t epoch = r.epoch;
-    const int32_t* kp_in = r.kp_in;
-    int32_t* kp_out = r.kp_out;
-    if constexpr (SEQ) {                         // relay_prime_kernel published C and EC
-        const uint32_t par = __builtin_amdgcn_readfirstlane(r.seq[kSeqC]);
-        epoch = __builtin_amdgcn_readfirstlane(r.seq[kSeqEC]);
-        kp_in = r.kp + (size_t)par * r.B;
-        kp_out = r.kp + (size_t)(par ^ 1u) * r.B;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {   // what the next step finds (no halo: HOBS unused)
-            r.seq[kSeqD] = par ^ 1u;
-            r.seq[kSeqE] = epoch;
-            r.seq[kSeqV] = 1u;
-        }
-    }
-    if (blockIdx.x < r.scal)
-        relay_scalar<BLOCK, KL, KA>(p, r, (int)blockIdx.x, epoch, kp_out);
-    else
-        relay_env_tile<BLOCK, V, POL, OUT>(p, r, per4, (int)(blockIdx.x - r.scal), epoch, kp_in);
-}
+// (round 5's env-aligned relay tiles, step_relay_env_kernel — measured 3-6 % slower at 2,048 -
+// 6,144 x 30 and 20 % at N = 8 / 16, profiles/ab_r05/relay_env_r05g.err — are in the git history)
 
 // The register step (env_step.h step_small_kernel, REG form) with wall-clock stamps and
 // timing-only ablations (PMENV_SMALL_ABL): where config 1's 1 x 5 x 50 x 5 step spends its

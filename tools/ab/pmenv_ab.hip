@@ -42,7 +42,8 @@ struct Tools {
     int flat1_pol = 0;          // PMENV_FLAT1_POL: 3 nt loads only, 4 nt stores only, 5 sc0 nt, 6 sc1 nt, 7 nt + sc1 nt
     int fused = 0, fused_vec = 4;   // PMENV_FUSED: advance_rows_kernel<fused> (db | all)
     int stream_block = 512;     // PMENV_STREAM_BLOCK: row-kernel workgroup (128 | 256)
-    bool relay_env = false;     // PMENV_RELAY_ENV: the relay step's env-aligned tiles (step_relay_env_kernel)
+    int relay_spin = -1;        // PMENV_RELAY_SPIN: a tile's polls before it runs a missing unit (-1: product's)
+    bool relay_tiles_first = false;   // PMENV_RELAY_TILES_FIRST: the tiles at blockIdx 0.., the scalar blocks last
     int stream_pol = 0;         // PMENV_STREAM_POL: 0 | 1 (nt) | 2 (sc0 nt)
     int flat_block = 512;       // PMENV_FLAT_BLOCK: the ds_bpermute stream's workgroup
     bool flat_db_wg = true;     // PMENV_FLAT_DB_WG=0: the ds_bpermute double-buffered stream
@@ -354,7 +355,8 @@ void plan(pmenv* h) {
             h->relay_v = v;
         }
     }
-    t->relay_env = knob_int("PMENV_RELAY_ENV", 0) != 0 && h->one_ok && c.num_assets <= 64 && h->one_waves <= 8;
+    t->relay_spin = knob_int("PMENV_RELAY_SPIN", -1);
+    t->relay_tiles_first = knob_int("PMENV_RELAY_TILES_FIRST", 0) != 0;
     if (const char* k = knob("PMENV_SMALL_GEOM")) {   // step_small_kernel's BLOCK x E: 64x32 | 256x8 | 256x16 | ...
         int bk = 0, e = 0;
         const int64_t nwf = (int64_t)c.num_assets * c.window * c.features;
@@ -564,6 +566,7 @@ bool launch_gen_t(const pmenv* h, const StepParams& p, hipStream_t stream) {
 }
 
 bool launch_gen(const pmenv* h, const StepParams& p, hipStream_t stream) {
+    if (h->cfg.features > 8) return false;      // the tools variants stage F <= 8 (the product takes F <= 16)
     if (h->gen_block == 256 && h->gen_v == 4) return launch_gen_t<256, 4>(h, p, stream);
     if (h->gen_block == 512 && h->gen_v == 2) return launch_gen_t<512, 2>(h, p, stream);
     // tiles the product does not instantiate (PMENV_GEN_GEOM=512x4 | 1024x2)
@@ -662,57 +665,30 @@ static void relay_geom(const pmenv* h, const StepParams& p, const RelayParams& r
     if (out) relay_geom_o<BK, V, true>(h, p, r, q, grid, stream);
     else relay_geom_o<BK, V, false>(h, p, r, q, grid, stream);
 }
-template <int BLOCK, int POL, bool OUT, bool SEQ>
-static void launch_relay_env_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
-                               hipStream_t stream) {
-    const size_t lds = ((size_t)BLOCK * kOneV + 2) * 16;
-    const uint32_t q = h->per4;
-    switch (h->relay_kl * 100 + h->relay_ka) {
-    case 801: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 8, 1, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
-    case 1601: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 16, 1, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
-    case 3200: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 32, 0, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
-    default: step_relay_env_kernel<BLOCK, kOneV, POL, OUT, 64, 0, SEQ><<<grid, BLOCK, lds, stream>>>(p, r, q); break;
-    }
-}
-template <int BLOCK>
-static void launch_relay_env_b(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, bool out,
-                               bool seq, int pol, hipStream_t stream) {
-#define PMENV_RE(POL, OUT, SEQ) launch_relay_env_g<BLOCK, POL, OUT, SEQ>(h, p, r, grid, stream)
-    if (pol == 1) {
-        if (out) { if (seq) PMENV_RE(1, true, true); else PMENV_RE(1, true, false); }
-        else { if (seq) PMENV_RE(1, false, true); else PMENV_RE(1, false, false); }
-    } else {
-        if (out) { if (seq) PMENV_RE(0, true, true); else PMENV_RE(0, true, false); }
-        else { if (seq) PMENV_RE(0, false, true); else PMENV_RE(0, false, false); }
-    }
-#undef PMENV_RE
-}
-
 bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, hipStream_t stream) {
     const int g = h->relay_block * 10 + h->relay_v;
     const Tools* tt = tools(h);
-    if (tt && tt->relay_env) {     // one tile per env (no halo used; the product primes it anyway)
-        const int block = h->one_waves <= 4 ? 256 : 512;
-        const int epb = (block / 64) * (64 / h->relay_kl);
-        RelayParams re = r;
-        re.scal = (uint32_t)((h->cfg.num_envs + epb - 1) / epb);
-        const unsigned genv = (unsigned)h->cfg.num_envs + re.scal;
-        const bool out = p.obs_out != p.obs;
-        const int pol = out ? h->flat_pol : h->flat_ip_pol;
-        if (block == 256) launch_relay_env_b<256>(h, p, re, genv, out, false, pol, stream);
-        else launch_relay_env_b<512>(h, p, re, genv, out, false, pol, stream);
-        return true;
-    }
+    // the forward-progress fallback exercised: PMENV_RELAY_SPIN=0 (a tile runs a missing unit on
+    // its first miss) and / or PMENV_RELAY_TILES_FIRST=1 (blockIdx rotated so every tile precedes
+    // every scalar block: the tiles fill the chip and run the scalar steps themselves)
+    RelayParams rr = r;
+    const bool mod = tt && (tt->relay_spin >= 0 || tt->relay_tiles_first);
+    if (tt && tt->relay_spin >= 0) rr.spin = (uint32_t)tt->relay_spin;
+    if (tt && tt->relay_tiles_first) rr.rot = r.scal;
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
     switch (g) {
-    case 1282: relay_geom<128, 2>(h, p, r, q, grid, out, stream); return true;
-    case 1284: relay_geom<128, 4>(h, p, r, q, grid, out, stream); return true;
-    case 2564: relay_geom<256, 4>(h, p, r, q, grid, out, stream); return true;
-    case 2561: relay_geom<256, 1>(h, p, r, q, grid, out, stream); return true;
-    case 2568: relay_geom<256, 8>(h, p, r, q, grid, out, stream); return true;
-    case 5124: relay_geom<512, 4>(h, p, r, q, grid, out, stream); return true;
-    default: return false;
+    case 1282: relay_geom<128, 2>(h, p, rr, q, grid, out, stream); return true;
+    case 1284: relay_geom<128, 4>(h, p, rr, q, grid, out, stream); return true;
+    case 2564: relay_geom<256, 4>(h, p, rr, q, grid, out, stream); return true;
+    case 2561: relay_geom<256, 1>(h, p, rr, q, grid, out, stream); return true;
+    case 2568: relay_geom<256, 8>(h, p, rr, q, grid, out, stream); return true;
+    case 5124: relay_geom<512, 4>(h, p, rr, q, grid, out, stream); return true;
+    default:
+        if (!mod) return false;
+        if (h->relay_block == 256) launch_relay_b<256, 0, true>(h, p, rr, grid, out, false, stream);
+        else launch_relay_b<512, 1, true>(h, p, rr, grid, out, false, stream);
+        return true;
     }
 }
 
