@@ -204,9 +204,15 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
  * f64 (info["returns"]), weights [B, N] f32 (info["actions"]).
  * The step kernel reads the action, the prices and the window's last closes (N floats per
  * env) straight from pinned, device-mapped staging, and writes the [N, W] weight channel
- * and the outputs back into it; the market channels never cross PCIe. SYNCHRONOUS: one
- * stream sync per call, after which the outputs are in place (so not graph-capturable).
- * The staging is allocated on the first call. */
+ * and the outputs back into it; the market channels never cross PCIe. SYNCHRONOUS: the
+ * outputs are in place when the call returns (so not graph-capturable: PMENV_ERR_ARG under
+ * capture). Up to 8 envs, and when this handle has enqueued no device work since its last
+ * host-buffer call, pmenv_step_host runs in one resident workgroup that polls the staging (no
+ * launch per call; it exits after 20 ms without a call or at pmenv_destroy); otherwise it is
+ * one launch on `stream`, ordered after the handle's earlier work there. Other kernels that
+ * read or write this handle's state must be complete before a host-buffer call. The staging is
+ * allocated on the first call. The host side (the last closes gathered, the channel scattered
+ * into obs) is serial on the calling thread: B*N*W strided stores per call. */
 int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* obs, float* reward, double* value,
                     double* ret, float* weights, hipStream_t stream);
 int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream);
@@ -259,14 +265,13 @@ const char* pmenv_step_path(const pmenv* h);
  * device-sequenced (a small relay_prime_kernel before each step_relay_kernel reads the epoch,
  * the parity and the copies' validity from device memory), so captured and eager relay steps
  * interleave freely; pmenv_step_path then says "relay steps device-sequenced".
- * REQUIREMENT: a tile spins until the scalar blocks before it in blockIdx order have relayed
- * its rows, so RELAY (and AUTO, which picks it for in-place windows of 24-256 MiB and
- * double-buffered ones of 48-128 MiB at N <= 64) relies on the GPU dispatching a grid's
- * workgroups in blockIdx order — what CDNA's command processor does (round-robin over the
- * XCDs, in order within each), not a HIP guarantee. The form that does not rely on it (an
- * ordered ticket: one fetch-add per workgroup on one counter) measured 4.7x slower (DESIGN.md
- * §3). Choose TWO_LAUNCH on a platform without in-order dispatch. (pmenv_gae_ex's look-back
- * pass makes no such assumption: a wave that waits too long computes the map itself.) */
+ * No dispatch-order assumption: a tile polls its rows' relay words a bounded number of times
+ * and, if one is still missing (its scalar block not yet dispatched), defers — it stores
+ * nothing, lists itself for the step and exits; the scalar blocks run the listed tiles once
+ * their words have arrived (one run per tile, under a claim word). In blockIdx dispatch order
+ * no tile defers; with every tile dispatched before every scalar block the step completes with
+ * the same bits. (pmenv_gae_ex's look-back pass likewise: a wave that waits too
+ * long computes the map itself.) */
 typedef enum pmenv_step_path_kind {
     PMENV_STEP_PATH_AUTO = 0,
     PMENV_STEP_PATH_ONE_LAUNCH = 1,

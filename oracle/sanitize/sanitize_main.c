@@ -378,6 +378,7 @@ static void emulate_surf(int B, int N, int W, int F, int CPW) {
     for (int64_t i = 0; i < (int64_t)B * W * N; ++i) ring[i] = (float)nrand();
     const int64_t cap = (int64_t)(4 * CPW / WF + 2) * W;
     float* sring = malloc(sizeof(float) * (size_t)cap);
+    uint8_t* seen = malloc((size_t)cap);
     for (int64_t c0 = 0; c0 < qtot; c0 += CPW) {
         const int64_t nblk = qtot - c0 < CPW ? qtot - c0 : CPW;
         const int64_t b_lo = c0 / per4, ql = c0 + nblk - 1, b_hi = ql / per4;
@@ -386,13 +387,31 @@ static void emulate_surf(int B, int N, int W, int F, int CPW) {
         const int64_t nrows = g_hi - g_lo + 1;
         CHECK(nrows * W <= cap, "surf: %lld staged floats past %lld", (long long)(nrows * W), (long long)cap);
         if (nrows * W > cap) break;
-        for (int64_t i = 0; i < nrows * W; ++i) {
-            const int64_t sl = i / nrows, r = i - sl * nrows, g = g_lo + r, b = g / N, n = g - b * N;
-            sring[r * W + sl] = ring[(b * W + sl) * N + n];
+        /* the kernel's walk: thread t from (t / nrows, t % nrows), stepping BLOCK elements by
+         * quotient / remainder increments; every (row, slot) staged exactly once */
+        const int BLOCK = 256;
+        memset(seen, 0, (size_t)cap);
+        for (int t = 0; t < BLOCK; ++t) {
+            const int64_t dq = BLOCK / nrows, dr = BLOCK - dq * nrows;
+            int64_t sl = t / nrows, r = t - sl * nrows;
+            for (int64_t i = t; i < nrows * W; i += BLOCK) {
+                CHECK(sl * nrows + r == i && sl < W && r < nrows, "surf: walk at %lld gives (%lld, %lld)", (long long)i,
+                      (long long)sl, (long long)r);
+                const int64_t g = g_lo + r, b = g / N, n = g - b * N;
+                sring[r * W + sl] = ring[(b * W + sl) * N + n];
+                ++seen[r * W + sl];
+                sl += dq;
+                r += dr;
+                if (r >= nrows) { r -= nrows; ++sl; }
+            }
         }
+        for (int64_t i = 0; i < nrows * W; ++i) CHECK(seen[i] == 1, "surf: staged float %lld written %d times", (long long)i, seen[i]);
         for (int64_t q = c0; q < c0 + nblk; ++q) {
             const int64_t b = q / per4, j0 = 4 * (q - b * per4), row = j0 / WF, kk = j0 - row * WF;
             const int f0 = (int)(kk % F);
+            const int64_t r0 = b * N + row - g_lo;           /* the staged counter the chunk reads */
+            CHECK(r0 >= 0 && r0 < nrows && (g_lo + r0) / N == b, "surf: chunk %lld reads row %lld's counter",
+                  (long long)q, (long long)r0);
             for (int kth = 0; kth < 2; ++kth) {
                 const int c = (Fm - f0) + kth * F;
                 if (c >= 4) continue;
@@ -410,7 +429,7 @@ static void emulate_surf(int B, int N, int W, int F, int CPW) {
             }
         }
     }
-    free(ring); free(sring);
+    free(ring); free(sring); free(seen);
 }
 
 /* ------------------------------------------------------------ 3. the flat one-launch step */

@@ -97,6 +97,16 @@ struct StepParams {
     FastDiv div_wf, div_f, div_w, div_units;
 };
 
+// the host-I/O step's staging outputs (env_step.h surface_body<true>, pmenv_step_host)
+struct HostIO {
+    const float* close_in;   // [B, N] obs[b, n, W-1, close] gathered by the host
+    float* chan;             // [B, N, W] channel F-1 out
+    double* value_out;       // [B] the value after the step (TradingEnv.value)
+    uint32_t* done;          // [B] completion words: env b's outputs are all in host memory once
+    uint32_t seq;            //     done[b] == seq (written last, system scope)
+};
+
+
 // The day's bar [N, F-1] of env b: a row of the per-env bar batch, or — resident
 // series mode — day[b] of a market series shared by all envs. Returns null for an
 // out-of-range day (the caller then reads NaN: the env's reward turns non-finite

@@ -1828,13 +1828,8 @@ __global__ __launch_bounds__(BLOCK) void step_tiny_kernel(StepParams p) {
 // [B, N, W] block (io.chan) beside the reward, return, post-drift weights and value
 // (io.value_out), which the host scatters into the caller's window after one stream sync.
 // The window itself never crosses the bus: only channel F-1 is the env's to write.
-struct HostIO {
-    const float* close_in;   // [B, N] obs[b, n, W-1, close] gathered by the host
-    float* chan;             // [B, N, W] channel F-1 out
-    double* value_out;       // [B] the value after the step (TradingEnv.value)
-    uint32_t* done;          // [B] completion words: env b's outputs are all in host memory once
-    uint32_t seq;            //     done[b] == seq (written last, system scope)
-};
+// HostIO: common.h
+
 
 // the host-I/O kernels' last act: every wave's stores into the mapped staging have completed
 // (vmcnt(0)) before the barrier, then one system-scope release and the env's completion word
@@ -1848,9 +1843,8 @@ __device__ __forceinline__ void hostio_done(const HostIO& io, int b) {
 }
 
 template <bool HOST>
-__device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& io) {
+__device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& io, const int b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int N = p.N, W = p.W, F = p.F;
     Scratch s = carve(lds, 0, N, F);
@@ -1929,10 +1923,55 @@ __device__ __forceinline__ void surface_body(const StepParams& p, const HostIO& 
 }
 
 static __global__ __launch_bounds__(kBlock) void step_surface_kernel(StepParams p) {
-    surface_body<false>(p, HostIO{});
+    surface_body<false>(p, HostIO{}, (int)blockIdx.x);
 }
 static __global__ __launch_bounds__(kBlock) void step_surface_host_kernel(StepParams p, HostIO io) {
-    surface_body<true>(p, io);
+    surface_body<true>(p, io, (int)blockIdx.x);
+}
+
+// The host-I/O step without a launch per call (pmenv_step_host, the reference driver's loop:
+// train/on_policy.py:59-67 steps ONE env with CPU tensors). One resident workgroup polls the
+// staging block's `go` word (system scope, over PCIe) and, each time the host posts a new tag
+// there after writing the call's inputs, runs step_surface_host_kernel's body for every env —
+// the same code, so the same bits — whose completion words the host spins on. It exits on the
+// tag 0 (the host's stop) or after `idle` ticks of s_memrealtime (100 MHz) without a new tag,
+// and stores the last tag it ran, so a relaunch picks up a tag posted as it left. Every call
+// starts with a system-scope acquire (this call's inputs, and state other launches wrote) and
+// ends with hostio_done's system-scope release (state visible to later launches on any XCD).
+struct HostRes {
+    const uint32_t* go;      // in the staging block: the tag of the call to run (0: stop)
+    uint32_t* last;          // device memory: the last tag run (read at start, written at exit)
+    uint32_t idle;           // ticks without a new tag before the workgroup exits
+};
+static __global__ __launch_bounds__(kBlock) void step_host_resident_kernel(StepParams p, HostIO io, HostRes rs) {
+    __shared__ uint32_t s_go;
+    uint32_t last = __builtin_amdgcn_readfirstlane(*rs.last);
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t g;
+            for (;;) {
+                g = __hip_atomic_load(rs.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (g != last) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)rs.idle) {
+                    g = 0u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_go = g;
+        }
+        __syncthreads();
+        const uint32_t g = __builtin_amdgcn_readfirstlane(s_go);
+        __syncthreads();                                   // s_go is free for the next poll
+        if (g == 0u) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");      // system scope
+        HostIO c = io;
+        c.seq = g;
+        for (int b = 0; b < p.B; ++b) surface_body<true>(p, c, b);
+        last = g;
+    }
+    if (threadIdx.x == 0) *rs.last = last;
 }
 
 // ---------------------------------------------------------------- the surface stream (two launches)
@@ -1969,10 +2008,27 @@ __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uin
     const uint32_t b_hi = fdiv(ql, p.div_units);
     const uint32_t g_hi = b_hi * (uint32_t)N + fdiv(4u * (ql - b_hi * per4) + 3u, p.div_wf);
     const uint32_t nrows = g_hi - g_lo + 1u;
-    for (uint32_t i = (uint32_t)tid; i < nrows * (uint32_t)W; i += BLOCK) {
-        const uint32_t sl = i / nrows, r = i - sl * nrows;
-        const uint32_t g = g_lo + r, b = g / (uint32_t)N, n = g - b * (uint32_t)N;
-        sring[r * (uint32_t)W + sl] = p.ring[((size_t)b * W + sl) * N + n];
+    // each row's counter (after the scalar step) staged beside its ring columns, so that no
+    // global load is left after the barrier; the element walk (slot i / nrows, row i % nrows)
+    // keeps its quotient and remainder by increments (a division per thread, none per element)
+    int32_t* sk = reinterpret_cast<int32_t*>(sring + (4u * CPW / WF + 2u) * (uint32_t)W);
+    if ((uint32_t)tid < nrows) {
+        const uint32_t g = g_lo + (uint32_t)tid;
+        sk[tid] = p.k[g / (uint32_t)N];
+    }
+    {
+        const uint32_t dq = (uint32_t)BLOCK / nrows, dr = (uint32_t)BLOCK - dq * nrows;
+        uint32_t sl = (uint32_t)tid / nrows, r = (uint32_t)tid - sl * nrows;
+        for (uint32_t i = (uint32_t)tid; i < nrows * (uint32_t)W; i += BLOCK) {
+            const uint32_t g = g_lo + r, b = g / (uint32_t)N, n = g - b * (uint32_t)N;
+            sring[r * (uint32_t)W + sl] = p.ring[((size_t)b * W + sl) * N + n];
+            sl += dq;
+            r += dr;
+            if (r >= nrows) {
+                r -= nrows;
+                ++sl;
+            }
+        }
     }
     __syncthreads();
     float r[V][2];
@@ -1984,10 +2040,10 @@ __global__ __launch_bounds__(BLOCK) void surface_stream_kernel(StepParams p, uin
         const uint32_t row = fdiv(j0, p.div_wf);
         const uint32_t kk = j0 - row * WF;
         const int f0 = (int)(kk - fdiv(kk, p.div_f) * (uint32_t)F);
-        const int32_t k1 = p.k[b];                               // after the scalar step
+        const uint32_t r0 = b * (uint32_t)N + row - g_lo;        // the chunk's row in the workgroup
+        const int32_t k1 = sk[r0];                               // after the scalar step (one env per chunk)
         const int idx = ring_slot(k1, W);
         const bool full = (int64_t)k1 >= W - 1;
-        const uint32_t r0 = b * (uint32_t)N + row - g_lo;        // the chunk's row in the workgroup
 #pragma unroll
         for (int kth = 0; kth < 2; ++kth) {
             const int c = (Fm - f0) + kth * F;                   // the chunk's kth weight float (>= 4: none)

@@ -118,8 +118,17 @@ struct pmenv {
     // `hio_dev` is its device address
     char* hio;
     char* hio_dev;
-    size_t hio_off[9];
+    size_t hio_off[10];
     uint32_t hio_seq;     // the last host-I/O call's completion tag
+    // the resident host-I/O step (step_host_resident_kernel): its own stream, an event recorded
+    // after its launch (complete = the workgroup has exited), the last tag it ran (device u32)
+    hipStream_t res_stream;
+    hipEvent_t res_ev;
+    uint32_t* res_last;
+    bool res_live;        // launched and not yet seen exited
+    bool dev_pending;     // an asynchronous call of this handle since its last synchronous host call
+    pmenv_dev::StepParams res_p;   // its launch arguments
+    pmenv_dev::HostIO res_io;
     int path;             // pmenv_step_path_kind
     void* tools;        // tools build: its knob state (null in the product library)
     char err[512];

@@ -326,11 +326,11 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     // in LDS, against 939 on the per-env kernel's dword writes, 892 with its writes in whole
     // chunks; cache-resident windows keep the per-env kernel: 4,096 x 30 38.3 against 48.6 in
     // whole chunks — ab_r05/surface_stream_r05s4_*, surface_ringlds_r05sr.*); the staged
-    // columns (rows x W floats) within 64 KiB
-    h->surf_lds = (size_t)(4 * 1024 / WF + 2) * c.window * 4;
+    // columns (rows x W floats) and counters (rows) within 64 KiB
+    h->surf_lds = (size_t)(4 * 1024 / WF + 2) * (c.window + 1) * 4;   // + each row's counter
     h->surf_stream = window_bytes(c) > (256ll << 20) && ((int64_t)c.num_assets * WF) % 4 == 0 &&
                      (int64_t)c.num_envs * ((int64_t)c.num_assets * WF / 4) < (1ll << 31) - 1024 &&
-                     h->surf_lds <= (64u << 10);
+                     h->surf_lds <= (64u << 10) && 4 * 1024 / WF + 2 <= 256;   // a thread per row's counter
     h->tile_floats = (int)((((int64_t)R * WF) + 3) / 4 * 4);
     h->lds_tile = scratch_bytes(h->tile_floats, c.num_assets, c.features);
     h->lds_surface = scratch_bytes(0, c.num_assets, c.features);
@@ -617,6 +617,7 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         {(const void*)step_advance_lds_kernel<false>, h->lds_tile},
         {(const void*)step_surface_kernel, h->lds_surface},
         {(const void*)step_surface_host_kernel, h->lds_surface},
+        {(const void*)step_host_resident_kernel, h->lds_surface},
         {(const void*)step_small_kernel<64, 32, false>, h->lds_surface},
         {(const void*)step_small_kernel<256, 8, false>, h->lds_surface},
         {(const void*)step_small_kernel<256, 16, false>, h->lds_surface},
@@ -643,6 +644,10 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
     return PMENV_OK;
 }
 
+namespace {
+void res_stop(pmenv* h);    // the resident host-I/O step (below)
+}
+
 int pmenv_destroy(pmenv* h) {
     if (!h) return PMENV_ERR_ARG;
     DeviceGuard g(h->device);
@@ -651,7 +656,15 @@ int pmenv_destroy(pmenv* h) {
     if (h->halo) (void)hipFree(h->halo);
     if (h->snap) (void)hipFree(h->snap);
     if (h->relay_mem) (void)hipFree(h->relay_mem);
-    if (h->hio) (void)hipHostFree(h->hio);
+    if (h->hio) {
+        res_stop(h);
+        (void)hipHostFree(h->hio);
+    }
+    if (h->res_stream) {
+        (void)hipEventDestroy(h->res_ev);
+        (void)hipStreamDestroy(h->res_stream);
+        (void)hipFree(h->res_last);
+    }
     free(h);
     return PMENV_OK;
 }
@@ -683,6 +696,7 @@ int pmenv_set_step_path(pmenv* h, int32_t path) {
 
 int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     if (obs && !aligned4(obs)) { set_err(h, "obs not 4-byte aligned"); return PMENV_ERR_ALIGN; }
     DeviceGuard g(h->device);
     StepParams p = base_params(h);
@@ -693,6 +707,7 @@ int pmenv_reset(pmenv* h, float* obs, const uint8_t* mask, hipStream_t stream) {
 
 int pmenv_step_ex(pmenv* h, const pmenv_step_args* a, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     if (!a || !a->action) { set_err(h, "action is required"); return PMENV_ERR_ARG; }
     if (!a->bar && !a->prices) { set_err(h, "surface mode (bar == NULL) needs prices"); return PMENV_ERR_ARG; }
     if (a->bar && !a->obs) { set_err(h, "advance mode (bar != NULL) needs obs"); return PMENV_ERR_ARG; }
@@ -824,15 +839,16 @@ int pmenv_step(pmenv* h, const float* action, const float* prices, const float* 
 namespace {
 // The host-I/O staging block (allocated on first use, freed by destroy): f32 action |
 // prices | closes [B*N] each, channel [B*N*W], weights [B*N], reward [B]; f64 return |
-// value [B]. Pinned and device-mapped, so the kernels read and write it over PCIe directly.
+// value [B]; u32 completion words [B]; the resident step's go word. Pinned and device-mapped,
+// so the kernels read and write it over PCIe directly.
 int hio_ensure(pmenv* h) {
     if (h->hio) return PMENV_OK;
     const size_t B = (size_t)h->cfg.num_envs, BN = B * (size_t)h->cfg.num_assets;
     auto up64 = [](size_t x) { return (x + 63) / 64 * 64; };
     size_t o = 0;
-    const size_t sizes[9] = {BN * 4, BN * 4, BN * 4, BN * (size_t)h->cfg.window * 4, BN * 4, B * 4, B * 8, B * 8,
-                             B * 4};
-    for (int i = 0; i < 9; ++i) {
+    const size_t sizes[10] = {BN * 4, BN * 4, BN * 4, BN * (size_t)h->cfg.window * 4, BN * 4, B * 4, B * 8, B * 8,
+                              B * 4, 4};
+    for (int i = 0; i < 10; ++i) {
         h->hio_off[i] = o;
         o = up64(o + sizes[i]);
     }
@@ -854,10 +870,11 @@ int hio_ensure(pmenv* h) {
     h->hio = (char*)p;
     h->hio_dev = (char*)d;
     memset(h->hio + h->hio_off[8], 0, B * 4);      // completion words: no call yet (tags start at 1)
+    memset(h->hio + h->hio_off[9], 0, 4);          // the go word: no tag posted
     h->hio_seq = 0;
     return PMENV_OK;
 }
-enum { kHioAct, kHioPri, kHioClose, kHioChan, kHioW, kHioRew, kHioRet, kHioVal, kHioDone };
+enum { kHioAct, kHioPri, kHioClose, kHioChan, kHioW, kHioRew, kHioRet, kHioVal, kHioDone, kHioGo };
 template <class T>
 T* hio_host(const pmenv* h, int f) { return reinterpret_cast<T*>(h->hio + h->hio_off[f]); }
 template <class T>
@@ -909,6 +926,82 @@ int hio_sync(pmenv* h, hipStream_t stream, const char* what) {
     }
     return PMENV_OK;
 }
+
+// ---- the resident host-I/O step (step_host_resident_kernel): no launch per call
+constexpr int kResMaxEnvs = 8;             // one workgroup steps every env in turn
+constexpr uint32_t kResIdle = 2000000u;    // 20 ms of s_memrealtime (100 MHz) without a call: it exits
+
+// the workgroup exits (the stop tag) and the handle forgets it (destroy, or its launch
+// arguments no longer match the call's)
+void res_stop(pmenv* h) {
+    if (!h->res_live) return;
+    __atomic_store_n(hio_host<uint32_t>(h, kHioGo), 0u, __ATOMIC_RELEASE);
+    (void)hipEventSynchronize(h->res_ev);
+    h->res_live = false;
+}
+
+int res_launch(pmenv* h, const StepParams& p, const HostIO& io) {
+    if (!h->res_stream) {
+        if (hipStreamCreateWithFlags(&h->res_stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&h->res_ev, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc((void**)&h->res_last, 64) != hipSuccess || hipMemset(h->res_last, 0, 64) != hipSuccess) {
+            set_err(h, "resident host-I/O step: stream / event / memory");
+            return PMENV_ERR_HIP;
+        }
+    }
+    // the go word holds the last tag posted (or 0): a fresh workgroup starts from what the
+    // previous one ran, so an unseen tag is run and a seen one is not run twice
+    HostRes rs;
+    rs.go = hio_dev<uint32_t>(h, kHioGo);
+    rs.last = h->res_last;
+    rs.idle = kResIdle;
+    step_host_resident_kernel<<<1, kBlock, h->lds_surface, h->res_stream>>>(p, io, rs);
+    if (const int rc = check_launch(h, "step_host_resident_kernel")) return rc;
+    if (hipEventRecord(h->res_ev, h->res_stream) != hipSuccess) {
+        set_err(h, "resident host-I/O step: event record");
+        return PMENV_ERR_HIP;
+    }
+    h->res_live = true;
+    h->res_p = p;
+    h->res_io = io;
+    return PMENV_OK;
+}
+
+// post the call's tag (its inputs are in the staging: stored before, released with the tag) and
+// spin on the completion words; a workgroup that exited idle before it saw the tag is relaunched
+int res_step(pmenv* h, const StepParams& p, const HostIO& io) {
+    const bool same = h->res_live && memcmp(&h->res_p, &p, sizeof p) == 0 &&
+                      h->res_io.close_in == io.close_in && h->res_io.chan == io.chan &&
+                      h->res_io.value_out == io.value_out && h->res_io.done == io.done;
+    if (!same) res_stop(h);
+    if (!h->res_live || hipEventQuery(h->res_ev) == hipSuccess)
+        if (const int rc = res_launch(h, p, io)) return rc;
+    __atomic_store_n(hio_host<uint32_t>(h, kHioGo), io.seq, __ATOMIC_RELEASE);
+    const volatile uint32_t* done = hio_host<volatile uint32_t>(h, kHioDone);
+    const int B = h->cfg.num_envs;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1;; ++it) {
+        int b = 0;
+        while (b < B && done[b] == io.seq) ++b;
+        if (b == B) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);        // the outputs are read after the words
+            return PMENV_OK;
+        }
+        if ((it & 1023u) == 0u) {
+            const hipError_t q = hipEventQuery(h->res_ev);
+            if (q == hipSuccess) {                          // exited idle as the tag arrived: relaunch
+                if (const int rc = res_launch(h, p, io)) return rc;
+            } else if (q != hipErrorNotReady) {
+                set_err(h, "step_host_resident_kernel: %s", hipGetErrorString(q));
+                return PMENV_ERR_HIP;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                set_err(h, "step_host_resident_kernel: no completion within 2 s");
+                return PMENV_ERR_HIP;
+            }
+        }
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -923,6 +1016,12 @@ int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* o
         return PMENV_ERR_ARG;
     }
     if (const int rc = hio_ensure(h)) return rc;
+    // the resident workgroup (no launch per call) for a few envs when none of this handle's own
+    // device work can be pending (what the call would otherwise be ordered after on `stream`);
+    // else one launch on `stream`
+    // (dev_pending: this handle enqueued device work since its last synchronous call — the
+    // ordering a launch on `stream` gives; hipStreamQuery would cost ~9 us per call)
+    const bool resident = h->cfg.num_envs <= kResMaxEnvs && !h->dev_pending;
     const pmenv_cfg& c = h->cfg;
     const size_t B = (size_t)c.num_envs, BN = B * (size_t)c.num_assets;
     memcpy(hio_host<float>(h, kHioAct), action, BN * 4);
@@ -941,8 +1040,13 @@ int pmenv_step_host(pmenv* h, const float* action, const float* prices, float* o
     io.value_out = hio_dev<double>(h, kHioVal);
     io.done = hio_dev<uint32_t>(h, kHioDone);
     io.seq = h->hio_seq = h->hio_seq + 1u == 0u ? 1u : h->hio_seq + 1u;
-    step_surface_host_kernel<<<c.num_envs, kBlock, h->lds_surface, stream>>>(p, io);
-    if (const int rc = hio_sync(h, stream, "step_surface_host_kernel")) return rc;
+    if (resident) {
+        if (const int rc = res_step(h, p, io)) return rc;
+    } else {
+        step_surface_host_kernel<<<c.num_envs, kBlock, h->lds_surface, stream>>>(p, io);
+        if (const int rc = hio_sync(h, stream, "step_surface_host_kernel")) return rc;
+        h->dev_pending = false;                     // everything before it on `stream` has run
+    }
     if (obs) hio_scatter_channel(h, obs);
     if (reward) memcpy(reward, hio_host<float>(h, kHioRew), B * 4);
     if (ret) memcpy(ret, hio_host<double>(h, kHioRet), B * 8);
@@ -970,6 +1074,7 @@ int pmenv_reset_host(pmenv* h, float* obs, double* value, hipStream_t stream) {
     io.seq = h->hio_seq = h->hio_seq + 1u == 0u ? 1u : h->hio_seq + 1u;
     reset_kernel<<<h->cfg.num_envs, kBlock, 0, stream>>>(p, nullptr, nullptr, io);
     if (const int rc = hio_sync(h, stream, "reset_kernel (host I/O)")) return rc;
+    h->dev_pending = false;
     if (obs) hio_scatter_channel(h, obs);
     if (value) memcpy(value, hio_host<double>(h, kHioVal), (size_t)h->cfg.num_envs * 8);
     return PMENV_OK;
@@ -1017,6 +1122,7 @@ const char* pmenv_step_path(const pmenv* h) {
 
 int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
     if (!h || !dst) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     DeviceGuard g(h->device);
     hipError_t e = hipMemcpyAsync(dst, h->state, h->state_bytes, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) { set_err(h, "get_state: %s", hipGetErrorString(e)); return PMENV_ERR_HIP; }
@@ -1025,6 +1131,7 @@ int pmenv_get_state(pmenv* h, void* dst, hipStream_t stream) {
 
 int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
     if (!h || !src) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     DeviceGuard g(h->device);
     if (const int rc = flat1_invalidate(h, stream)) return rc;
     hipError_t e = hipMemcpyAsync(h->state, src, h->state_bytes, hipMemcpyDeviceToDevice, stream);
@@ -1034,6 +1141,7 @@ int pmenv_set_state(pmenv* h, const void* src, hipStream_t stream) {
 
 int pmenv_window_written(pmenv* h, const float* obs, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     (void)obs;                                 // any window: the halo is dropped whichever it was
     DeviceGuard g(h->device);
     return flat1_invalidate(h, stream, kInvalHalo);
@@ -1041,12 +1149,14 @@ int pmenv_window_written(pmenv* h, const float* obs, hipStream_t stream) {
 
 int pmenv_state_written(pmenv* h, hipStream_t stream) {
     if (!h) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     DeviceGuard g(h->device);
     return flat1_invalidate(h, stream, kInvalSnap | kInvalHalo);
 }
 
 int pmenv_nonfinite_count(pmenv* h, uint64_t* out, hipStream_t stream) {
     if (!h || !out) return PMENV_ERR_ARG;
+    h->dev_pending = true;                          // device work of this handle may be in flight
     DeviceGuard g(h->device);
     unsigned long long v = 0;
     hipError_t e = hipMemcpyAsync(&v, h->nonfinite, 8, hipMemcpyDeviceToHost, stream);

@@ -184,6 +184,44 @@ def test_gpu_host_io_direct_equals_staged_bitwise(B, N, W, F):
         assert np.array_equal(a, b)
 
 
+def test_gpu_host_io_resident_across_idle_exits_and_device_steps():
+    """pmenv_step_host runs in one resident workgroup (no launch per call) that exits after
+    20 ms without a call and is relaunched on the next; device-tensor steps of the same handle
+    run between host steps. Bitwise what the staged path gives for the same sequence."""
+    import time
+    from pmenv import TradingEnv
+    N, W, F, T = 7, 12, 5, 40
+    rng = np.random.default_rng(77)
+    wins = rng.uniform(0.5, 1.5, (T + 1, N, W, F)).astype(np.float32)
+    acts = rng.standard_normal((T + 1, N)).astype(np.float32)
+    prices = rng.uniform(0.95, 1.05, (T + 1, N)).astype(np.float32)
+    res = []
+    for direct in (True, False):
+        env = TradingEnv(num_envs=1, num_assets=N, window=W, features=F, device="cuda:0")
+        env._HOST_DIRECT = direct
+        rec = []
+        for t in range(T + 1):
+            x = torch.tensor(wins[t])
+            if t == 0:
+                env.reset(x)
+                continue
+            if t % 9 == 4:                                   # the resident workgroup exits idle
+                time.sleep(0.03)
+            if t % 7 == 3:                                   # a device-tensor step on the same handle
+                xd = x.to("cuda:0")
+                r, _ = env.step(torch.tensor(acts[t]).reshape(N, 1).to("cuda:0"), xd, torch.tensor(prices[t]).to("cuda:0"))
+                x = xd.cpu()
+            else:
+                r, _ = env.step(torch.tensor(acts[t]).reshape(N, 1), x, torch.tensor(prices[t]))
+            v = torch.as_tensor(env.value).detach().to("cpu", torch.float64).numpy().copy()
+            rec.append((r.detach().cpu().numpy().copy(), v, x.numpy().copy()))
+        res.append(rec)
+    for (ra, va, xa), (rb, vb, xb) in zip(*res):
+        assert np.array_equal(np.atleast_1d(ra).view(np.uint8), np.atleast_1d(rb).view(np.uint8))
+        assert np.array_equal(np.atleast_1d(va).view(np.uint8), np.atleast_1d(vb).view(np.uint8))
+        assert np.array_equal(xa.view(np.uint8), xb.view(np.uint8))
+
+
 def test_gpu_given_dims_are_checked_against_the_first_tensor():
     """A dimension the constructor fixes is not rebound: a window of another shape raises
     ValueError (as the reference's fixed-size ring fails on it)."""

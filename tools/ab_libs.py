@@ -23,6 +23,7 @@ ap.add_argument("--libs", required=True)
 ap.add_argument("--envs", type=int, default=8192)
 ap.add_argument("--assets", type=int, default=30)
 ap.add_argument("--window", type=int, default=50)
+ap.add_argument("--features", type=int, default=5, help="F (the bar has F - 1 channels, close at 3)")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--H", type=int, default=48, help="distinct days of bars / actions (cycled)")
@@ -37,7 +38,7 @@ a = ap.parse_args()
 
 dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
-B, N, W, F = a.envs, a.assets, a.window, 5
+B, N, W, F = a.envs, a.assets, a.window, a.features
 # "lib.so+KNOB=VAL+...": tools-build knobs set while that variant's handle is created
 specs = [x.split("+") for x in a.libs.split(",")]
 libs = [sp[0] if os.path.isabs(sp[0]) else os.path.join(ROOT, sp[0]) for sp in specs]
@@ -50,12 +51,13 @@ STEP_PATHS = _abi.STEP_PATHS
 g = torch.Generator(device=dev).manual_seed(7)
 # a positive OHLC random walk (the values only need to be plausible prices)
 close = torch.exp(torch.cumsum(torch.randn(a.H + W, B, N, 1, generator=g, device=dev) * 0.015, 0))
-ser = torch.cat([close * 1.001, close * 1.01, close * 0.99, close], dim=3)
+ser = torch.cat([close * 1.001, close * 1.01, close * 0.99, close] +
+                [close * (1.0 + 0.001 * c) for c in range(F - 5)], dim=3)[..., :F - 1].contiguous()
 del close
 act = torch.softmax(torch.randn(a.H, B, N, generator=g, device=dev), dim=-1)
 obs0 = torch.empty(B, N, W, F, device=dev)
-obs0[..., :4] = ser[:W].permute(1, 2, 0, 3)
-obs0[..., 4] = 0.0
+obs0[..., :F - 1] = ser[:W].permute(1, 2, 0, 3)
+obs0[..., F - 1] = 0.0
 
 
 def bind(path):
