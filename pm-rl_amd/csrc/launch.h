@@ -307,7 +307,7 @@ inline void launch_flat1(pmenv* h, StepParams p, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------- one launch, relayed (step_relay.h)
-template <int BLOCK, int POL, bool OUT, bool SEQ, bool ANY = false>
+template <int BLOCK, int POL, bool OUT, bool SEQ, int ANY = 0>
 inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
                            hipStream_t stream) {
     const uint32_t q = h->flat_qtot;
@@ -321,7 +321,7 @@ inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParam
     default: step_relay_kernel<BLOCK, 2, POL, OUT, 64, 8, 8, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     }
 }
-template <int BLOCK, int POL, bool ANY = false>
+template <int BLOCK, int POL, int ANY = 0>
 inline void launch_relay_b(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid, bool out,
                            bool seq, hipStream_t stream) {
     if (out) {

@@ -132,6 +132,36 @@ __device__ __forceinline__ KArgs kargs() {
     return k;
 }
 
+// Tools build only (step_relay_kernel<..., ANY = 2>, PMENV_RELAY_STAMPS: the product's order and
+// polls): thread 0 of each workgroup reads s_memrealtime (100 MHz) at the phases of its role — each
+// read issued once `dep` (a value of the phase's last load) has arrived, DRAIN: once the wave's
+// stores have completed — holds the stamps in scalar registers and stores them at its end into
+// g_relay_stamps[epoch % kStampSlots][bid][k] (tools/relay_stamps.py); a null pointer stores none.
+// The product's instantiations (ANY = 0) hold no stamp code.
+constexpr uint32_t kStampSlots = 16, kStampMaxWg = 40960;
+static __device__ uint64_t* g_relay_stamps;
+template <bool ST, bool DRAIN = false>
+__device__ __forceinline__ uint64_t relay_clock(uint32_t dep) {
+    uint64_t t = 0;
+    if constexpr (ST) {
+        if constexpr (DRAIN)
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep) : "memory");
+        else
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep) : "memory");
+    }
+    return t;
+}
+template <bool ST, int K>
+__device__ __forceinline__ void relay_stamps_put(uint32_t bid, uint32_t epoch, const uint64_t (&ts)[K]) {
+    if constexpr (ST) {
+        uint64_t* s = g_relay_stamps;
+        if (s && threadIdx.x == 0 && bid < kStampMaxWg) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[((size_t)(epoch % kStampSlots) * kStampMaxWg + bid) * 8 + k] = ts[k];
+        }
+    }
+}
+
 __device__ __forceinline__ void relay_put(uint64_t* w, uint32_t epoch, uint32_t bits) {
     __hip_atomic_store(w, ((uint64_t)epoch << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -154,9 +184,10 @@ __device__ __forceinline__ uint32_t relay_list_read(const RelayParams& r, uint32
 // form, KL lanes x KA strided assets (scalar_step_vec_kernel<KL, KA, true>). Only w' goes
 // through the relay words; the counter of the next step goes to kp_out (read after this
 // launch has ended).
-template <int BLOCK, int KL, int KA>
+template <int BLOCK, int KL, int KA, bool ST = false>
 __device__ __forceinline__ uint32_t relay_scalar(const StepParams& p, const RelayParams& r, int s, uint32_t epoch,
-                                                 int32_t* kp_out) {
+                                                 int32_t* kp_out, uint64_t t_entry = 0) {
+    uint64_t ts[3] = {t_entry, 0, 0};
     constexpr int EPW = 64 / KL, EPB = (BLOCK / 64) * EPW;
     const int lane = threadIdx.x & 63;
     const int b = s * EPB + (int)(threadIdx.x >> 6) * EPW + lane / KL;
@@ -171,6 +202,7 @@ __device__ __forceinline__ uint32_t relay_scalar(const StepParams& p, const Rela
         if (env_ok && j < N) relay_put(r.w + (size_t)b * N + j, epoch, __float_as_uint(m.wp));
         if (env_ok && j == 0) kp_out[b] = m.k + 1;
         listed = relay_list_read(r, epoch);
+        ts[1] = relay_clock<ST>(listed);                            // its words published
         scalar_tail<KL>(p, b, lane, in, m);
     } else {
         const VecIn<KA> in = vec_load<KL, KA, true>(p, b, lane);
@@ -182,8 +214,11 @@ __device__ __forceinline__ uint32_t relay_scalar(const StepParams& p, const Rela
         }
         if (env_ok && j == 0) kp_out[b] = in.k + 1;
         listed = relay_list_read(r, epoch);
+        ts[1] = relay_clock<ST>(listed);
         vec_tail<KL, KA, true>(p, b, lane, in, m);
     }
+    ts[2] = relay_clock<ST, true>(0);                               // its state written
+    relay_stamps_put<ST>((uint32_t)s, epoch, ts);
     return listed;
 }
 
@@ -198,11 +233,12 @@ __device__ __forceinline__ uint32_t relay_scalar(const StepParams& p, const Rela
 // after the re-check, or by a scalar block), which polls once, returns false if a word is missing,
 // and else runs only under the tile's claim (one run per step: in place, a second run would shift
 // the window twice).
-template <int BLOCK, int V, int POL, bool OUT, bool ADOPT>
+template <int BLOCK, int V, int POL, bool OUT, bool ADOPT, bool ST = false>
 __device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParams& r, uint32_t qtot, uint32_t spin, uint32_t t,
                                            uint32_t epoch, const int32_t* kp_in, const float* halo_in,
                                            float* halo_out, f4* sh4, f4* sh_bar, float* sh_wp, int32_t* sh_kc,
-                                           int32_t* sh_ok) {
+                                           int32_t* sh_ok, uint64_t t_entry = 0) {
+    uint64_t ts[6] = {t_entry, 0, 0, 0, 0, 0};
     constexpr int kAux = POL == 1 ? 2 : 0;
     constexpr int CPW = BLOCK * V, F = 5;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -238,6 +274,7 @@ __device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParam
     // w': relayed by the scalar blocks, polled `spin` times at most (ADOPT: once)
     ww = relay_get(r.w + g);
     bool ready = !mine || (uint32_t)(ww >> 32) == epoch;
+    ts[1] = relay_clock<ST>((uint32_t)ww);                          // its loads returned
     for (uint32_t polls = 0; !ADOPT && !__all(ready) && polls < spin; ++polls) {
         __builtin_amdgcn_s_sleep(2);
         if (!ready) {
@@ -246,6 +283,7 @@ __device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParam
         }
     }
     const bool wave_ok = __all(ready);                              // the whole wave, before any branch
+    ts[2] = relay_clock<ST>((uint32_t)ww);                          // wave 0's words arrived
     if (mine) {
         sh_bar[tid] = xb;
         sh_wp[tid] = __uint_as_float((uint32_t)ww);
@@ -256,6 +294,7 @@ __device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParam
     if (tid < 2) sh4[CPW + tid] = hal;
     if (lane == 0) sh_ok[wave] = wave_ok ? 1 : 0;
     __syncthreads();
+    ts[3] = relay_clock<ST>(0);                                     // every wave staged
     if constexpr (ADOPT) {                                          // polled once; then the tile's claim
         bool tile_ok = true;
 #pragma unroll
@@ -297,6 +336,9 @@ __device__ __forceinline__ bool relay_tile(const StepParams& p, const RelayParam
         buf_store4<kAux>(rd, ok ? (uint32_t)j * 16u : 0x80000000u, o);  // past the end: dropped
         if (ok && first_out && j < 2) reinterpret_cast<f4*>(halo_out)[2 * (t - 1) + j] = o;
     }
+    ts[4] = relay_clock<ST>(0);                                     // its stores issued
+    ts[5] = relay_clock<ST, true>(0);                               // its stores completed
+    relay_stamps_put<ST>(r.scal + t, epoch, ts);
     return ok;
 }
 
@@ -362,10 +404,10 @@ __device__ __forceinline__ void relay_defer(uint32_t t, f4* sh4, f4* sh_bar, flo
 // policy (0 default, 1 nt), (KL, KA) the scalar step's form (relay_scalar), OCC the waves
 // per SIMD the kernel is held to (the 8-assets-per-lane form would otherwise take 84 VGPRs
 // and cut the tiles to 5 waves per SIMD)
-// ANY (tools build only): the dispatch order and the polls before a tile defers from the launch
-// arguments (r.rot, r.spin), to force the deferral paths; the product takes blockIdx order and
-// kRelaySpin
-template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1, bool SEQ = false, bool ANY = false>
+// ANY (tools build only): 1 — the dispatch order and the polls before a tile defers from the launch
+// arguments (r.rot, r.spin), to force the deferral paths; 2 — the product's code with wall-clock
+// stamps (relay_clock). The product (0) takes blockIdx order and kRelaySpin.
+template <int BLOCK, int V, int POL, bool OUT, int KL, int KA, int OCC = 1, bool SEQ = false, int ANY = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void step_relay_kernel(
     StepParams p, RelayParams r, uint32_t qtot) {
     __shared__ f4 sh4[BLOCK * V + 2];
@@ -384,16 +426,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) vo
             r.seq[kSeqHobs + 1] = (uint32_t)(hobs >> 32);
         }
     }
+    constexpr bool kSt = ANY == 2;
+    const uint64_t t_entry = relay_clock<kSt>(0);
     uint32_t bid = blockIdx.x;
-    if constexpr (ANY) {
+    if constexpr (ANY == 1) {
         bid += r.rot;
         if (bid >= r.grid) bid -= r.grid;
     }
     if (bid < r.scal) {
-        const uint32_t listed = relay_scalar<BLOCK, KL, KA>(p, r, (int)bid, c.epoch, c.kp_out);
+        const uint32_t listed = relay_scalar<BLOCK, KL, KA, kSt>(p, r, (int)bid, c.epoch, c.kp_out, t_entry);
         relay_adopt<BLOCK, V, POL, OUT, SEQ>(sh4, sh_bar, sh_wp, sh_kc, sh_ok, listed);
-    } else if (!relay_tile<BLOCK, V, POL, OUT, false>(p, r, qtot, ANY ? r.spin : kRelaySpin, bid - r.scal, c.epoch, c.kp_in, c.halo_in, c.halo_out,
-                                                      sh4, sh_bar, sh_wp, sh_kc, sh_ok)) {
+    } else if (!relay_tile<BLOCK, V, POL, OUT, false, kSt>(p, r, qtot, ANY == 1 ? r.spin : kRelaySpin, bid - r.scal, c.epoch,
+                                                           c.kp_in, c.halo_in, c.halo_out, sh4, sh_bar, sh_wp, sh_kc,
+                                                           sh_ok, t_entry)) {
         relay_defer<BLOCK, V, POL, OUT, SEQ>(bid - r.scal, sh4, sh_bar, sh_wp, sh_kc, sh_ok);
     }
 }

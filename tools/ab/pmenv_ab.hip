@@ -44,6 +44,7 @@ struct Tools {
     int stream_block = 512;     // PMENV_STREAM_BLOCK: row-kernel workgroup (128 | 256)
     int relay_spin = -1;        // PMENV_RELAY_SPIN: a tile's polls before it runs a missing unit (-1: product's)
     bool relay_tiles_first = false;   // PMENV_RELAY_TILES_FIRST: the tiles at blockIdx 0.., the scalar blocks last
+    bool relay_stamps = false;  // PMENV_RELAY_STAMPS: the product's relay step with wall-clock stamps (step_relay.h)
     int stream_pol = 0;         // PMENV_STREAM_POL: 0 | 1 (nt) | 2 (sc0 nt)
     int flat_block = 512;       // PMENV_FLAT_BLOCK: the ds_bpermute stream's workgroup
     bool flat_db_wg = true;     // PMENV_FLAT_DB_WG=0: the ds_bpermute double-buffered stream
@@ -357,6 +358,7 @@ void plan(pmenv* h) {
     }
     t->relay_spin = knob_int("PMENV_RELAY_SPIN", -1);
     t->relay_tiles_first = knob_int("PMENV_RELAY_TILES_FIRST", 0) != 0;
+    t->relay_stamps = knob_int("PMENV_RELAY_STAMPS", 0) != 0;
     if (const char* k = knob("PMENV_SMALL_GEOM")) {   // step_small_kernel's BLOCK x E: 64x32 | 256x8 | 256x16 | ...
         int bk = 0, e = 0;
         const int64_t nwf = (int64_t)c.num_assets * c.window * c.features;
@@ -672,7 +674,7 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     // its first miss) and / or PMENV_RELAY_TILES_FIRST=1 (blockIdx rotated so every tile precedes
     // every scalar block: the tiles fill the chip and run the scalar steps themselves)
     RelayParams rr = r;
-    const bool mod = tt && (tt->relay_spin >= 0 || tt->relay_tiles_first);
+    const bool mod = tt && (tt->relay_spin >= 0 || tt->relay_tiles_first || tt->relay_stamps);
     if (tt && tt->relay_spin >= 0) rr.spin = (uint32_t)tt->relay_spin;
     if (tt && tt->relay_tiles_first) rr.rot = r.scal;
     const bool out = p.obs_out != p.obs;
@@ -686,8 +688,11 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     case 5124: relay_geom<512, 4>(h, p, rr, q, grid, out, stream); return true;
     default:
         if (!mod) return false;
-        if (h->relay_block == 256) launch_relay_b<256, 0, true>(h, p, rr, grid, out, false, stream);
-        else launch_relay_b<512, 1, true>(h, p, rr, grid, out, false, stream);
+        if (tt->relay_stamps && tt->relay_spin < 0 && !tt->relay_tiles_first) {   // the product's code, stamped
+            if (h->relay_block == 256) launch_relay_b<256, 0, 2>(h, p, rr, grid, out, false, stream);
+            else launch_relay_b<512, 1, 2>(h, p, rr, grid, out, false, stream);
+        } else if (h->relay_block == 256) launch_relay_b<256, 0, 1>(h, p, rr, grid, out, false, stream);
+        else launch_relay_b<512, 1, 1>(h, p, rr, grid, out, false, stream);
         return true;
     }
 }
@@ -1096,6 +1101,18 @@ bool batch_reward_forward(const float* a, const float* v_prev, const float* p, i
 }
 
 }  // namespace pmenv_tools
+
+// the relay step's stamps (PMENV_RELAY_STAMPS, step_relay.h relay_clock): `buf` (device, kStampSlots x
+// kStampMaxWg x 8 u64, zeroed by the caller) receives them from the next launches on; null stops them
+extern "C" int pmenv_tools_relay_stamps(uint64_t* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(pmenv_dev::g_relay_stamps), &buf, sizeof(buf), 0, hipMemcpyHostToDevice) ==
+                   hipSuccess ? 0 : 1;
+}
+extern "C" int pmenv_tools_relay_stamp_dims(uint32_t* slots, uint32_t* max_wg) {
+    *slots = pmenv_dev::kStampSlots;
+    *max_wg = pmenv_dev::kStampMaxWg;
+    return 0;
+}
 
 // the stamps of small_stamp_kernel (PMENV_SMALL_ABL), 1024 launches x 8 u64 (100 MHz ticks)
 extern "C" int pmenv_tools_small_stamps(uint64_t* out) {
