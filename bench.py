@@ -583,6 +583,8 @@ def main():
             "reference_goldens": ref_gold,
             "nonfinite_envs": nonfinite,
             "step_path": env.step_path,
+            # the library this line measured (the configs summaries print it: tools/bench_configs.sh)
+            "library": {"path": os.path.relpath(_abi.LIB_PATH, ROOT), "sha256": lib_sha, "src_sha256": src_sha},
             "knobs": knobs,
             "alt": alt,
             "collective": collective,

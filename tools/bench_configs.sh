@@ -4,7 +4,7 @@ TAG=${1:-r02}
 mkdir -p gpurun_out/configs_$TAG
 run() { name=$1; shift; timeout -k 10 600 python bench.py "$@" > gpurun_out/configs_$TAG/cfg_$name.json 2> gpurun_out/configs_$TAG/cfg_$name.err || return $?; python -c "
 import json; d=json.loads(open('gpurun_out/configs_$TAG/cfg_$name.json').read().strip().splitlines()[-1]); rf=d['roofline']
-print('$name', f\"{d['value']/1e6:.1f}M env-steps/s\", f\"{d['ms_per_step']:.4f} ms\", f\"{rf['kernel']} {rf['kernel_us']['median']:.1f} us frac {rf['frac']:.3f} step {rf['frac_step']:.3f}\", 'l3_resident', rf['l3_resident'], 'mae', d['reward_mae'], 'cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']/1e6,2))" | tee -a gpurun_out/configs_$TAG/summary.txt; }
+print('$name', 'lib', d['library']['sha256'][:16], 'src', (d['library']['src_sha256'] or '')[:16], f\"{d['value']/1e6:.1f}M env-steps/s\", f\"{d['ms_per_step']:.4f} ms\", f\"{rf['kernel']} {rf['kernel_us']['median']:.1f} us frac {rf['frac']:.3f} step {rf['frac_step']:.3f}\", 'l3_resident', rf['l3_resident'], 'mae', d['reward_mae'], 'cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value']/1e6,2))" | tee -a gpurun_out/configs_$TAG/summary.txt; }
 run c2_4096x30 --envs-per-gpu 4096 --steps 200 --warmup 20 &&
 run c3_16384x30 --envs-per-gpu 16384 --steps 200 --warmup 20 &&
 run c4share_8192x30 --envs-per-gpu 8192 --steps 200 --warmup 20 &&

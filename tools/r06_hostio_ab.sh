@@ -1,4 +1,6 @@
 #!/bin/bash
+# (tools/libpmenv_base.so: the round-5 library, pm-rl_amd/csrc of commit fc5c583 built with build.py's flags;
+#  removed from the tree after round 6's A/B runs — rebuild it from that commit to re-run)
 # Round 6: the host-I/O step per library (PMENV_LIB): the reference driver's loop and the raw C ABI call
 set -o pipefail
 T=${1:-r06}

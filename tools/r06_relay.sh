@@ -1,4 +1,6 @@
 #!/bin/bash
+# (tools/libpmenv_base.so: the round-5 library, pm-rl_amd/csrc of commit fc5c583 built with build.py's flags;
+#  removed from the tree after round 6's A/B runs — rebuild it from that commit to re-run)
 # Round 6: the relay step's forward-progress deferral and the F <= 16 generic stream on the GPU box.
 #   bash tools/r06_relay.sh TAG [quick]
 # 1. the relay GPU tests and the generic-stream / register-step parity tests on the product

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (tools/libpmenv_base.so: the round-5 library, pm-rl_amd/csrc of commit fc5c583 built with build.py's flags;
+#  removed from the tree after round 6's A/B runs — rebuild it from that commit to re-run)
 # Round 6: the surface stream with staged counters and the F <= 16 generic stream, against the
 # round-5 library (tools/libpmenv_base.so), one process per comparison, bits compared.
 #   bash tools/r06_streams.sh TAG
