@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the edit: profiles/r06/relay_stamps/compose_branchfree_edit.py, applied by a variant build;
+#  the variant library was removed after the run, r06o)
 # Round 6: compose2's last-day / slot patch written with bitwise selects instead of short-circuit
 # conditions (no exec-mask branches; the same values) — tools/libpmenv_vcompose.so, built from the
 # working tree with that edit — against the product, in process, bits compared.
