@@ -1,4 +1,5 @@
 #!/bin/bash
+# (tools/libpmenv_r05.so was removed from the tree after the run, r06p: rebuild it from fc5c583 to re-run)
 # Round 6: the cache-resident shares through bench.py itself, the round-6 product against the
 # round-5 library (tools/libpmenv_r05.so: pm-rl_amd/csrc of commit fc5c583 built with build.py's
 # flags), alternating on one box (the box copy's libpmenv.so swapped between runs, restored at
