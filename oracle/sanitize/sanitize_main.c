@@ -1230,7 +1230,7 @@ int main(void) {
             for (int cpw = 0; cpw < 2; ++cpw)
                 emulate_flat1(fshapes[i][0], fshapes[i][1], fshapes[i][2], cpw ? 1024 : 96, 2 * fshapes[i][2] + 3,
                               storage);
-    /* the relayed step: the product's 256 x 2 and 512 x 2 tiles, small tiles that put many
+    /* the relayed step: the product's 256 x 2 and 512 x 2 tiles (256 x 4 below), small tiles that put many
      * rows and envs in one tile, the register (32 / 64 lanes) and packed (8 / 16 lanes)
      * scalar forms' blocks, W = 2 (every day a last day), both ring orders, in place and
      * double-buffered; every dispatch model, the fallback after 0 to 3 polls */
@@ -1244,6 +1244,14 @@ int main(void) {
                     for (int bk = 0; bk < 3; ++bk)
                         emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], bks[bk], 2, rshapes[i][3], 12, storage,
                                       db, model, (int)(urand() * 4));
+    /* the 256 x 4 tiles AUTO gives the largest cache-resident in-place windows (register form,
+     * 17 <= N <= 32) */
+    for (size_t i = 0; i < sizeof rshapes / sizeof rshapes[0]; ++i)
+        if (rshapes[i][3] == 32 && 4 * 256 * 4 / (rshapes[i][2] * 5) + 2 <= 256)
+            for (int storage = 0; storage < 2; ++storage)
+                for (int model = 0; model < 4; ++model)
+                    emulate_relay(rshapes[i][0], rshapes[i][1], rshapes[i][2], 256, 4, 32, 12, storage, 0, model,
+                                  (int)(urand() * 4));
     /* negative control: without the fallback (round 5's kernel), a non-monotone dispatch order with
      * one workgroup resident deadlocks (a tile dispatched before its scalar block waits forever) —
      * the detection above sees a deadlock when there is one */

@@ -311,6 +311,12 @@ template <int BLOCK, int POL, bool OUT, bool SEQ, int ANY = 0>
 inline void launch_relay_g(const pmenv* h, const StepParams& p, const RelayParams& r, unsigned grid,
                            hipStream_t stream) {
     const uint32_t q = h->flat_qtot;
+    if constexpr (BLOCK == 256) {
+        if (h->relay_v == 4) {                      // 16 KiB tiles: the register form of 17 <= N <= 32 only
+            step_relay_kernel<256, 4, POL, OUT, 32, 0, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q);
+            return;
+        }
+    }
     switch (h->relay_kl * 100 + h->relay_ka) {
     case 801: step_relay_kernel<BLOCK, 2, POL, OUT, 8, 1, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;
     case 1601: step_relay_kernel<BLOCK, 2, POL, OUT, 16, 1, 1, SEQ, ANY><<<grid, BLOCK, 0, stream>>>(p, r, q); break;

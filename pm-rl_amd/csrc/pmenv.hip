@@ -483,6 +483,15 @@ int pmenv_create_in(const pmenv_cfg* cfg, int device, void* state, size_t state_
         if (win > (48ll << 20) && win <= (128ll << 20)) h->relay_auto |= PMENV_FUSE_DB;
         h->one_auto &= ~h->relay_auto;
         h->flat1_auto &= ~h->relay_auto;
+        // 256 x 4 tiles (16 KiB) for the largest cache-resident in-place windows, 192-256 MiB,
+        // with the register-form scalar step of 17 <= N <= 32: config 4's 8-GPU share, 8,192 x
+        // 30 in place, 78.6 vs 81.5 us (profiles/r06/relay_stamps/geom_8192x30.err; round 4: 76.8
+        // vs 79.5 and 77.5 vs 78.1, ab_r04/relay_geom*); at 4,096 x 30 (123 MB) they lose
+        // (42.3 vs 41.1), so 256 x 2 stays below
+        const bool rows_fit4 = 4 * 256 * 4 / (c.window * 5) + 2 <= 256;
+        if ((h->relay_auto & PMENV_FUSE_INPLACE) && win > (192ll << 20) && h->relay_block == 256 &&
+            h->relay_kl == 32 && h->relay_ka == 0 && rows_fit4)
+            h->relay_v = 4;
     }
     // ---- the generic stream (advance_gen_kernel, F != 5): 2 <= F <= 16 (its halo is the two
     // chunks past a workgroup, four past F = 8), 16-B granular env windows, at most BLOCK rows

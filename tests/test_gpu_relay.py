@@ -142,15 +142,17 @@ def _capture(fn):
     return g, out
 
 
+@pytest.mark.parametrize("B,W", [(512, 20), (8192, 50)], ids=["256x2", "256x4"])
 @pytest.mark.parametrize("db", [False, True], ids=["inplace", "obs_out"])
-def test_gpu_relay_graph_capture_replays_the_relay_step(db):
+def test_gpu_relay_graph_capture_replays_the_relay_step(db, B, W):
     """A captured RELAY step stays step_relay_kernel: its epoch and parity come from the
     launch counter on the device (the ordered ticket), and the validity of its counter copy
     and halo from device words the captured invalidations clear. Eager relay steps, replays
     of a one-step graph and replays of a [reset, step, step] graph interleave, each bitwise
-    equal to an eager two-launch env driven with the same inputs."""
+    equal to an eager two-launch env driven with the same inputs. 8,192 x 30 x 50 is the
+    window AUTO gives 256 x 4 tiles (in place)."""
     from pmenv import TradingEnv, synth
-    B, N, W, T = 512, 30, 20, 16
+    N, T = 30, 16
     ser = synth.series(W + T + 8, B, N, seed=31, device=DEV)
     act = synth.actions(T + 8, B, N, seed=32, device=DEV)
     er = TradingEnv(num_envs=B, num_assets=N, window=W, device=DEV, step_impl="relay")
