@@ -679,6 +679,17 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     if (tt && tt->relay_tiles_first) rr.rot = r.scal;
     const bool out = p.obs_out != p.obs;
     const uint32_t q = h->flat_qtot;
+    // the product's geometries (256 x 2, 512 x 2, and 256 x 4 for the register form of N <= 32:
+    // launch_relay_g's own rule) take the modified launches; other geometries only the A/B ones
+    const bool prod_geom = g == 2562 || g == 5122 || (g == 2564 && h->relay_kl == 32 && h->relay_ka == 0);
+    if (mod && prod_geom) {
+        if (tt->relay_stamps && tt->relay_spin < 0 && !tt->relay_tiles_first) {   // the product's code, stamped
+            if (h->relay_block == 256) launch_relay_b<256, 0, 2>(h, p, rr, grid, out, false, stream);
+            else launch_relay_b<512, 1, 2>(h, p, rr, grid, out, false, stream);
+        } else if (h->relay_block == 256) launch_relay_b<256, 0, 1>(h, p, rr, grid, out, false, stream);
+        else launch_relay_b<512, 1, 1>(h, p, rr, grid, out, false, stream);
+        return true;
+    }
     switch (g) {
     case 1282: relay_geom<128, 2>(h, p, rr, q, grid, out, stream); return true;
     case 1284: relay_geom<128, 4>(h, p, rr, q, grid, out, stream); return true;
@@ -686,14 +697,7 @@ bool launch_relay(const pmenv* h, const StepParams& p, const RelayParams& r, uns
     case 2561: relay_geom<256, 1>(h, p, rr, q, grid, out, stream); return true;
     case 2568: relay_geom<256, 8>(h, p, rr, q, grid, out, stream); return true;
     case 5124: relay_geom<512, 4>(h, p, rr, q, grid, out, stream); return true;
-    default:
-        if (!mod) return false;
-        if (tt->relay_stamps && tt->relay_spin < 0 && !tt->relay_tiles_first) {   // the product's code, stamped
-            if (h->relay_block == 256) launch_relay_b<256, 0, 2>(h, p, rr, grid, out, false, stream);
-            else launch_relay_b<512, 1, 2>(h, p, rr, grid, out, false, stream);
-        } else if (h->relay_block == 256) launch_relay_b<256, 0, 1>(h, p, rr, grid, out, false, stream);
-        else launch_relay_b<512, 1, 1>(h, p, rr, grid, out, false, stream);
-        return true;
+    default: return false;
     }
 }
 
