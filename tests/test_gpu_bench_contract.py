@@ -38,6 +38,14 @@ def test_bench_prints_the_contract_line():
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert 0 < r["achieved"] and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     assert r["l3_resident"] is True                     # a 61 MB window sits in the Infinity Cache
+    # which kernel time the headline frac divides by: the event mean, or the unbracketed step
+    # time when the event mean exceeds it (then frac == frac_step); the event figure stays
+    assert r["frac_source"] and abs(r["frac_event"] - r["achieved_event"] / r["peak"]) < 1e-9
+    if r["kernel_avg_us"] > d["ms_per_step"] * 1e3:
+        assert r["frac_source"].startswith("ms_per_step") and r["frac"] == r["frac_step"]
+    else:
+        assert r["frac_source"].startswith("kernel_avg_us") and r["frac"] == r["frac_event"]
+    assert d["library"]["sha256"] and d["library"]["path"].endswith("libpmenv.so")
     c = d["cpu_baseline"]
     assert c["value"] > 0 and c["cores"] >= 1 and c["kind"] == "port" and c["sample"]
     assert d["parity_sample"]["obs_bit_exact"] is True
