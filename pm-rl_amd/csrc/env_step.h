@@ -1049,7 +1049,9 @@ __device__ __forceinline__ f4 flat_compose(const StepParams& p, const FlatSide& 
 // common form — the shifted source, or (storage order, ring full) its own weight dwords —
 // and only a chunk holding a row's last day or its ring slot (a divergent branch: a few
 // lanes per wave instruction) fetches the row's bar and w' (`side(xb, xwp)`, NaN bar for a
-// day outside the series) and patches those elements. k: the counter before the step.
+// day outside the series) and patches those elements. k: the counter before the step. The
+// conditions are bitwise (`&`, `|`), not short-circuit: no exec-mask branches inside the patch
+// (round 6: 8,192 x 30 relay 77.5 vs 78.5 us, the same bits; profiles/r06/relay_v4/compose_v4_*).
 template <typename Side>
 __device__ __forceinline__ f4 compose2(const StepParams& p, int kk, int32_t k, const float (&un)[4],
                                        const float (&sh)[4], Side side) {
@@ -1061,10 +1063,10 @@ __device__ __forceinline__ f4 compose2(const StepParams& p, int kk, int32_t k, c
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int f = f0 + e >= F ? f0 + e - F : f0 + e;
-        o[e] = pick(!shift_w && f == F - 1, un[e], sh[e]);
+        o[e] = pick(!shift_w & (f == F - 1), un[e], sh[e]);
     }
     const int slot_w = (int)(((uint32_t)(1 + k) - fdiv((uint32_t)(1 + k), p.div_w) * (uint32_t)W) * F + (F - 1));
-    if (kk + 3 >= WF - F || (!shift_w && (uint32_t)(slot_w - kk) <= 3u)) {   // a last day or the slot
+    if ((kk + 3 >= WF - F) | (!shift_w & ((uint32_t)(slot_w - kk) <= 3u))) {   // a last day or the slot
         f4 xb;
         float xwp;
         side(xb, xwp);
@@ -1073,10 +1075,10 @@ __device__ __forceinline__ f4 compose2(const StepParams& p, int kk, int32_t k, c
             const int pos = kk + e;
             const int f = f0 + e >= F ? f0 + e - F : f0 + e;
             const bool in_row = pos < WF;
-            const bool lastday = in_row && pos >= WF - F;
+            const bool lastday = in_row & (pos >= WF - F);
             const float bsel = pick(f == 0, xb.x, pick(f == 1, xb.y, pick(f == 2, xb.z, xb.w)));
-            o[e] = pick(lastday && f < F - 1, bsel, o[e]);
-            o[e] = pick(shift_w ? (lastday && f == F - 1) : (in_row && pos == slot_w), xwp, o[e]);
+            o[e] = pick(lastday & (f < F - 1), bsel, o[e]);
+            o[e] = pick((shift_w & lastday & (f == F - 1)) | (!shift_w & in_row & (pos == slot_w)), xwp, o[e]);
         }
     }
     return f4{o[0], o[1], o[2], o[3]};
